@@ -1,0 +1,99 @@
+# mireduce native build (gfx950 / MI355X). Replaces the reference's cuda/C/common/common.mk +
+# cuda/C/src/reduction/Makefile (sm_10/13/20) and mpi/Makefile (mpixlc / mpicc).
+#
+#   make            library, python extension, apps (reduction, reduce_xgmi, bandwidth_test, reduce_mpi)
+#   make python     only the python extension (cuda_mpi_reductions_amd/_C*.so)
+#   make asan       host-code ASan/UBSan build of the CPU-only apps + unit tests (GPU code untouched)
+#   make clean
+#
+# Variables: ARCH=gfx950  DEBUG=1  MPI_HOME=/opt/conda  SAVE_TEMPS=1 (keep .s for inspection)
+
+ARCH      ?= gfx950
+ROCM      ?= /opt/rocm
+HIPCC     ?= $(ROCM)/bin/hipcc
+HOSTCXX   ?= $(ROCM)/lib/llvm/bin/clang++
+MPI_HOME  ?= /opt/conda
+PYTHON    ?= python3
+BUILD     ?= build
+
+OPT       := $(if $(DEBUG),-O0 -g,-O3)
+CXXSTD    := -std=c++17
+INCLUDES  := -Icsrc/include -I$(ROCM)/include
+WARN      := -Wall -Wno-unused-result
+COMMON    := $(CXXSTD) $(OPT) $(WARN) -fPIC $(INCLUDES)
+HIPFLAGS  := $(COMMON) -x hip --offload-arch=$(ARCH) -munsafe-fp-atomics $(if $(SAVE_TEMPS),-save-temps=obj,)
+HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__
+LDLIBS    := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lpthread
+
+PY_INC    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_paths()['include'])")
+PYBIND_INC:= $(shell $(PYTHON) -c "import pybind11; print(pybind11.get_include())")
+PY_EXT    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
+PYEXT     := cuda_mpi_reductions_amd/_C$(PY_EXT)
+
+KERNEL_SRC  := csrc/kernels/reduce.hip csrc/kernels/fill.hip
+RUNTIME_SRC := $(wildcard csrc/runtime/*.cpp)
+COMM_SRC    := $(wildcard csrc/comm/*.cpp)
+
+KERNEL_OBJ  := $(patsubst csrc/%.hip,$(BUILD)/obj/%.o,$(KERNEL_SRC))
+RUNTIME_OBJ := $(patsubst csrc/%.cpp,$(BUILD)/obj/%.o,$(RUNTIME_SRC))
+COMM_OBJ    := $(patsubst csrc/%.cpp,$(BUILD)/obj/%.o,$(COMM_SRC))
+LIB         := $(BUILD)/lib/libmireduce.a
+
+APPS := $(BUILD)/bin/reduction $(BUILD)/bin/reduce_xgmi $(BUILD)/bin/bandwidth_test
+MPI_APP := $(BUILD)/bin/reduce_mpi
+
+.PHONY: all python apps mpi clean asan
+all: python $(EXTRA_ALL)
+
+python: $(PYEXT)
+apps: $(APPS)
+mpi: $(MPI_APP)
+
+HEADERS := $(wildcard csrc/include/mireduce/*.hpp)
+
+$(BUILD)/obj/%.o: csrc/%.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/obj/%.o: csrc/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HOSTCXX) $(HOSTFLAGS) -c $< -o $@
+
+$(LIB): $(KERNEL_OBJ) $(RUNTIME_OBJ) $(COMM_OBJ)
+	@mkdir -p $(dir $@)
+	rm -f $@
+	ar rcs $@ $^
+
+$(BUILD)/obj/python/module.o: csrc/python/module.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HOSTCXX) $(HOSTFLAGS) -I$(PY_INC) -I$(PYBIND_INC) -fvisibility=hidden -c $< -o $@
+
+$(PYEXT): $(BUILD)/obj/python/module.o $(LIB)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive \
+	    -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lrccl $(LDLIBS) -o $@
+
+$(BUILD)/bin/%: csrc/apps/%.cpp $(LIB) $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HOSTCXX) $(HOSTFLAGS) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive \
+	    -lrccl $(LDLIBS) -o $@
+
+# reduce.c parity app: plain C++ against MPICH (CPU buffers only; no HIP needed).
+$(MPI_APP): csrc/apps/reduce_mpi.cpp csrc/runtime/mt19937.cpp csrc/runtime/cli.cpp csrc/runtime/report.cpp csrc/runtime/timer.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	g++ $(CXXSTD) -O3 -Wall -Icsrc/include -DMIREDUCE_NO_HIP -I$(MPI_HOME)/include \
+	    csrc/apps/reduce_mpi.cpp csrc/runtime/mt19937.cpp csrc/runtime/cli.cpp csrc/runtime/report.cpp csrc/runtime/timer.cpp \
+	    -L$(MPI_HOME)/lib -Wl,-rpath,$(MPI_HOME)/lib -lmpi -o $@
+
+# Host sanitizers: CPU-only code paths under ASan+UBSan.
+asan: csrc/apps/reduce_mpi.cpp
+	@mkdir -p $(BUILD)/asan
+	g++ $(CXXSTD) -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -Icsrc/include -DMIREDUCE_NO_HIP \
+	    -I$(MPI_HOME)/include csrc/apps/reduce_mpi.cpp csrc/runtime/mt19937.cpp csrc/runtime/cli.cpp \
+	    csrc/runtime/report.cpp csrc/runtime/timer.cpp -L$(MPI_HOME)/lib -Wl,-rpath,$(MPI_HOME)/lib -lmpi \
+	    -o $(BUILD)/asan/reduce_mpi
+	g++ $(CXXSTD) -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -Icsrc/include -DMIREDUCE_NO_HIP \
+	    tests/native/host_unit.cpp csrc/runtime/mt19937.cpp csrc/runtime/cli.cpp csrc/runtime/report.cpp \
+	    csrc/runtime/timer.cpp -o $(BUILD)/asan/host_unit
+
+clean:
+	rm -rf $(BUILD) $(PYEXT)

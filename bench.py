@@ -1,0 +1,153 @@
+#!/usr/bin/env python3
+"""Headline benchmark: reduction bandwidth (GB/s, whole node), 1B-double SUM on N MI355X.
+
+Driver contract: ``python bench.py --gpus N --steps K --warmup W`` (N>1 under
+``torch.distributed.run``, one rank per GPU, RCCL over xGMI). One *step* is one complete global
+reduction of the 1e9-element float64 array (BASELINE.json config 4): every rank reduces its
+contiguous 1e9/N shard with the native single-pass HIP kernel (csrc/kernels/reduce.hip) into a
+1-element slot, then the slots are all-reduced with RCCL. The array is synthetic (on-device
+counter-based U[0,1) fill, untimed) and fixed in size as N grows -> strong scaling.
+
+Timing: W untimed warm-up steps; then barrier + synchronize, K timed steps, synchronize; the
+MAX elapsed time over ranks defines the measurement. Value = total bytes reduced per step x K /
+elapsed / 1e9 (GB = 1e9 B, the CUDA sample's unit, reduction.cpp:744-745). Steps are
+independent reductions, so by default step i+1's local reduce overlaps step i's all-reduce
+(RCCL runs on its own stream); ``--serial`` makes each step wait for its all-reduce.
+Every step's result is checked after timing against torch's own fp64 reduction of the shards.
+
+Reference number: 92.7729 GB/s (CUDA DOUBLE SUM, mpi/CUdata.txt:2).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+from cuda_mpi_reductions_amd._native import native, native_path
+from cuda_mpi_reductions_amd.models import CONFIGS, NORTH_STAR, ScalarReduction
+from cuda_mpi_reductions_amd.ops import KernelConfig
+from cuda_mpi_reductions_amd.parallel import dist as pdist
+
+METRIC = "reduction bandwidth (GB/s, whole node), 1B-double sum at 1/2/4/8 MI355X"
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--config", default=NORTH_STAR, choices=sorted(k for k, v in CONFIGS.items() if v.mode == "scalar"))
+    p.add_argument("--n", type=int, default=None, help="override the global element count")
+    p.add_argument("--serial", action="store_true", help="no overlap between consecutive steps")
+    p.add_argument("--block", type=int, default=0)
+    p.add_argument("--unroll", type=int, default=0)
+    p.add_argument("--wg-per-cu", type=int, default=0)
+    p.add_argument("--groups", type=int, default=0)
+    p.add_argument("--policy", choices=["nt", "default"], default="nt")
+    p.add_argument("--two-pass", action="store_true")
+    p.add_argument("--no-verify", action="store_true")
+    return p.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    native()  # fail loudly if the HIP extension is missing
+    ctx = pdist.init()
+    if args.gpus != ctx.world_size and ctx.is_root:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}; using {ctx.world_size}",
+              file=sys.stderr)
+    cfg = CONFIGS[args.config]
+    if args.n is not None:
+        from dataclasses import replace
+        cfg = replace(cfg, n_total=args.n)
+    kernel = KernelConfig(block=args.block, unroll=args.unroll, wg_per_cu=args.wg_per_cu,
+                          groups=args.groups, nontemporal=(args.policy == "nt"),
+                          single_pass=not args.two_pass)
+    wl = ScalarReduction(cfg, ctx, kernel).setup()
+    K, W = args.steps, args.warmup
+    slots = wl.new_slots(W + K)
+    dev = ctx.device
+
+    def run(first: int, count: int):
+        works = []
+        for i in range(first, first + count):
+            w = wl.step(slots[i:i + 1], async_op=True)
+            if w is not None:
+                if args.serial:
+                    w.wait()
+                else:
+                    works.append(w)
+        for w in works:
+            w.wait()
+
+    run(0, W)
+    torch.cuda.synchronize(dev)
+    pdist.barrier(ctx)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run(W, K)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    pdist.barrier(ctx)
+    elapsed = pdist.max_over_ranks(t1 - t0, ctx)
+
+    verified = None
+    if not args.no_verify:
+        ref = wl.verify(slots[-1:])
+        ok = ref["ok"]
+        # every timed slot must hold the same global value (all steps reduce the same data)
+        if K > 1:
+            s = slots[W:]
+            if cfg.op == "sum" and s.dtype.is_floating_point:
+                ok = ok and bool(((s - s[-1]).abs() <= ref["tolerance"]).all().item())
+            else:
+                ok = ok and bool((s == s[-1]).all().item())
+        verified = ok
+        if not ok and ctx.is_root:
+            print(f"[bench] VERIFICATION FAILED: {ref}", file=sys.stderr)
+
+    bytes_step = wl.bytes_total
+    gbps = bytes_step * K / elapsed / 1e9
+    ms = elapsed / K * 1e3
+    if ctx.is_root:
+        line = {
+            "metric": METRIC,
+            "value": round(gbps, 3),
+            "unit": "GB/s",
+            "n_gpus": ctx.world_size,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": round(ms, 5),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(gbps / cfg.baseline, 3) if cfg.baseline else None,
+            "dtype": "fp64" if cfg.dtype == torch.float64 else str(cfg.dtype).replace("torch.", ""),
+            "data": "synthetic (on-device counter-based U[0,1) fill, untimed; random-filled array)",
+            "config": {
+                "model": f"{cfg.name}: {cfg.description}",
+                "global_batch": wl.n_total,
+                "seq_len": 1,
+                "parallelism": f"dp{ctx.world_size}",
+                "n_total_elements": wl.n_total,
+                "bytes_per_step": bytes_step,
+                "op": cfg.op.upper(),
+                "overlap": "serial" if args.serial else "pipelined (step i+1 local reduce || step i all-reduce)",
+                "kernel_plan": wl.reducer.last_plan if wl.reducer else None,
+            },
+            "per_gpu_gbps": round(gbps / ctx.world_size, 3),
+            "baseline_value": cfg.baseline,
+            "baseline_source": cfg.baseline_source,
+            "verified": verified,
+            "native_ext": os.path.basename(native_path()),
+        }
+        print(json.dumps(line), flush=True)
+    pdist.shutdown(ctx)
+    return 0 if verified in (None, True) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

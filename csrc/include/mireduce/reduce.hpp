@@ -1,0 +1,107 @@
+// Public C++ API of the single-GPU reduction library.
+//
+// Reference parity: replaces `template<class T> void {sum,min,max}reduce(int size, int threads,
+// int blocks, int whichKernel, T* d_idata, T* d_odata)` (cuda/C/src/reduction/reduction.h:15-25)
+// and the launch-geometry planner getNumBlocksAndThreads (reduction.cpp:272-291).
+// Differences by design: 64-bit sizes (bug B4), an explicit accumulator dtype, a
+// one-launch finalisation (reference: second in-place launch, reduction.cpp:344-357), and a
+// persistent grid sized for 256 CUs instead of the fixed 64 blocks (reduction.cpp:668).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "mireduce/rng.hpp"
+#include "mireduce/types.hpp"
+
+namespace mireduce {
+
+// Tunables of the streaming kernel. 0 means "use the tuned gfx950 default".
+struct ReduceConfig {
+  int block = 0;          // threads per workgroup: 256 | 512
+  int unroll = 0;         // independent 16-byte loads in flight per thread: 2 | 4 | 8
+  int wg_per_cu = 0;      // persistent-grid occupancy target
+  int max_blocks = 0;     // hard cap on the grid (reference --maxblocks)
+  int groups = 0;         // fan-in shards of the arrival ticket (<= 64)
+  bool nontemporal = true;   // streaming loads bypass-allocate (nt) vs default policy
+  bool single_pass = true;   // last-arriver finalisation vs a second finalize launch
+};
+
+// What the planner chose (printed by the apps, recorded in JSON sidecars).
+struct LaunchPlan {
+  int block = 0;
+  int unroll = 0;
+  int grid = 0;
+  int groups = 0;
+  bool nontemporal = true;
+  bool single_pass = true;
+  uint64_t head = 0;   // scalar elements before the first 16-B aligned vector
+  uint64_t nvec = 0;   // 16-byte vectors in the streaming body
+  uint64_t tail = 0;   // scalar elements after the body
+};
+
+// Device scratch for one reduction stream: per-workgroup partials, per-group partials and the
+// arrival tickets (zeroed once; the last arriver of each launch resets them). One Workspace
+// must not be used by two concurrently running reductions.
+class Workspace {
+ public:
+  explicit Workspace(int device = -1, int max_grid = 16384);
+  ~Workspace();
+  Workspace(const Workspace&) = delete;
+  Workspace& operator=(const Workspace&) = delete;
+
+  int device() const { return device_; }
+  int num_cus() const { return num_cus_; }
+  int max_grid() const { return max_grid_; }
+  void* partials() const { return partials_; }
+  void* group_partials() const { return group_partials_; }
+  unsigned* tickets() const { return tickets_; }
+  // Re-zero the tickets (only needed after an aborted launch).
+  void reset(hipStream_t stream);
+
+ private:
+  int device_ = 0;
+  int num_cus_ = 256;
+  int max_grid_ = 0;
+  void* partials_ = nullptr;
+  void* group_partials_ = nullptr;
+  unsigned* tickets_ = nullptr;
+};
+
+constexpr int kTicketStride = 32;  // one counter per 128-byte line
+constexpr int kMaxGroups = 64;
+
+LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cfg, int num_cus,
+                       int max_grid);
+
+// Enqueue a full reduction of n elements at device pointer `in` into out[0] (device pointer,
+// element type `acc`). Asynchronous on `stream`; safe to capture into a hipGraph.
+// Throws mireduce::Error on invalid arguments.
+LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
+                  hipStream_t stream, const ReduceConfig& cfg = {});
+
+// First level only: writes plan.grid partials (element type `acc`) to `partials`.
+LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, void* partials,
+                           int max_grid, int num_cus, hipStream_t stream,
+                           const ReduceConfig& cfg = {});
+
+// Fold `count` partials on the device with one workgroup.
+void reduce_finalize(const void* partials, size_t count, DType acc, Op op, void* out,
+                     hipStream_t stream);
+
+// Element-wise combine: inout[i] = op(inout[i], other[i]) for n elements (vector mode).
+void combine_elementwise(void* inout, const void* other, size_t n, DType t, Op op,
+                         hipStream_t stream);
+
+// Fill n elements with a synthetic pattern (bit-identical with fill_host).
+void fill_device(void* ptr, size_t n, DType t, const FillSpec& spec, hipStream_t stream);
+void fill_host(void* ptr, size_t n, DType t, const FillSpec& spec);
+
+// Human-readable list of compiled kernel variants ("block x unroll x policy").
+std::vector<std::string> compiled_variants();
+
+}  // namespace mireduce

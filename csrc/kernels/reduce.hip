@@ -1,0 +1,497 @@
+// Streaming reduction kernels for gfx950 (MI355X, CDNA4).
+//
+// Capability parity: the reference's block-reduction kernels sumreduce6/minreduce6/maxreduce6
+// (cuda/C/src/reduction/reduction_kernel.cu:74-253), their 20-way launch switch per (op, T)
+// (reduction_kernel.cu:263-524) and the second in-place finalisation launch
+// (reduction.cpp:344-357). Design:
+//   * one templated kernel, op functors (ops.hpp), operator identity instead of g_idata[i] (B2);
+//   * 16-byte non-temporal vector loads, UNROLL independent loads in flight per lane, grid-stride
+//     over BLOCK*UNROLL-vector tiles with 64-bit indices (B4);
+//   * wave64 butterfly (__shfl_xor over 64 lanes) instead of the 32-lane volatile tail
+//     (reduction_kernel.cu:110-122 assumes warp lockstep — wrong on CDNA), then one LDS slot per
+//     wave;
+//   * single launch: each workgroup publishes its partial write-through (sc1), drains, and takes
+//     an agent-scope ticket; the last arriver of each of G ticket groups folds its group, and the
+//     last group folds the G group partials (threadFenceReduction_kernel.cu:116-171 idea, but
+//     with the gfx950 release/acquire forms and a sharded fan-in: one counter for 2048
+//     arrivals costs ~25 us, eight counters ~3 us).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mireduce/check.hpp"
+#include "mireduce/ops.hpp"
+#include "mireduce/reduce.hpp"
+
+namespace mireduce {
+namespace kern {
+
+template <class T> struct Vec16;
+template <> struct Vec16<int32_t> { using type = int32_t __attribute__((ext_vector_type(4))); static constexpr int N = 4; };
+template <> struct Vec16<int64_t> { using type = int64_t __attribute__((ext_vector_type(2))); static constexpr int N = 2; };
+template <> struct Vec16<float>   { using type = float __attribute__((ext_vector_type(4)));   static constexpr int N = 4; };
+template <> struct Vec16<double>  { using type = double __attribute__((ext_vector_type(2)));  static constexpr int N = 2; };
+
+template <class T> struct Bits { using type = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>; };
+
+// Write-through (sc1) store / L1-bypassing (sc1) load of one accumulator value: the
+// agent-scope relaxed atomic forms lower to global_store/load ... sc1 on gfx950.
+template <class T>
+__device__ __forceinline__ void store_sc1(T* p, T v) {
+  using B = typename Bits<T>::type;
+  B b;
+  __builtin_memcpy(&b, &v, sizeof(T));
+  __hip_atomic_store(reinterpret_cast<B*>(p), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <class T>
+__device__ __forceinline__ T load_sc1(const T* p) {
+  using B = typename Bits<T>::type;
+  B b = __hip_atomic_load(reinterpret_cast<const B*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  T v;
+  __builtin_memcpy(&v, &b, sizeof(T));
+  return v;
+}
+
+template <class OpT, class AccT>
+__device__ __forceinline__ AccT wave_reduce(AccT v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = OpT::apply(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// Result is valid in wave 0 (all lanes). Caller must barrier before reusing `lds`.
+template <class OpT, class AccT, int BLOCK>
+__device__ __forceinline__ AccT block_reduce(AccT v, AccT* lds) {
+  constexpr int kWaves = BLOCK / 64;
+  v = wave_reduce<OpT>(v);
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  if (lane == 0) lds[wave] = v;
+  __syncthreads();
+  if (wave == 0) {
+    v = lane < kWaves ? lds[lane] : OpT::template identity<AccT>();
+    v = wave_reduce<OpT>(v);
+  }
+  return v;
+}
+
+struct Args {
+  const void* body;      // 16-byte aligned start of the vector body
+  const void* head_ptr;  // original pointer (head elements live here)
+  uint64_t head;         // scalar elements before `body`
+  uint64_t nvec;         // 16-byte vectors
+  uint64_t tail;         // scalar elements after the body
+  void* partials;        // [gridDim.x] AccT
+  void* group_partials;  // [groups] AccT
+  unsigned* tickets;     // [(groups + 1) * kTicketStride]
+  void* out;             // AccT[1]
+  int groups;            // 0: two-pass mode (write partials only)
+};
+
+template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT>
+__global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
+  using V = typename Vec16<T>::type;
+  constexpr int N = Vec16<T>::N;
+  __shared__ AccT lds[BLOCK / 64];
+  __shared__ int is_last;
+
+  AccT acc[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) acc[u] = OpT::template identity<AccT>();
+
+  const V* __restrict__ vin = static_cast<const V*>(a.body);
+  constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
+  const uint64_t ntiles = a.nvec / kTile;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const V* p = vin + t * kTile + threadIdx.x;
+    V v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      if constexpr (NT) v[u] = __builtin_nontemporal_load(p + u * BLOCK);
+      else v[u] = p[u * BLOCK];
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], static_cast<AccT>(v[u][k]));
+    }
+  }
+  // Vectors past the last full tile, grid-strided.
+  for (uint64_t i = ntiles * kTile + static_cast<uint64_t>(blockIdx.x) * BLOCK + threadIdx.x;
+       i < a.nvec; i += static_cast<uint64_t>(gridDim.x) * BLOCK) {
+    const V v = vin[i];
+#pragma unroll
+    for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], static_cast<AccT>(v[k]));
+  }
+  // Unaligned head and sub-vector tail (< N elements each), folded by the last workgroup.
+  if (blockIdx.x == gridDim.x - 1) {
+    const T* hp = static_cast<const T*>(a.head_ptr);
+    if (threadIdx.x < a.head) acc[0] = OpT::apply(acc[0], static_cast<AccT>(hp[threadIdx.x]));
+    const T* tp = static_cast<const T*>(a.body) + a.nvec * N;
+    if (threadIdx.x < a.tail) acc[0] = OpT::apply(acc[0], static_cast<AccT>(tp[threadIdx.x]));
+  }
+#pragma unroll
+  for (int u = 1; u < UNROLL; ++u) acc[0] = OpT::apply(acc[0], acc[u]);
+
+  AccT v = block_reduce<OpT, AccT, BLOCK>(acc[0], lds);
+  AccT* partials = static_cast<AccT*>(a.partials);
+  if (a.groups == 0) {  // two-pass mode: the finalize kernel (kernel boundary) reads these
+    if (threadIdx.x == 0) partials[blockIdx.x] = v;
+    return;
+  }
+
+  // ---- single-pass finalisation (cdna_hip_programming.md §6 Guideline 16, sc1 form) ----
+  const unsigned G = static_cast<unsigned>(a.groups);
+  const unsigned g = blockIdx.x % G;  // group label only; correctness is placement-independent
+  if (threadIdx.x == 0) {
+    store_sc1(&partials[blockIdx.x], v);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned members = gridDim.x / G + (g < gridDim.x % G ? 1u : 0u);
+    const unsigned prev = __hip_atomic_fetch_add(&a.tickets[g * kTicketStride], 1u,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = (prev == members - 1);
+  }
+  __syncthreads();
+  if (!is_last) return;
+
+  // Last arriver of group g: fold partials g, g+G, g+2G, ... (sc1 loads: L1 never holds them).
+  AccT s = OpT::template identity<AccT>();
+  for (unsigned i = g + threadIdx.x * G; i < gridDim.x; i += BLOCK * G)
+    s = OpT::apply(s, load_sc1(&partials[i]));
+  s = block_reduce<OpT, AccT, BLOCK>(s, lds);
+  AccT* gpart = static_cast<AccT*>(a.group_partials);
+  if (threadIdx.x == 0) {
+    store_sc1(&gpart[g], s);
+    __hip_atomic_store(&a.tickets[g * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(&a.tickets[G * kTicketStride], 1u,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = (prev == G - 1);
+  }
+  __syncthreads();
+  if (!is_last) return;
+
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    AccT t = lane < static_cast<int>(G) ? load_sc1(&gpart[lane]) : OpT::template identity<AccT>();
+    t = wave_reduce<OpT>(t);
+    if (lane == 0) {
+      *static_cast<AccT*>(a.out) = t;
+      __hip_atomic_store(&a.tickets[G * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Second level of the two-pass path (and the on-device fold for reduce_finalize): one
+// workgroup folds `count` values. Launched after a kernel boundary, so plain loads are fine.
+template <class OpT, class AccT>
+__global__ __launch_bounds__(256) void finalize(const AccT* __restrict__ partials, uint64_t count,
+                                                AccT* __restrict__ out) {
+  __shared__ AccT lds[4];
+  AccT s = OpT::template identity<AccT>();
+  for (uint64_t i = threadIdx.x; i < count; i += 256) s = OpT::apply(s, partials[i]);
+  s = block_reduce<OpT, AccT, 256>(s, lds);
+  if (threadIdx.x == 0) *out = s;
+}
+
+template <class OpT, class T>
+__global__ __launch_bounds__(256) void combine(T* __restrict__ inout, const T* __restrict__ other,
+                                               uint64_t n) {
+  using V = typename Vec16<T>::type;
+  constexpr int N = Vec16<T>::N;
+  const uint64_t nvec = n / N;
+  V* vio = reinterpret_cast<V*>(inout);
+  const V* vo = reinterpret_cast<const V*>(other);
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < nvec; i += stride) {
+    V x = __builtin_nontemporal_load(vio + i);
+    const V y = __builtin_nontemporal_load(vo + i);
+#pragma unroll
+    for (int k = 0; k < N; ++k) x[k] = OpT::apply(x[k], y[k]);
+    __builtin_nontemporal_store(x, vio + i);
+  }
+  const uint64_t rem = n - nvec * N;
+  if (blockIdx.x == 0 && threadIdx.x < rem) {
+    const uint64_t i = nvec * N + threadIdx.x;
+    inout[i] = OpT::apply(inout[i], other[i]);
+  }
+}
+
+}  // namespace kern
+
+// ----------------------------------------------------------------------------------------------
+// Host-side dispatch: a table keyed by (op, dtype, acc, block, unroll, policy) replaces the
+// reference's runtime switch over 20 template instantiations per (op, T).
+// ----------------------------------------------------------------------------------------------
+namespace {
+
+using LaunchFn = void (*)(const kern::Args&, int grid, hipStream_t);
+
+template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT>
+void launch_stream(const kern::Args& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((kern::reduce_stream<OpT, T, AccT, BLOCK, UNROLL, NT>), dim3(grid), dim3(BLOCK),
+                     0, s, a);
+}
+
+constexpr int kBlocks[] = {256, 512};
+constexpr int kUnrolls[] = {2, 4, 8};
+
+int block_index(int b) { return b == 512 ? 1 : (b == 256 ? 0 : -1); }
+int unroll_index(int u) { return u == 2 ? 0 : (u == 4 ? 1 : (u == 8 ? 2 : -1)); }
+
+// combo index: (op, dtype, acc) → 0..13
+int combo_index(Op op, DType t, DType acc) {
+  const int o = static_cast<int>(op);
+  switch (t) {
+    case DType::Int32:
+      if (op == Op::Sum) return acc == DType::Int64 ? 0 : (acc == DType::Int32 ? 1 : -1);
+      return acc == DType::Int32 ? 1 + o : -1;  // 2 (min), 3 (max)
+    case DType::Int64:
+      return acc == DType::Int64 ? 4 + o : -1;  // 4..6
+    case DType::Float32:
+      if (op == Op::Sum) return acc == DType::Float64 ? 7 : (acc == DType::Float32 ? 8 : -1);
+      return acc == DType::Float32 ? 8 + o : -1;  // 9 (min), 10 (max)
+    case DType::Float64:
+      return acc == DType::Float64 ? 11 + o : -1;  // 11..13
+  }
+  return -1;
+}
+constexpr int kCombos = 14;
+
+struct Table {
+  LaunchFn fn[kCombos][2][3][2];
+};
+
+template <class OpT, class T, class AccT>
+void fill_combo(Table& tb, int c) {
+  tb.fn[c][0][0][0] = launch_stream<OpT, T, AccT, 256, 2, false>;
+  tb.fn[c][0][0][1] = launch_stream<OpT, T, AccT, 256, 2, true>;
+  tb.fn[c][0][1][0] = launch_stream<OpT, T, AccT, 256, 4, false>;
+  tb.fn[c][0][1][1] = launch_stream<OpT, T, AccT, 256, 4, true>;
+  tb.fn[c][0][2][0] = launch_stream<OpT, T, AccT, 256, 8, false>;
+  tb.fn[c][0][2][1] = launch_stream<OpT, T, AccT, 256, 8, true>;
+  tb.fn[c][1][0][0] = launch_stream<OpT, T, AccT, 512, 2, false>;
+  tb.fn[c][1][0][1] = launch_stream<OpT, T, AccT, 512, 2, true>;
+  tb.fn[c][1][1][0] = launch_stream<OpT, T, AccT, 512, 4, false>;
+  tb.fn[c][1][1][1] = launch_stream<OpT, T, AccT, 512, 4, true>;
+  tb.fn[c][1][2][0] = launch_stream<OpT, T, AccT, 512, 8, false>;
+  tb.fn[c][1][2][1] = launch_stream<OpT, T, AccT, 512, 8, true>;
+}
+
+const Table& table() {
+  static const Table tb = [] {
+    Table t{};
+    fill_combo<SumOp, int32_t, int64_t>(t, 0);
+    fill_combo<SumOp, int32_t, int32_t>(t, 1);
+    fill_combo<MinOp, int32_t, int32_t>(t, 2);
+    fill_combo<MaxOp, int32_t, int32_t>(t, 3);
+    fill_combo<SumOp, int64_t, int64_t>(t, 4);
+    fill_combo<MinOp, int64_t, int64_t>(t, 5);
+    fill_combo<MaxOp, int64_t, int64_t>(t, 6);
+    fill_combo<SumOp, float, double>(t, 7);
+    fill_combo<SumOp, float, float>(t, 8);
+    fill_combo<MinOp, float, float>(t, 9);
+    fill_combo<MaxOp, float, float>(t, 10);
+    fill_combo<SumOp, double, double>(t, 11);
+    fill_combo<MinOp, double, double>(t, 12);
+    fill_combo<MaxOp, double, double>(t, 13);
+    return t;
+  }();
+  return tb;
+}
+
+// Tuned gfx950 defaults (see docs/TUNING.md; profiles/ holds the rocprofv3 evidence).
+constexpr int kDefaultBlock = 256;
+constexpr int kDefaultUnroll = 4;
+constexpr int kDefaultWgPerCu = 8;
+constexpr int kDefaultGroups = 8;
+
+template <class OpT, class AccT>
+void launch_finalize(const void* partials, uint64_t count, void* out, hipStream_t s) {
+  hipLaunchKernelGGL((kern::finalize<OpT, AccT>), dim3(1), dim3(256), 0, s,
+                     static_cast<const AccT*>(partials), count, static_cast<AccT*>(out));
+}
+
+template <class OpT>
+void finalize_by_acc(DType acc, const void* partials, uint64_t count, void* out, hipStream_t s) {
+  switch (acc) {
+    case DType::Int32: launch_finalize<OpT, int32_t>(partials, count, out, s); break;
+    case DType::Int64: launch_finalize<OpT, int64_t>(partials, count, out, s); break;
+    case DType::Float32: launch_finalize<OpT, float>(partials, count, out, s); break;
+    case DType::Float64: launch_finalize<OpT, double>(partials, count, out, s); break;
+  }
+}
+
+template <class OpT, class T>
+void launch_combine(void* inout, const void* other, uint64_t n, hipStream_t s) {
+  constexpr int N = kern::Vec16<T>::N;
+  uint64_t blocks = (n / N + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL((kern::combine<OpT, T>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s,
+                     static_cast<T*>(inout), static_cast<const T*>(other), n);
+}
+
+template <class OpT>
+void combine_by_type(DType t, void* inout, const void* other, uint64_t n, hipStream_t s) {
+  switch (t) {
+    case DType::Int32: launch_combine<OpT, int32_t>(inout, other, n, s); break;
+    case DType::Int64: launch_combine<OpT, int64_t>(inout, other, n, s); break;
+    case DType::Float32: launch_combine<OpT, float>(inout, other, n, s); break;
+    case DType::Float64: launch_combine<OpT, double>(inout, other, n, s); break;
+  }
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------------------------------------
+
+Workspace::Workspace(int device, int max_grid) : max_grid_(max_grid) {
+  MIREDUCE_REQUIRE(max_grid >= 1, "Workspace: max_grid must be positive");
+  if (device < 0) MIREDUCE_HIP_THROW(hipGetDevice(&device));
+  device_ = device;
+  int cus = 0;
+  MIREDUCE_HIP_THROW(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  num_cus_ = cus > 0 ? cus : 256;
+  int prev = 0;
+  MIREDUCE_HIP_THROW(hipGetDevice(&prev));
+  MIREDUCE_HIP_THROW(hipSetDevice(device));
+  MIREDUCE_HIP_THROW(hipMalloc(&partials_, static_cast<size_t>(max_grid) * 8));
+  MIREDUCE_HIP_THROW(hipMalloc(&group_partials_, static_cast<size_t>(kMaxGroups) * 8));
+  const size_t tbytes = static_cast<size_t>(kMaxGroups + 1) * kTicketStride * sizeof(unsigned);
+  MIREDUCE_HIP_THROW(hipMalloc(reinterpret_cast<void**>(&tickets_), tbytes));
+  MIREDUCE_HIP_THROW(hipMemset(tickets_, 0, tbytes));
+  MIREDUCE_HIP_THROW(hipDeviceSynchronize());
+  MIREDUCE_HIP_THROW(hipSetDevice(prev));
+}
+
+Workspace::~Workspace() {
+  (void)hipFree(partials_);
+  (void)hipFree(group_partials_);
+  (void)hipFree(tickets_);
+}
+
+void Workspace::reset(hipStream_t stream) {
+  const size_t tbytes = static_cast<size_t>(kMaxGroups + 1) * kTicketStride * sizeof(unsigned);
+  MIREDUCE_HIP_THROW(hipMemsetAsync(tickets_, 0, tbytes, stream));
+}
+
+LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cfg, int num_cus,
+                       int max_grid) {
+  LaunchPlan p;
+  p.block = cfg.block ? cfg.block : kDefaultBlock;
+  p.unroll = cfg.unroll ? cfg.unroll : kDefaultUnroll;
+  p.nontemporal = cfg.nontemporal;
+  p.single_pass = cfg.single_pass;
+  MIREDUCE_REQUIRE(block_index(p.block) >= 0, "block must be 256 or 512");
+  MIREDUCE_REQUIRE(unroll_index(p.unroll) >= 0, "unroll must be 2, 4 or 8");
+  const size_t es = dtype_size(t);
+  const size_t vec = 16 / es;
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(in);
+  MIREDUCE_REQUIRE(n == 0 || addr % es == 0, "input pointer is not aligned to its element size");
+  uint64_t head = 0;
+  if (addr % 16 != 0) head = (16 - addr % 16) / es;
+  if (head > n) head = n;
+  p.head = head;
+  p.nvec = (n - head) / vec;
+  p.tail = (n - head) - p.nvec * vec;
+  const int wg_per_cu = cfg.wg_per_cu ? cfg.wg_per_cu : kDefaultWgPerCu * 256 / p.block;
+  const uint64_t tile = static_cast<uint64_t>(p.block) * p.unroll;
+  uint64_t want = (p.nvec + tile - 1) / tile;
+  const uint64_t cap = static_cast<uint64_t>(num_cus) * wg_per_cu;
+  if (want > cap) want = cap;
+  if (cfg.max_blocks > 0 && want > static_cast<uint64_t>(cfg.max_blocks)) want = cfg.max_blocks;
+  if (want > static_cast<uint64_t>(max_grid)) want = max_grid;
+  if (want < 1) want = 1;
+  p.grid = static_cast<int>(want);
+  int groups = cfg.groups ? cfg.groups : kDefaultGroups;
+  if (groups > kMaxGroups) groups = kMaxGroups;
+  if (groups > p.grid) groups = p.grid;
+  p.groups = p.single_pass ? groups : 0;
+  return p;
+}
+
+static kern::Args make_args(const void* in, const LaunchPlan& p, DType t) {
+  kern::Args a{};
+  a.head_ptr = in;
+  a.body = static_cast<const char*>(in) + p.head * dtype_size(t);
+  a.head = p.head;
+  a.nvec = p.nvec;
+  a.tail = p.tail;
+  return a;
+}
+
+LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
+                  hipStream_t stream, const ReduceConfig& cfg) {
+  const int c = combo_index(op, t, acc);
+  MIREDUCE_REQUIRE(c >= 0, "unsupported (dtype, op, accumulator) combination");
+  MIREDUCE_REQUIRE(out != nullptr, "output pointer is null");
+  LaunchPlan p = plan_reduce(in, n, t, cfg, ws.num_cus(), ws.max_grid());
+  kern::Args a = make_args(in, p, t);
+  a.partials = ws.partials();
+  a.group_partials = ws.group_partials();
+  a.tickets = ws.tickets();
+  a.out = out;
+  a.groups = p.groups;
+  const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0];
+  fn(a, p.grid, stream);
+  MIREDUCE_HIP_THROW(hipGetLastError());
+  if (!p.single_pass) reduce_finalize(ws.partials(), p.grid, acc, op, out, stream);
+  return p;
+}
+
+LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, void* partials,
+                           int max_grid, int num_cus, hipStream_t stream, const ReduceConfig& cfg) {
+  const int c = combo_index(op, t, acc);
+  MIREDUCE_REQUIRE(c >= 0, "unsupported (dtype, op, accumulator) combination");
+  ReduceConfig c2 = cfg;
+  c2.single_pass = false;
+  LaunchPlan p = plan_reduce(in, n, t, c2, num_cus, max_grid);
+  kern::Args a = make_args(in, p, t);
+  a.partials = partials;
+  a.groups = 0;
+  const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0];
+  fn(a, p.grid, stream);
+  MIREDUCE_HIP_THROW(hipGetLastError());
+  return p;
+}
+
+void reduce_finalize(const void* partials, size_t count, DType acc, Op op, void* out,
+                     hipStream_t stream) {
+  switch (op) {
+    case Op::Sum: finalize_by_acc<SumOp>(acc, partials, count, out, stream); break;
+    case Op::Min: finalize_by_acc<MinOp>(acc, partials, count, out, stream); break;
+    case Op::Max: finalize_by_acc<MaxOp>(acc, partials, count, out, stream); break;
+  }
+  MIREDUCE_HIP_THROW(hipGetLastError());
+}
+
+void combine_elementwise(void* inout, const void* other, size_t n, DType t, Op op,
+                         hipStream_t stream) {
+  if (n == 0) return;
+  MIREDUCE_REQUIRE(reinterpret_cast<uintptr_t>(inout) % 16 == 0 &&
+                       reinterpret_cast<uintptr_t>(other) % 16 == 0,
+                   "combine_elementwise needs 16-byte aligned buffers");
+  switch (op) {
+    case Op::Sum: combine_by_type<SumOp>(t, inout, other, n, stream); break;
+    case Op::Min: combine_by_type<MinOp>(t, inout, other, n, stream); break;
+    case Op::Max: combine_by_type<MaxOp>(t, inout, other, n, stream); break;
+  }
+  MIREDUCE_HIP_THROW(hipGetLastError());
+}
+
+std::vector<std::string> compiled_variants() {
+  std::vector<std::string> v;
+  for (int b : kBlocks)
+    for (int u : kUnrolls)
+      for (int nt = 0; nt < 2; ++nt)
+        v.push_back("block=" + std::to_string(b) + " unroll=" + std::to_string(u) +
+                    (nt ? " policy=nt" : " policy=default"));
+  return v;
+}
+
+}  // namespace mireduce

@@ -1,0 +1,284 @@
+// pybind11 binding: cuda_mpi_reductions_amd._C
+//
+// Exposes the native HIP kernels, the host reference reducers and MT19937 to Python. Tensors
+// cross the boundary as raw device pointers + HIP stream handles (taken from torch on the Python
+// side), so this module has no libtorch dependency and builds in seconds.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+#include <cstring>
+#include <memory>
+
+#include "mireduce/check.hpp"
+#include "mireduce/cpu_reference.hpp"
+#include "mireduce/mt19937.hpp"
+#include "mireduce/reduce.hpp"
+#include "mireduce/types.hpp"
+
+namespace py = pybind11;
+using namespace mireduce;
+
+namespace {
+
+template <class T>
+T* as_ptr(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+py::dict plan_dict(const LaunchPlan& p) {
+  py::dict d;
+  d["block"] = p.block;
+  d["unroll"] = p.unroll;
+  d["grid"] = p.grid;
+  d["groups"] = p.groups;
+  d["nontemporal"] = p.nontemporal;
+  d["single_pass"] = p.single_pass;
+  d["head"] = p.head;
+  d["nvec"] = p.nvec;
+  d["tail"] = p.tail;
+  return d;
+}
+
+ReduceConfig make_cfg(int block, int unroll, int wg_per_cu, int max_blocks, int groups,
+                      bool nontemporal, bool single_pass) {
+  ReduceConfig c;
+  c.block = block;
+  c.unroll = unroll;
+  c.wg_per_cu = wg_per_cu;
+  c.max_blocks = max_blocks;
+  c.groups = groups;
+  c.nontemporal = nontemporal;
+  c.single_pass = single_pass;
+  return c;
+}
+
+py::object acc_to_py(const void* p, DType acc) {
+  if (dtype_is_float(acc)) return py::float_(acc_as_double(p, acc));
+  return py::int_(acc_as_int64(p, acc));
+}
+
+void check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw Error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "mireduce native core: gfx950 HIP reduction kernels, host references, MT19937";
+
+  py::register_exception<Error>(m, "NativeError");
+
+  m.attr("DTYPE_INT32") = static_cast<int>(DType::Int32);
+  m.attr("DTYPE_INT64") = static_cast<int>(DType::Int64);
+  m.attr("DTYPE_FLOAT32") = static_cast<int>(DType::Float32);
+  m.attr("DTYPE_FLOAT64") = static_cast<int>(DType::Float64);
+  m.attr("OP_SUM") = static_cast<int>(Op::Sum);
+  m.attr("OP_MIN") = static_cast<int>(Op::Min);
+  m.attr("OP_MAX") = static_cast<int>(Op::Max);
+  m.attr("TICKET_STRIDE") = kTicketStride;
+
+  m.def("device_count", [] {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+
+  m.def("device_info", [](int dev) {
+    hipDeviceProp_t p;
+    check_hip(hipGetDeviceProperties(&p, dev), "hipGetDeviceProperties");
+    py::dict d;
+    d["name"] = std::string(p.name);
+    d["arch"] = std::string(p.gcnArchName);
+    d["cus"] = p.multiProcessorCount;
+    d["total_mem"] = static_cast<uint64_t>(p.totalGlobalMem);
+    d["clock_khz"] = p.clockRate;
+    d["mem_clock_khz"] = p.memoryClockRate;
+    d["mem_bus_width"] = p.memoryBusWidth;
+    d["l2_bytes"] = p.l2CacheSize;
+    d["pci_bus_id"] = p.pciBusID;
+    int rt = 0;
+    (void)hipRuntimeGetVersion(&rt);
+    d["hip_runtime"] = rt;
+    return d;
+  });
+
+  m.def("mem_info", [](int dev) {
+    int prev = 0;
+    check_hip(hipGetDevice(&prev), "hipGetDevice");
+    check_hip(hipSetDevice(dev), "hipSetDevice");
+    size_t free_b = 0, total_b = 0;
+    check_hip(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo");
+    check_hip(hipSetDevice(prev), "hipSetDevice");
+    return py::make_tuple(free_b, total_b);
+  });
+
+  py::class_<Workspace, std::shared_ptr<Workspace>>(m, "Workspace")
+      .def(py::init<int, int>(), py::arg("device") = -1, py::arg("max_grid") = 16384)
+      .def_property_readonly("device", &Workspace::device)
+      .def_property_readonly("num_cus", &Workspace::num_cus)
+      .def_property_readonly("max_grid", &Workspace::max_grid)
+      .def_property_readonly("partials_ptr", [](const Workspace& w) { return reinterpret_cast<uintptr_t>(w.partials()); })
+      .def("reset", [](Workspace& w, uintptr_t stream) { w.reset(as_stream(stream)); }, py::arg("stream") = 0);
+
+  m.def(
+      "reduce",
+      [](Workspace& ws, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out,
+         uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks, int groups,
+         bool nontemporal, bool single_pass) {
+        const LaunchPlan p = reduce(as_ptr<const void>(in), n, static_cast<DType>(dtype),
+                                    static_cast<Op>(op), static_cast<DType>(acc),
+                                    as_ptr<void>(out), ws, as_stream(stream),
+                                    make_cfg(block, unroll, wg_per_cu, max_blocks, groups,
+                                             nontemporal, single_pass));
+        return plan_dict(p);
+      },
+      py::arg("ws"), py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"),
+      py::arg("acc"), py::arg("out_ptr"), py::arg("stream") = 0, py::arg("block") = 0,
+      py::arg("unroll") = 0, py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0,
+      py::arg("groups") = 0, py::arg("nontemporal") = true, py::arg("single_pass") = true);
+
+  m.def(
+      "plan",
+      [](uintptr_t in, uint64_t n, int dtype, int num_cus, int max_grid, int block, int unroll,
+         int wg_per_cu, int max_blocks, int groups, bool nontemporal, bool single_pass) {
+        return plan_dict(plan_reduce(as_ptr<const void>(in), n, static_cast<DType>(dtype),
+                                     make_cfg(block, unroll, wg_per_cu, max_blocks, groups,
+                                              nontemporal, single_pass),
+                                     num_cus, max_grid));
+      },
+      py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("num_cus") = 256,
+      py::arg("max_grid") = 16384, py::arg("block") = 0, py::arg("unroll") = 0,
+      py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0, py::arg("groups") = 0,
+      py::arg("nontemporal") = true, py::arg("single_pass") = true);
+
+  m.def(
+      "reduce_partials",
+      [](uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t partials, int max_grid,
+         int num_cus, uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks) {
+        ReduceConfig c = make_cfg(block, unroll, wg_per_cu, max_blocks, 0, true, false);
+        return plan_dict(reduce_partials(as_ptr<const void>(in), n, static_cast<DType>(dtype),
+                                         static_cast<Op>(op), static_cast<DType>(acc),
+                                         as_ptr<void>(partials), max_grid, num_cus,
+                                         as_stream(stream), c));
+      },
+      py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"), py::arg("acc"),
+      py::arg("partials_ptr"), py::arg("max_grid"), py::arg("num_cus"), py::arg("stream") = 0,
+      py::arg("block") = 0, py::arg("unroll") = 0, py::arg("wg_per_cu") = 0,
+      py::arg("max_blocks") = 0);
+
+  m.def(
+      "reduce_finalize",
+      [](uintptr_t partials, uint64_t count, int acc, int op, uintptr_t out, uintptr_t stream) {
+        reduce_finalize(as_ptr<const void>(partials), count, static_cast<DType>(acc),
+                        static_cast<Op>(op), as_ptr<void>(out), as_stream(stream));
+      },
+      py::arg("partials_ptr"), py::arg("count"), py::arg("acc"), py::arg("op"), py::arg("out_ptr"),
+      py::arg("stream") = 0);
+
+  m.def(
+      "combine_elementwise",
+      [](uintptr_t inout, uintptr_t other, uint64_t n, int dtype, int op, uintptr_t stream) {
+        combine_elementwise(as_ptr<void>(inout), as_ptr<const void>(other), n,
+                            static_cast<DType>(dtype), static_cast<Op>(op), as_stream(stream));
+      },
+      py::arg("inout_ptr"), py::arg("other_ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"),
+      py::arg("stream") = 0);
+
+  m.def(
+      "fill_device",
+      [](uintptr_t ptr, uint64_t n, int dtype, int pattern, uint64_t seed, uint64_t offset,
+         double value, uintptr_t stream) {
+        FillSpec s;
+        s.pattern = static_cast<Pattern>(pattern);
+        s.seed = seed;
+        s.offset = offset;
+        s.value = value;
+        fill_device(as_ptr<void>(ptr), n, static_cast<DType>(dtype), s, as_stream(stream));
+      },
+      py::arg("ptr"), py::arg("n"), py::arg("dtype"), py::arg("pattern") = 0,
+      py::arg("seed") = 0x5EED, py::arg("offset") = 0, py::arg("value") = 0.0,
+      py::arg("stream") = 0);
+
+  m.def(
+      "fill_host",
+      [](uintptr_t ptr, uint64_t n, int dtype, int pattern, uint64_t seed, uint64_t offset,
+         double value) {
+        FillSpec s;
+        s.pattern = static_cast<Pattern>(pattern);
+        s.seed = seed;
+        s.offset = offset;
+        s.value = value;
+        py::gil_scoped_release nogil;
+        fill_host(as_ptr<void>(ptr), n, static_cast<DType>(dtype), s);
+      },
+      py::arg("ptr"), py::arg("n"), py::arg("dtype"), py::arg("pattern") = 0,
+      py::arg("seed") = 0x5EED, py::arg("offset") = 0, py::arg("value") = 0.0);
+
+  m.def(
+      "cpu_reduce",
+      [](uintptr_t ptr, uint64_t n, int dtype, int op, int acc, int threads) {
+        alignas(8) unsigned char out[8] = {0};
+        {
+          py::gil_scoped_release nogil;
+          cpu_reduce(as_ptr<const void>(ptr), n, static_cast<DType>(dtype), static_cast<Op>(op),
+                     static_cast<DType>(acc), out, threads);
+        }
+        return acc_to_py(out, static_cast<DType>(acc));
+      },
+      py::arg("ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"), py::arg("acc"),
+      py::arg("threads") = 0);
+
+  m.def(
+      "cpu_abs_sum",
+      [](uintptr_t ptr, uint64_t n, int dtype, int threads) {
+        py::gil_scoped_release nogil;
+        return cpu_abs_sum(as_ptr<const void>(ptr), n, static_cast<DType>(dtype), threads);
+      },
+      py::arg("ptr"), py::arg("n"), py::arg("dtype"), py::arg("threads") = 0);
+
+  m.def("sum_tolerance", [](int dtype, int acc, uint64_t n, double abs_sum) {
+    return sum_tolerance(static_cast<DType>(dtype), static_cast<DType>(acc), n, abs_sum);
+  });
+
+  m.def("default_acc", [](int dtype, int op) {
+    return static_cast<int>(default_acc(static_cast<DType>(dtype), static_cast<Op>(op)));
+  });
+
+  m.def("acc_supported", [](int dtype, int op, int acc) {
+    return acc_supported(static_cast<DType>(dtype), static_cast<Op>(op), static_cast<DType>(acc));
+  });
+
+  m.def("compiled_variants", &compiled_variants);
+
+  m.def("synchronize", [](int dev) {
+    if (dev >= 0) check_hip(hipSetDevice(dev), "hipSetDevice");
+    py::gil_scoped_release nogil;
+    check_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  }, py::arg("device") = -1);
+
+  py::class_<Mt19937>(m, "Mt19937")
+      .def(py::init<uint32_t>(), py::arg("seed") = 5489u)
+      .def("init_genrand", &Mt19937::init_genrand)
+      .def("init_by_array",
+           [](Mt19937& g, const std::vector<uint64_t>& key) { g.init_by_array(key.data(), key.size()); })
+      .def("genrand_int32", &Mt19937::genrand_int32)
+      .def("genrand_int31", &Mt19937::genrand_int31)
+      .def("genrand_real1", &Mt19937::genrand_real1)
+      .def("genrand_real2", &Mt19937::genrand_real2)
+      .def("genrand_real3", &Mt19937::genrand_real3)
+      .def("genrand_res53", &Mt19937::genrand_res53)
+      .def("fill_int32",
+           [](Mt19937& g, uintptr_t ptr, uint64_t n) {
+             int32_t* p = as_ptr<int32_t>(ptr);
+             py::gil_scoped_release nogil;
+             for (uint64_t i = 0; i < n; ++i) p[i] = static_cast<int32_t>(g.genrand_int32());
+           })
+      .def("fill_res53", [](Mt19937& g, uintptr_t ptr, uint64_t n) {
+        double* p = as_ptr<double>(ptr);
+        py::gil_scoped_release nogil;
+        for (uint64_t i = 0; i < n; ++i) p[i] = g.genrand_res53();
+      });
+}

@@ -1,0 +1,171 @@
+// Host reference reducers; see cpu_reference.hpp.
+#include "mireduce/cpu_reference.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "mireduce/check.hpp"
+#include "mireduce/ops.hpp"
+
+namespace mireduce {
+
+namespace {
+
+// Neumaier-compensated accumulator (Kahan variant that also handles |x| > |sum|).
+template <class A>
+struct Compensated {
+  A sum = 0, c = 0;
+  void add(A x) {
+    const A t = sum + x;
+    if (std::fabs(sum) >= std::fabs(x)) c += (sum - t) + x;
+    else c += (x - t) + sum;
+    sum = t;
+  }
+  A value() const { return sum + c; }
+};
+
+template <class OpT, class T, class A>
+A reduce_range(const T* p, size_t n) {
+  if constexpr (std::is_same_v<OpT, SumOp> && std::is_floating_point_v<A>) {
+    Compensated<A> k;
+    for (size_t i = 0; i < n; ++i) k.add(static_cast<A>(p[i]));
+    return k.value();
+  } else {
+    A a = OpT::template identity<A>();
+    for (size_t i = 0; i < n; ++i) a = OpT::apply(a, static_cast<A>(p[i]));
+    return a;
+  }
+}
+
+int pick_threads(size_t n, int threads) {
+  if (threads > 0) return threads;
+  if (n < (1u << 22)) return 1;
+  unsigned hc = std::thread::hardware_concurrency();
+  if (hc == 0) hc = 1;
+  return static_cast<int>(std::min<unsigned>(hc, 16));
+}
+
+template <class OpT, class T, class A>
+A reduce_parallel(const T* p, size_t n, int threads) {
+  threads = pick_threads(n, threads);
+  if (threads <= 1) return reduce_range<OpT, T, A>(p, n);
+  std::vector<A> part(threads);
+  std::vector<std::thread> pool;
+  const size_t chunk = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; ++t) {
+    pool.emplace_back([&, t] {
+      const size_t b = std::min(n, t * chunk), e = std::min(n, b + chunk);
+      part[t] = reduce_range<OpT, T, A>(p + b, e - b);
+    });
+  }
+  for (auto& th : pool) th.join();
+  return reduce_range<OpT, A, A>(part.data(), part.size());
+}
+
+template <class OpT, class T>
+void dispatch_acc(const void* in, size_t n, DType acc, void* out, int threads) {
+  const T* p = static_cast<const T*>(in);
+  switch (acc) {
+    case DType::Int32: { int32_t r = reduce_parallel<OpT, T, int32_t>(p, n, threads); std::memcpy(out, &r, 4); break; }
+    case DType::Int64: { int64_t r = reduce_parallel<OpT, T, int64_t>(p, n, threads); std::memcpy(out, &r, 8); break; }
+    case DType::Float32: { float r = reduce_parallel<OpT, T, float>(p, n, threads); std::memcpy(out, &r, 4); break; }
+    case DType::Float64: { double r = reduce_parallel<OpT, T, double>(p, n, threads); std::memcpy(out, &r, 8); break; }
+  }
+}
+
+template <class OpT>
+void dispatch_t(const void* in, size_t n, DType t, DType acc, void* out, int threads) {
+  switch (t) {
+    case DType::Int32: dispatch_acc<OpT, int32_t>(in, n, acc, out, threads); break;
+    case DType::Int64: dispatch_acc<OpT, int64_t>(in, n, acc, out, threads); break;
+    case DType::Float32: dispatch_acc<OpT, float>(in, n, acc, out, threads); break;
+    case DType::Float64: dispatch_acc<OpT, double>(in, n, acc, out, threads); break;
+  }
+}
+
+}  // namespace
+
+void cpu_reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out, int threads) {
+  MIREDUCE_REQUIRE(acc_supported(t, op, acc), "unsupported (dtype, op, accumulator) combination");
+  switch (op) {
+    case Op::Sum: dispatch_t<SumOp>(in, n, t, acc, out, threads); break;
+    case Op::Min: dispatch_t<MinOp>(in, n, t, acc, out, threads); break;
+    case Op::Max: dispatch_t<MaxOp>(in, n, t, acc, out, threads); break;
+  }
+}
+
+namespace {
+template <class T>
+double abs_sum_range(const T* p, size_t n) {
+  Compensated<double> k;
+  for (size_t i = 0; i < n; ++i) k.add(std::fabs(static_cast<double>(p[i])));
+  return k.value();
+}
+template <class T>
+double abs_sum_t(const void* in, size_t n, int threads) {
+  const T* p = static_cast<const T*>(in);
+  threads = pick_threads(n, threads);
+  if (threads <= 1) return abs_sum_range(p, n);
+  std::vector<double> part(threads);
+  std::vector<std::thread> pool;
+  const size_t chunk = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; ++t)
+    pool.emplace_back([&, t] {
+      const size_t b = std::min(n, t * chunk), e = std::min(n, b + chunk);
+      part[t] = abs_sum_range(p + b, e - b);
+    });
+  for (auto& th : pool) th.join();
+  return abs_sum_range(part.data(), part.size());
+}
+}  // namespace
+
+double cpu_abs_sum(const void* in, size_t n, DType t, int threads) {
+  switch (t) {
+    case DType::Int32: return abs_sum_t<int32_t>(in, n, threads);
+    case DType::Int64: return abs_sum_t<int64_t>(in, n, threads);
+    case DType::Float32: return abs_sum_t<float>(in, n, threads);
+    case DType::Float64: return abs_sum_t<double>(in, n, threads);
+  }
+  return 0.0;
+}
+
+void cpu_fold(const void* partials, size_t count, DType acc, Op op, void* out) {
+  cpu_reduce(partials, count, acc, op, acc, out, 1);
+}
+
+double sum_tolerance(DType t, DType acc, size_t n, double abs_sum) {
+  if (!dtype_is_float(acc)) return 0.0;
+  // Device summation is blocked: per-lane sequential runs plus a log-depth tree. A generous
+  // bound: (per-lane run + tree depth + margin) * eps(acc) * Σ|x|, floored at the reference's
+  // absolute thresholds (1e-12 for double, reduction.cpp:760; 1e-8*n for float, :765).
+  const double eps = (acc == DType::Float64) ? 1.1102230246251565e-16 : 5.960464477539063e-8;
+  const double depth = std::log2(static_cast<double>(n) + 2.0);
+  double tol = (4096.0 + 4.0 * depth) * eps * abs_sum;
+  const double floor_abs = (t == DType::Float32 && acc == DType::Float32) ? 1e-8 * static_cast<double>(n) : 1e-12;
+  return std::max(tol, floor_abs);
+}
+
+double acc_as_double(const void* p, DType acc) {
+  switch (acc) {
+    case DType::Int32: { int32_t v; std::memcpy(&v, p, 4); return v; }
+    case DType::Int64: { int64_t v; std::memcpy(&v, p, 8); return static_cast<double>(v); }
+    case DType::Float32: { float v; std::memcpy(&v, p, 4); return v; }
+    case DType::Float64: { double v; std::memcpy(&v, p, 8); return v; }
+  }
+  return 0.0;
+}
+
+int64_t acc_as_int64(const void* p, DType acc) {
+  switch (acc) {
+    case DType::Int32: { int32_t v; std::memcpy(&v, p, 4); return v; }
+    case DType::Int64: { int64_t v; std::memcpy(&v, p, 8); return v; }
+    case DType::Float32: { float v; std::memcpy(&v, p, 4); return static_cast<int64_t>(v); }
+    case DType::Float64: { double v; std::memcpy(&v, p, 8); return static_cast<int64_t>(v); }
+  }
+  return 0;
+}
+
+}  // namespace mireduce

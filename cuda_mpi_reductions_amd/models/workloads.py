@@ -1,0 +1,217 @@
+"""Benchmark workloads — the "models" of a reduction framework.
+
+The reference has no neural model; its runnable artefacts are two benchmarks:
+* ``reduction --method=... --type=...`` — one array reduced to one scalar on one GPU
+  (cuda/C/src/reduction/reduction.cpp:84-204, 661-783);
+* ``reduce`` — element-wise vector ``MPI_Reduce`` of an N/P shard per rank to root 0
+  (mpi/reduce.c:9-108).
+
+Here both semantics are workloads with a common ``setup / step / verify`` life-cycle, and the
+five BASELINE.json configs are registered in :data:`CONFIGS`. A *step* of
+:class:`ScalarReduction` is: local HIP reduction of this rank's shard into a 1-element slot,
+then an RCCL all-reduce of that slot over xGMI (SURVEY.md §5.8 "mode scalar").
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field, replace
+from typing import Optional
+
+import torch
+
+from ..ops import KernelConfig, Reducer, default_acc_dtype, fill_, sum_tolerance
+from ..parallel import dist as pdist
+
+__all__ = ["WorkloadConfig", "CONFIGS", "NORTH_STAR", "ScalarReduction", "VectorReduction",
+           "element_size"]
+
+
+@dataclass(frozen=True)
+class WorkloadConfig:
+    name: str
+    dtype: torch.dtype
+    op: str
+    n_total: Optional[int]          # None: size each GPU's shard to fill its HBM
+    mode: str = "scalar"            # "scalar" (array -> one value) | "vector" (reduce.c)
+    collective: str = "allreduce"   # "allreduce" | "reduce"
+    pattern: str = "uniform"
+    device: str = "cuda"
+    baseline: Optional[float] = None
+    baseline_unit: str = "GB/s"
+    baseline_source: str = ""
+    description: str = ""
+    hbm_fraction: float = 0.96      # share of free HBM used when n_total is None
+
+
+def element_size(dt: torch.dtype) -> int:
+    return torch.empty((), dtype=dt).element_size()
+
+
+CONFIGS: dict[str, WorkloadConfig] = {
+    "mpi_1m_int32_sum_cpu2": WorkloadConfig(
+        name="mpi_1m_int32_sum_cpu2", dtype=torch.int32, op="sum", n_total=1 << 20,
+        mode="vector", collective="reduce", pattern="fullrange", device="cpu",
+        description="1M int32 sum via MPI_Reduce on 2 CPU ranks (reduce.c plumbing, no GPU)",
+    ),
+    "gpu_256m_double_sum": WorkloadConfig(
+        name="gpu_256m_double_sum", dtype=torch.float64, op="sum", n_total=256 * 1024 * 1024,
+        baseline=92.7729, baseline_source="mpi/CUdata.txt:2 (CUDA DOUBLE SUM)",
+        description="256M double sum on one MI355X (single-GPU HIP tree-reduction kernel)",
+    ),
+    "gpu_256m_int64_min": WorkloadConfig(
+        name="gpu_256m_int64_min", dtype=torch.int64, op="min", n_total=256 * 1024 * 1024,
+        baseline=92.6014, baseline_source="mpi/CUdata.txt:3 (CUDA DOUBLE MIN; reference has no int64)",
+        description="256M int64 min-reduce on one MI355X (non-sum op path)",
+    ),
+    "xgmi_1b_double_sum": WorkloadConfig(
+        name="xgmi_1b_double_sum", dtype=torch.float64, op="sum", n_total=1_000_000_000,
+        baseline=92.7729, baseline_source="mpi/CUdata.txt:2 (CUDA DOUBLE SUM, best reference GB/s)",
+        description="1B double sum across N MI355X: local HIP reduce + RCCL all-reduce over xGMI",
+    ),
+    "hbm_fill_fp32_sum": WorkloadConfig(
+        name="hbm_fill_fp32_sum", dtype=torch.float32, op="sum", n_total=None,
+        description="fp32 sum with each GPU's shard sized to fill its 288 GB HBM (HBM saturation)",
+    ),
+}
+
+NORTH_STAR = "xgmi_1b_double_sum"
+
+
+class ScalarReduction:
+    """Global reduction of a sharded array to one value on every rank."""
+
+    def __init__(self, cfg: WorkloadConfig, ctx: pdist.DistContext,
+                 kernel: Optional[KernelConfig] = None, seed: int = 0x5EED,
+                 acc_dtype: Optional[torch.dtype] = None):
+        if cfg.mode != "scalar":
+            raise ValueError("ScalarReduction needs a scalar-mode config")
+        self.cfg = cfg
+        self.ctx = ctx
+        self.kernel = kernel or KernelConfig()
+        self.seed = seed
+        self.acc = acc_dtype or default_acc_dtype(cfg.dtype, cfg.op)
+        self.x: Optional[torch.Tensor] = None
+        self.offset = 0
+        self.count = 0
+        self.n_total = 0
+        self.reducer: Optional[Reducer] = None
+
+    # ------------------------------------------------------------------ setup
+    def _size_for_hbm(self) -> int:
+        free_b, _ = torch.cuda.mem_get_info(self.ctx.device)
+        es = element_size(self.cfg.dtype)
+        n = int(free_b * self.cfg.hbm_fraction) // es
+        return n - n % 64
+
+    def setup(self) -> "ScalarReduction":
+        dev = self.ctx.device
+        if self.cfg.n_total is None:
+            if dev.type != "cuda":
+                raise RuntimeError("HBM-fill config needs GPUs")
+            per_rank = self._size_for_hbm()
+            t = torch.tensor([per_rank], dtype=torch.int64, device=dev)
+            if self.ctx.world_size > 1:
+                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
+            per_rank = int(t.item())
+            self.n_total = per_rank * self.ctx.world_size
+            self.offset, self.count = self.ctx.rank * per_rank, per_rank
+        else:
+            self.n_total = self.cfg.n_total
+            self.offset, self.count = pdist.shard(self.n_total, self.ctx.rank, self.ctx.world_size)
+        self.x = torch.empty(self.count, dtype=self.cfg.dtype, device=dev)
+        fill_(self.x, self.cfg.pattern, seed=self.seed, offset=self.offset)
+        if dev.type == "cuda":
+            self.reducer = Reducer(dev, config=self.kernel)
+            torch.cuda.synchronize(dev)
+        return self
+
+    @property
+    def bytes_total(self) -> int:
+        return self.n_total * element_size(self.cfg.dtype)
+
+    # ------------------------------------------------------------------ step
+    def new_slots(self, k: int) -> torch.Tensor:
+        return torch.empty(k, dtype=self.acc, device=self.ctx.device)
+
+    def local(self, out: torch.Tensor) -> torch.Tensor:
+        if self.reducer is not None:
+            return self.reducer(self.x, self.cfg.op, self.acc, out=out)
+        from ..ops import reduce as host_reduce
+        return host_reduce(self.x, self.cfg.op, self.acc, out=out)
+
+    def step(self, out: torch.Tensor, async_op: bool = True):
+        """Local reduce into ``out`` (1 element) then all-reduce it across ranks. Returns the
+        collective's work handle (``None`` for a single rank)."""
+        self.local(out)
+        if self.ctx.world_size == 1:
+            return None
+        return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op)
+
+    # ------------------------------------------------------------------ verify
+    def reference(self):
+        """Independent global result: torch's own reduction of each shard, combined across
+        ranks in fp64 / int64 (parity: the CPU check of reduction.cpp:748-780)."""
+        x = self.x
+        if self.cfg.op == "sum":
+            if x.dtype.is_floating_point:
+                loc = x.sum(dtype=torch.float64).reshape(1)
+                absl = x.abs().sum(dtype=torch.float64).reshape(1)
+            else:
+                loc = x.sum(dtype=torch.int64).reshape(1)
+                absl = x.abs().sum(dtype=torch.float64).reshape(1)
+        elif self.cfg.op == "min":
+            loc, absl = x.min().reshape(1), torch.zeros(1, dtype=torch.float64, device=x.device)
+        else:
+            loc, absl = x.max().reshape(1), torch.zeros(1, dtype=torch.float64, device=x.device)
+        if self.ctx.world_size > 1:
+            torch.distributed.all_reduce(loc, op=pdist.reduce_op(self.cfg.op))
+            torch.distributed.all_reduce(absl)
+        return loc.item(), absl.item()
+
+    def verify(self, result: torch.Tensor) -> dict:
+        got = result.reshape(-1)[0].item()
+        exp, abs_sum = self.reference()
+        if self.cfg.op == "sum" and self.acc.is_floating_point:
+            tol = sum_tolerance(self.cfg.dtype, self.acc, self.n_total, abs_sum)
+            ok = math.isfinite(got) and abs(got - exp) <= tol
+        else:
+            tol = 0.0
+            ok = got == exp
+        return {"ok": bool(ok), "got": got, "expected": exp, "tolerance": tol}
+
+
+class VectorReduction:
+    """reduce.c semantics: each rank holds N/P elements; element-wise reduce to root 0 (or all)."""
+
+    def __init__(self, cfg: WorkloadConfig, ctx: pdist.DistContext, seed: int = 0x5EED):
+        self.cfg = cfg
+        self.ctx = ctx
+        self.seed = seed
+        self.count = cfg.n_total // ctx.world_size if cfg.n_total else 0
+        self.x: Optional[torch.Tensor] = None
+        self.y: Optional[torch.Tensor] = None
+
+    def setup(self, mt19937: bool = False) -> "VectorReduction":
+        dev = self.ctx.device
+        self.x = torch.empty(self.count, dtype=self.cfg.dtype, device="cpu" if mt19937 else dev)
+        if mt19937:
+            from ..ops import mt19937_fill_
+            mt19937_fill_(self.x, self.ctx.rank)
+            self.x = self.x.to(dev)
+        else:
+            # per-rank distinct streams, like reduce.c's rank-seeded generator
+            fill_(self.x, self.cfg.pattern, seed=self.seed + self.ctx.rank, offset=0)
+        self.y = torch.empty_like(self.x)
+        return self
+
+    @property
+    def bytes_total(self) -> int:
+        # reduce.c counts the full NUM_INTS*sizeof(int) regardless of P (mpi/reduce.c:79,93);
+        # we count the bytes actually reduced (count * P), which equals it when P divides N.
+        return self.count * self.ctx.world_size * element_size(self.cfg.dtype)
+
+    def step(self, async_op: bool = False):
+        self.y.copy_(self.x)
+        if self.cfg.collective == "reduce":
+            return pdist.vector_reduce(self.y, self.cfg.op, root=0, async_op=async_op)
+        return pdist.vector_allreduce(self.y, self.cfg.op, async_op=async_op)

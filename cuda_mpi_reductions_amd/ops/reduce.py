@@ -1,0 +1,211 @@
+"""Tensor-level reductions backed by the native gfx950 kernels.
+
+Reference parity: ``{sum,min,max}reduce<T>`` launch templates (cuda/C/src/reduction/reduction.h:15-25)
+and the CPU references ``sumreduceCPU``/``minreduceCPU``/``maxreduceCPU``
+(cuda/C/src/reduction/reduction.cpp:214-249).
+
+* device tensors  -> ``_C.reduce`` (one-launch single-pass kernel, csrc/kernels/reduce.hip)
+* host tensors    -> ``_C.cpu_reduce`` (compensated / exact native reference, multi-threaded)
+"""
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+
+from .._native import native
+
+__all__ = [
+    "DTYPE_CODES",
+    "OP_CODES",
+    "KernelConfig",
+    "Reducer",
+    "reduce",
+    "reduce_partials",
+    "default_acc_dtype",
+    "dtype_code",
+    "op_code",
+    "cpu_reduce",
+    "sum_tolerance",
+]
+
+DTYPE_CODES = {torch.int32: 0, torch.int64: 1, torch.float32: 2, torch.float64: 3}
+CODE_DTYPES = {v: k for k, v in DTYPE_CODES.items()}
+OP_CODES = {"sum": 0, "min": 1, "max": 2}
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    try:
+        return DTYPE_CODES[dt]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {dt}; supported: int32, int64, float32, float64") from None
+
+
+def op_code(op: str) -> int:
+    try:
+        return OP_CODES[op.lower()]
+    except KeyError:
+        raise ValueError(f"unsupported op {op!r}; supported: sum, min, max") from None
+
+
+def default_acc_dtype(dt: torch.dtype, op: str) -> torch.dtype:
+    """int32 SUM -> int64, float32 SUM -> float64, everything else keeps its dtype."""
+    return CODE_DTYPES[native().default_acc(dtype_code(dt), op_code(op))]
+
+
+@dataclass
+class KernelConfig:
+    """Tunables of the streaming kernel (0 = tuned default; see docs/TUNING.md)."""
+
+    block: int = 0
+    unroll: int = 0
+    wg_per_cu: int = 0
+    max_blocks: int = 0
+    groups: int = 0
+    nontemporal: bool = True
+    single_pass: bool = True
+
+    def kwargs(self) -> dict:
+        return dict(
+            block=self.block,
+            unroll=self.unroll,
+            wg_per_cu=self.wg_per_cu,
+            max_blocks=self.max_blocks,
+            groups=self.groups,
+            nontemporal=self.nontemporal,
+            single_pass=self.single_pass,
+        )
+
+
+def _stream_handle(device: torch.device, stream: Optional[torch.cuda.Stream]) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return int(s.cuda_stream)
+
+
+class Reducer:
+    """A per-device reduction engine owning its scratch workspace.
+
+    One ``Reducer`` must not run two reductions concurrently on different streams (the
+    workspace's arrival tickets are shared); create one per stream for concurrent use.
+    """
+
+    def __init__(self, device=None, max_grid: int = 16384, config: Optional[KernelConfig] = None):
+        C = native()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("Reducer needs a GPU device")
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", idx)
+        self.ws = C.Workspace(idx, max_grid)
+        self.config = config or KernelConfig()
+        self.last_plan: dict = {}
+
+    @property
+    def num_cus(self) -> int:
+        return self.ws.num_cus
+
+    def __call__(
+        self,
+        x: torch.Tensor,
+        op: str = "sum",
+        acc_dtype: Optional[torch.dtype] = None,
+        out: Optional[torch.Tensor] = None,
+        stream: Optional[torch.cuda.Stream] = None,
+        config: Optional[KernelConfig] = None,
+    ) -> torch.Tensor:
+        C = native()
+        if x.device != self.device:
+            raise ValueError(f"tensor on {x.device}, reducer on {self.device}")
+        if not x.is_contiguous():
+            x = x.contiguous()
+        acc = acc_dtype or default_acc_dtype(x.dtype, op)
+        if out is None:
+            out = torch.empty(1, dtype=acc, device=self.device)
+        elif out.dtype != acc or out.device != self.device or out.numel() < 1:
+            raise ValueError("out must be a 1+ element tensor of the accumulator dtype on the same device")
+        cfg = config or self.config
+        self.last_plan = C.reduce(
+            self.ws,
+            x.data_ptr(),
+            x.numel(),
+            dtype_code(x.dtype),
+            op_code(op),
+            dtype_code(acc),
+            out.data_ptr(),
+            _stream_handle(self.device, stream),
+            **cfg.kwargs(),
+        )
+        return out
+
+
+_reducers: dict = {}
+_lock = threading.Lock()
+
+
+def _default_reducer(device: torch.device) -> Reducer:
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    with _lock:
+        r = _reducers.get(key)
+        if r is None:
+            r = Reducer(device)
+            _reducers[key] = r
+        return r
+
+
+def cpu_reduce(x: torch.Tensor, op: str = "sum", acc_dtype: Optional[torch.dtype] = None, threads: int = 0):
+    """Native host reference: returns a Python int/float (exact ints, compensated floats)."""
+    C = native()
+    if x.device.type != "cpu":
+        raise ValueError("cpu_reduce needs a host tensor")
+    x = x.contiguous()
+    acc = acc_dtype or default_acc_dtype(x.dtype, op)
+    return C.cpu_reduce(x.data_ptr(), x.numel(), dtype_code(x.dtype), op_code(op), dtype_code(acc), threads)
+
+
+def reduce(
+    x: torch.Tensor,
+    op: str = "sum",
+    acc_dtype: Optional[torch.dtype] = None,
+    out: Optional[torch.Tensor] = None,
+    config: Optional[KernelConfig] = None,
+) -> torch.Tensor:
+    """Reduce all elements of ``x`` with ``op`` into a 1-element tensor of the accumulator dtype.
+
+    Device tensors run the native HIP kernel on the current stream (asynchronous). Host tensors
+    run the native CPU reference.
+    """
+    if x.device.type == "cuda":
+        return _default_reducer(x.device)(x, op, acc_dtype, out, config=config)
+    acc = acc_dtype or default_acc_dtype(x.dtype, op)
+    val = cpu_reduce(x, op, acc)
+    res = torch.tensor([val], dtype=acc)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+def reduce_partials(x: torch.Tensor, op: str = "sum", acc_dtype=None, max_grid: int = 16384,
+                    config: Optional[KernelConfig] = None):
+    """First level only (the reference's --cpufinal path): returns the per-workgroup partials."""
+    C = native()
+    if x.device.type != "cuda":
+        raise ValueError("reduce_partials needs a device tensor")
+    acc = acc_dtype or default_acc_dtype(x.dtype, op)
+    cfg = config or KernelConfig()
+    parts = torch.empty(max_grid, dtype=acc, device=x.device)
+    info = torch.cuda.get_device_properties(x.device)
+    plan = C.reduce_partials(
+        x.data_ptr(), x.numel(), dtype_code(x.dtype), op_code(op), dtype_code(acc), parts.data_ptr(),
+        max_grid, info.multi_processor_count, _stream_handle(x.device, None),
+        block=cfg.block, unroll=cfg.unroll, wg_per_cu=cfg.wg_per_cu, max_blocks=cfg.max_blocks,
+    )
+    return parts[: plan["grid"]], plan
+
+
+def sum_tolerance(dtype: torch.dtype, acc: torch.dtype, n: int, abs_sum: float) -> float:
+    return native().sum_tolerance(dtype_code(dtype), dtype_code(acc), n, abs_sum)

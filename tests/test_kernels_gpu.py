@@ -1,0 +1,197 @@
+"""Numerics of the native HIP reduction kernels vs plain PyTorch fp64/int64 references.
+
+Closes the reference's test gaps: every (op x dtype x accumulator), sizes
+around wavefront/tile/grid boundaries, misaligned base pointers (the min/max OOB bug B1/B2 of
+reduction_kernel.cu:140,157), >2^31 elements (bug B4), every compiled kernel variant, the
+two-kernel path as an oracle for the single-pass path, and back-to-back launches (ticket reset).
+"""
+import math
+
+import pytest
+import torch
+
+from cuda_mpi_reductions_amd._native import native
+from cuda_mpi_reductions_amd.ops import KernelConfig, Reducer, fill_, reduce, reduce_partials, sum_tolerance
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+COMBOS = [
+    (torch.int32, "sum", torch.int64),
+    (torch.int32, "sum", torch.int32),
+    (torch.int32, "min", torch.int32),
+    (torch.int32, "max", torch.int32),
+    (torch.int64, "sum", torch.int64),
+    (torch.int64, "min", torch.int64),
+    (torch.int64, "max", torch.int64),
+    (torch.float32, "sum", torch.float64),
+    (torch.float32, "sum", torch.float32),
+    (torch.float32, "min", torch.float32),
+    (torch.float32, "max", torch.float32),
+    (torch.float64, "sum", torch.float64),
+    (torch.float64, "min", torch.float64),
+    (torch.float64, "max", torch.float64),
+]
+SIZES = [1, 2, 3, 63, 64, 65, 255, 256, 257, 1023, 1024, 1025, 4097, 65537, 1_000_003, (1 << 22) + 7]
+
+
+def expected(x: torch.Tensor, op: str, acc: torch.dtype):
+    if op == "sum":
+        if acc.is_floating_point:
+            return x.double().sum().item(), x.double().abs().sum().item()
+        if acc == torch.int32:  # wraps modulo 2^32
+            s = x.long().sum().item() & 0xFFFFFFFF
+            return (s - (1 << 32) if s >= (1 << 31) else s), 0.0
+        return x.long().sum().item(), 0.0
+    if op == "min":
+        return x.min().item(), 0.0
+    return x.max().item(), 0.0
+
+
+def check(got, x, op, acc, n):
+    exp, abs_sum = expected(x, op, acc)
+    if op == "sum" and acc.is_floating_point:
+        tol = sum_tolerance(x.dtype, acc, n, abs_sum)
+        assert abs(got - exp) <= tol, (got, exp, tol)
+    else:
+        assert got == exp, (got, exp)
+
+
+@pytest.mark.parametrize("dt,op,acc", COMBOS, ids=lambda v: str(v).replace("torch.", ""))
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("misalign", [0, 1])
+def test_all_combos_sizes(dt, op, acc, n, misalign):
+    base = torch.empty(n + misalign, dtype=dt, device=DEV)
+    fill_(base, "fullrange" if not dt.is_floating_point else "uniform", seed=n * 7 + misalign)
+    x = base[misalign:]
+    got = reduce(x, op, acc).item()
+    check(got, x, op, acc, n)
+
+
+def test_empty_gives_identity():
+    for dt, op, acc in COMBOS:
+        x = torch.empty(0, dtype=dt, device=DEV)
+        got = reduce(x, op, acc).item()
+        if op == "sum":
+            assert got == 0
+        elif op == "min":
+            assert got == (math.inf if acc.is_floating_point else torch.iinfo(acc).max)
+        else:
+            assert got == (-math.inf if acc.is_floating_point else torch.iinfo(acc).min)
+
+
+@pytest.mark.parametrize("block", [256, 512])
+@pytest.mark.parametrize("unroll", [2, 4, 8])
+@pytest.mark.parametrize("nt", [True, False])
+@pytest.mark.parametrize("single_pass", [True, False])
+def test_every_variant(block, unroll, nt, single_pass):
+    n = 3_000_017
+    x = torch.empty(n, dtype=torch.float64, device=DEV)
+    fill_(x, "uniform", seed=11)
+    r = Reducer(DEV, config=KernelConfig(block=block, unroll=unroll, nontemporal=nt, single_pass=single_pass))
+    for op in ("sum", "min", "max"):
+        check(r(x, op).item(), x, op, torch.float64, n)
+    xi = torch.empty(n, dtype=torch.int64, device=DEV)
+    fill_(xi, "fullrange", seed=12)
+    for op in ("min", "max"):
+        check(r(xi, op).item(), xi, op, torch.int64, n)
+
+
+@pytest.mark.parametrize("groups", [1, 2, 7, 8, 64])
+@pytest.mark.parametrize("max_blocks", [1, 3, 64, 0])
+def test_ticket_groups_and_grid(groups, max_blocks):
+    n = 5_000_011
+    x = torch.empty(n, dtype=torch.int32, device=DEV)
+    fill_(x, "fullrange", seed=3)
+    r = Reducer(DEV, config=KernelConfig(groups=groups, max_blocks=max_blocks))
+    check(r(x, "sum").item(), x, "sum", torch.int64, n)
+    check(r(x, "max").item(), x, "max", torch.int32, n)
+
+
+def test_back_to_back_launches_reset_tickets():
+    # 300 launches queued without host sync, each on different data: a stale ticket or a missing
+    # reset would make some launch finalise early/never.
+    n = 2_000_003
+    r = Reducer(DEV)
+    xs = [torch.empty(n, dtype=torch.int64, device=DEV) for _ in range(3)]
+    for i, x in enumerate(xs):
+        fill_(x, "fullrange", seed=100 + i)
+    outs = torch.empty(300, dtype=torch.int64, device=DEV)
+    for i in range(300):
+        r(xs[i % 3], "sum", out=outs[i:i + 1])
+    torch.cuda.synchronize()
+    exp = [x.sum().item() for x in xs]
+    got = outs.tolist()
+    assert all(got[i] == exp[i % 3] for i in range(300))
+
+
+def test_single_vs_two_pass_int_bitwise():
+    n = 7_000_001
+    x = torch.empty(n, dtype=torch.int64, device=DEV)
+    fill_(x, "fullrange", seed=5)
+    a = Reducer(DEV, config=KernelConfig(single_pass=True))(x, "sum").item()
+    b = Reducer(DEV, config=KernelConfig(single_pass=False))(x, "sum").item()
+    assert a == b == x.sum().item()
+
+
+def test_partials_and_host_fold():
+    C = native()
+    n = 4_000_037
+    x = torch.empty(n, dtype=torch.float64, device=DEV)
+    fill_(x, "uniform", seed=9)
+    for op in ("sum", "min", "max"):
+        parts, plan = reduce_partials(x, op)
+        host = parts.cpu()
+        folded = C.cpu_reduce(host.data_ptr(), host.numel(), 3, {"sum": 0, "min": 1, "max": 2}[op], 3, 1)
+        check(folded, x, op, torch.float64, n)
+
+
+@pytest.mark.parametrize("dt", [torch.int32, torch.int64, torch.float32, torch.float64])
+@pytest.mark.parametrize("pattern", ["uniform", "smallint", "fullrange", "iotamod", "constant"])
+def test_device_fill_matches_host_fill(dt, pattern):
+    n = 100_003
+    d = torch.empty(n, dtype=dt, device=DEV)
+    h = torch.empty(n, dtype=dt)
+    fill_(d, pattern, seed=42, offset=12345, value=3.0)
+    fill_(h, pattern, seed=42, offset=12345, value=3.0)
+    assert torch.equal(d.cpu(), h)
+
+
+@pytest.mark.parametrize("op", ["sum", "min", "max"])
+def test_combine_elementwise(op):
+    C = native()
+    n = 1_000_005
+    a = torch.empty(n, dtype=torch.float64, device=DEV)
+    b = torch.empty(n, dtype=torch.float64, device=DEV)
+    fill_(a, "uniform", seed=1)
+    fill_(b, "uniform", seed=2)
+    ref = {"sum": a + b, "min": torch.minimum(a, b), "max": torch.maximum(a, b)}[op]
+    C.combine_elementwise(a.data_ptr(), b.data_ptr(), n, 3, {"sum": 0, "min": 1, "max": 2}[op],
+                          torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(a, ref)
+
+
+def test_more_than_2_pow_31_elements():
+    # 2^31 + 17 int32 (8 GiB): 64-bit indexing end to end (reference: int size / unsigned bytes).
+    n = (1 << 31) + 17
+    x = torch.empty(n, dtype=torch.int32, device=DEV)
+    fill_(x, "iotamod")
+    got = reduce(x, "sum").item()
+    full, rem = divmod(n, 1024)
+    exp = full * (1023 * 1024 // 2) + rem * (rem - 1) // 2
+    assert got == exp
+    assert reduce(x, "max").item() == 1023
+    assert reduce(x, "min").item() == 0
+    del x
+    torch.cuda.empty_cache()
+
+
+def test_nan_and_inf_semantics():
+    x = torch.tensor([1.0, float("nan"), -3.0, 2.0], dtype=torch.float64, device=DEV)
+    # MIN/MAX ignore NaN (IEEE minNum/maxNum, same as std::fmin on the host); SUM propagates it.
+    assert reduce(x, "min").item() == -3.0
+    assert reduce(x, "max").item() == 2.0
+    assert math.isnan(reduce(x, "sum").item())
+    y = torch.tensor([1.0, float("inf"), -2.0], dtype=torch.float32, device=DEV)
+    assert reduce(y, "max").item() == math.inf

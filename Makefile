@@ -30,7 +30,7 @@ PYBIND_INC:= $(shell $(PYTHON) -c "import pybind11; print(pybind11.get_include()
 PY_EXT    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
 PYEXT     := cuda_mpi_reductions_amd/_C$(PY_EXT)
 
-KERNEL_SRC  := csrc/kernels/reduce.hip csrc/kernels/fill.hip
+KERNEL_SRC  := $(wildcard csrc/kernels/*.hip)
 RUNTIME_SRC := $(wildcard csrc/runtime/*.cpp)
 COMM_SRC    := $(wildcard csrc/comm/*.cpp)
 
@@ -38,12 +38,13 @@ KERNEL_OBJ  := $(patsubst csrc/%.hip,$(BUILD)/obj/%.o,$(KERNEL_SRC))
 RUNTIME_OBJ := $(patsubst csrc/%.cpp,$(BUILD)/obj/%.o,$(RUNTIME_SRC))
 COMM_OBJ    := $(patsubst csrc/%.cpp,$(BUILD)/obj/%.o,$(COMM_SRC))
 LIB         := $(BUILD)/lib/libmireduce.a
+COMMLIB     := $(BUILD)/lib/libmireduce_comm.a
 
 APPS := $(BUILD)/bin/reduction $(BUILD)/bin/reduce_xgmi $(BUILD)/bin/bandwidth_test
 MPI_APP := $(BUILD)/bin/reduce_mpi
 
 .PHONY: all python apps mpi clean asan
-all: python $(EXTRA_ALL)
+all: python apps mpi
 
 python: $(PYEXT)
 apps: $(APPS)
@@ -59,7 +60,13 @@ $(BUILD)/obj/%.o: csrc/%.cpp $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HOSTCXX) $(HOSTFLAGS) -c $< -o $@
 
-$(LIB): $(KERNEL_OBJ) $(RUNTIME_OBJ) $(COMM_OBJ)
+# core: kernels + host runtime (no RCCL: the python extension shares a process with torch's RCCL)
+$(LIB): $(KERNEL_OBJ) $(RUNTIME_OBJ)
+	@mkdir -p $(dir $@)
+	rm -f $@
+	ar rcs $@ $^
+
+$(COMMLIB): $(COMM_OBJ)
 	@mkdir -p $(dir $@)
 	rm -f $@
 	ar rcs $@ $^
@@ -70,30 +77,28 @@ $(BUILD)/obj/python/module.o: csrc/python/module.cpp $(HEADERS)
 
 $(PYEXT): $(BUILD)/obj/python/module.o $(LIB)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive \
-	    -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lrccl $(LDLIBS) -o $@
+	    $(LDLIBS) -o $@
 
-$(BUILD)/bin/%: csrc/apps/%.cpp $(LIB) $(HEADERS)
+$(BUILD)/bin/%: csrc/apps/%.cpp $(LIB) $(COMMLIB) $(HEADERS)
 	@mkdir -p $(dir $@)
-	$(HOSTCXX) $(HOSTFLAGS) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive \
-	    -lrccl $(LDLIBS) -o $@
+	$(HOSTCXX) $(HOSTFLAGS) $< -Wl,--whole-archive $(LIB) $(COMMLIB) -Wl,--no-whole-archive \
+	    -L$(ROCM)/lib -lrccl $(LDLIBS) -o $@
 
 # reduce.c parity app: plain C++ against MPICH (CPU buffers only; no HIP needed).
-$(MPI_APP): csrc/apps/reduce_mpi.cpp csrc/runtime/mt19937.cpp csrc/runtime/cli.cpp csrc/runtime/report.cpp csrc/runtime/timer.cpp $(HEADERS)
+MPI_SRCS := csrc/apps/reduce_mpi.cpp csrc/runtime/mt19937.cpp csrc/runtime/cli.cpp csrc/runtime/report.cpp csrc/runtime/timer.cpp csrc/runtime/types.cpp
+$(MPI_APP): $(MPI_SRCS) $(HEADERS)
 	@mkdir -p $(dir $@)
 	g++ $(CXXSTD) -O3 -Wall -Icsrc/include -DMIREDUCE_NO_HIP -I$(MPI_HOME)/include \
-	    csrc/apps/reduce_mpi.cpp csrc/runtime/mt19937.cpp csrc/runtime/cli.cpp csrc/runtime/report.cpp csrc/runtime/timer.cpp \
-	    -L$(MPI_HOME)/lib -Wl,-rpath,$(MPI_HOME)/lib -lmpi -o $@
+	    $(MPI_SRCS) -static-libstdc++ -static-libgcc $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,$(MPI_HOME)/lib -o $@
 
 # Host sanitizers: CPU-only code paths under ASan+UBSan.
 asan: csrc/apps/reduce_mpi.cpp
 	@mkdir -p $(BUILD)/asan
 	g++ $(CXXSTD) -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -Icsrc/include -DMIREDUCE_NO_HIP \
-	    -I$(MPI_HOME)/include csrc/apps/reduce_mpi.cpp csrc/runtime/mt19937.cpp csrc/runtime/cli.cpp \
-	    csrc/runtime/report.cpp csrc/runtime/timer.cpp -L$(MPI_HOME)/lib -Wl,-rpath,$(MPI_HOME)/lib -lmpi \
+	    -I$(MPI_HOME)/include $(MPI_SRCS) -static-libstdc++ -static-libgcc $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,$(MPI_HOME)/lib \
 	    -o $(BUILD)/asan/reduce_mpi
 	g++ $(CXXSTD) -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -Icsrc/include -DMIREDUCE_NO_HIP \
-	    tests/native/host_unit.cpp csrc/runtime/mt19937.cpp csrc/runtime/cli.cpp csrc/runtime/report.cpp \
-	    csrc/runtime/timer.cpp -o $(BUILD)/asan/host_unit
+	    tests/native/host_unit.cpp $(filter-out csrc/apps/reduce_mpi.cpp,$(MPI_SRCS)) -o $(BUILD)/asan/host_unit
 
 clean:
 	rm -rf $(BUILD) $(PYEXT)

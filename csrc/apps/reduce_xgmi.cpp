@@ -1,0 +1,428 @@
+// reduce_xgmi — cross-GPU reduction benchmark: one process per MI355X, RCCL over xGMI.
+//
+// Two semantics:
+//   --mode=vector  reduce.c on GPUs: each rank holds N/P elements, element-wise ncclReduce to
+//                  root 0 (or ncclAllReduce), {MAX,MIN,SUM} x {INT,DOUBLE} x RETRY_COUNT, output
+//                  byte-compatible with mpi/reduce.c:67-69,80-82,94-96 (GB = 2^30 B of total data).
+//   --mode=scalar  the north star: every rank reduces its contiguous shard of a global array with
+//                  the single-pass HIP kernel, then a 1-element ncclAllReduce — the hybrid
+//                  local-reduce + scalar MPI_Reduce of the vendored simpleMPI
+//                  (cuda/C/src/simpleMPI/simpleMPI.cpp:92-98) on RCCL.
+// Launch: torchrun / mpirun / srun (see comm.hpp); rank r uses GPU LOCAL_RANK % device_count.
+// Timing: host barrier, then `--iters` back-to-back iterations on one stream (optionally replayed
+// from a hipGraph, --graph), stream drained with an RCCL async-error watchdog; the MAX over
+// ranks of the per-iteration time is reported (fixes reduce.c's root-only, barrier-less rdtsc,
+// bug B8). Verification: vector mode checks sampled indices against the host-combined inputs of
+// all ranks; scalar mode checks the all-reduced value against the host fold of every rank's
+// local result and each local result against the two-launch oracle path.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cinttypes>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "mireduce/check.hpp"
+#include "mireduce/cli.hpp"
+#include "mireduce/comm.hpp"
+#include "mireduce/cpu_reference.hpp"
+#include "mireduce/device.hpp"
+#include "mireduce/mt19937.hpp"
+#include "mireduce/reduce.hpp"
+#include "mireduce/report.hpp"
+#include "mireduce/timer.hpp"
+
+using namespace mireduce;
+
+namespace {
+
+constexpr uint64_t kNumInts = 512ull * 1024 * 1024;     // mpi/constants.h:1
+constexpr uint64_t kNumDoubles = 256ull * 1024 * 1024;  // mpi/constants.h:2
+
+const std::set<std::string> kKnown = {"mode", "collective", "dtypes", "ops", "ints", "doubles", "longs", "floats",
+                                      "n", "retries", "warmup", "iters", "root", "json", "graph", "mt19937",
+                                      "noverify", "seed", "help", "unroll", "block", "wg-per-cu", "policy",
+                                      "units", "timeout"};
+
+struct Ctx {
+  LaunchEnv env;
+  int device = 0;
+  std::unique_ptr<TcpBootstrap> boot;
+  std::unique_ptr<RcclComm> comm;
+  hipStream_t stream = nullptr;
+  int retries = 5, warmup = 1, iters = 10, root = 0;
+  std::string mode = "vector", collective, json;
+  bool graph = false, verify = true, mt = false;
+  uint64_t seed = 0x5EED;
+  double timeout_s = 300;
+  bool units_gb = false;  // gnuplot column in 2^30 (reduce.c) unless --units=gb
+  ReduceConfig kcfg;
+};
+
+uint64_t global_count(DType t, uint64_t ints, uint64_t longs, uint64_t floats, uint64_t doubles) {
+  switch (t) {
+    case DType::Int32: return ints;
+    case DType::Int64: return longs;
+    case DType::Float32: return floats;
+    case DType::Float64: return doubles;
+  }
+  return 0;
+}
+
+// Time `iters` repetitions of `body` on the stream (optionally as one hipGraph replay).
+template <class F>
+double time_iters(Ctx& c, F&& body) {
+  hipGraphExec_t exec = nullptr;
+  hipGraph_t graph = nullptr;
+  if (c.graph) {
+    HIP_CHECK(hipStreamBeginCapture(c.stream, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < c.iters; ++i) body();
+    HIP_CHECK(hipStreamEndCapture(c.stream, &graph));
+    HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    HIP_CHECK(hipGraphLaunch(exec, c.stream));  // upload / first replay outside the clock
+    c.comm->synchronize(c.stream, c.timeout_s);
+  }
+  c.boot->barrier();
+  const double t0 = StopWatch::now_s();
+  if (c.graph) HIP_CHECK(hipGraphLaunch(exec, c.stream));
+  else
+    for (int i = 0; i < c.iters; ++i) body();
+  c.comm->synchronize(c.stream, c.timeout_s);
+  const double dt = (StopWatch::now_s() - t0) / c.iters;
+  if (exec) HIP_CHECK(hipGraphExecDestroy(exec));
+  if (graph) HIP_CHECK(hipGraphDestroy(graph));
+  return c.boot->max_double(dt);
+}
+
+void emit(Ctx& c, DType t, Op o, double bytes_total, double dt, Json extra) {
+  const double gib = bytes_total / dt / kGiB;
+  const double gb = bytes_total / dt / kGB;
+  if (c.env.rank == c.root) {
+    std::printf("%s\n", gnuplot_line(dtype_gnuplot_name(t), op_name(o), c.env.world, c.units_gb ? gb : gib).c_str());
+    std::fflush(stdout);
+    if (!c.json.empty()) {
+      extra.set("app", "reduce_xgmi").set("mode", c.mode).set("collective", c.collective)
+          .set("dtype", dtype_gnuplot_name(t)).set("op", op_name(o)).set("ranks", c.env.world)
+          .set("bytes_total", bytes_total).set("seconds", dt).set("gib_per_s", gib).set("gb_per_s", gb)
+          .set("iters", c.iters).set("graph", c.graph).set("rccl_version", RcclComm::version())
+          .set("launcher", c.env.launcher);
+      extra.write_file(c.json);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ vector mode
+template <class T>
+bool check_samples(Ctx& c, Op o, const void* d_send, const void* d_recv, uint64_t count) {
+  const int kS = 16;
+  std::vector<uint64_t> idx(kS);
+  for (int s = 0; s < kS; ++s) idx[s] = (static_cast<uint64_t>(s) * 2654435761ull + 7) % count;
+  std::vector<T> mine(kS), got(kS), all(static_cast<size_t>(kS) * c.env.world);
+  for (int s = 0; s < kS; ++s) {
+    HIP_CHECK(hipMemcpy(&mine[s], static_cast<const T*>(d_send) + idx[s], sizeof(T), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(&got[s], static_cast<const T*>(d_recv) + idx[s], sizeof(T), hipMemcpyDeviceToHost));
+  }
+  c.boot->allgather(mine.data(), all.data(), kS * sizeof(T));
+  const bool holder = c.collective == "allreduce" || c.env.rank == c.root;
+  int ok = 1;
+  if (holder) {
+    for (int s = 0; s < kS; ++s) {
+      T e = all[s];
+      for (int r = 1; r < c.env.world; ++r) {
+        const T v = all[static_cast<size_t>(r) * kS + s];
+        if (o == Op::Sum) e = wrap_add(e, v);
+        else if (o == Op::Min) e = MinOp::apply(e, v);
+        else e = MaxOp::apply(e, v);
+      }
+      if constexpr (std::is_floating_point_v<T>) {
+        const double tol = o == Op::Sum ? 1e-12 * c.env.world * (std::fabs(static_cast<double>(e)) + 1.0) : 0.0;
+        if (std::fabs(static_cast<double>(e) - static_cast<double>(got[s])) > tol) ok = 0;
+      } else if (e != got[s]) {
+        ok = 0;
+      }
+    }
+  }
+  std::vector<int> oks(c.env.world);
+  c.boot->allgather(&ok, oks.data(), sizeof ok);
+  return std::all_of(oks.begin(), oks.end(), [](int v) { return v != 0; });
+}
+
+bool run_vector(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>& ops,
+                const std::vector<uint64_t>& counts) {
+  struct B {
+    DType t;
+    uint64_t count;
+    DeviceBuffer send, recv;
+  };
+  std::vector<B> bufs;
+  for (size_t k = 0; k < dtypes.size(); ++k) {
+    const DType t = dtypes[k];
+    B b{t, std::max<uint64_t>(1, counts[k] / c.env.world), {}, {}};
+    b.send.allocate(b.count * dtype_size(t));
+    b.recv.allocate(b.count * dtype_size(t));
+    if (c.mt) {  // reduce.c's exact data: MT19937 seeded {rank,0x123,...}, host-generated, H2D
+      Mt19937 g;
+      const uint64_t seeds[6] = {static_cast<uint64_t>(c.env.rank), 0x123, 0x234, 0x345, 0x456, 0x789};
+      g.init_by_array(seeds, 6);
+      std::vector<unsigned char> h(b.count * dtype_size(t));
+      for (uint64_t i = 0; i < b.count; ++i) {
+        if (t == DType::Int32) reinterpret_cast<int32_t*>(h.data())[i] = static_cast<int32_t>(g.genrand_int32());
+        else if (t == DType::Float64) reinterpret_cast<double*>(h.data())[i] = g.genrand_res53();
+        else if (t == DType::Float32) reinterpret_cast<float*>(h.data())[i] = static_cast<float>(g.genrand_res53());
+        else reinterpret_cast<int64_t*>(h.data())[i] = (static_cast<int64_t>(g.genrand_int32()) << 32) | g.genrand_int32();
+      }
+      HIP_CHECK(hipMemcpy(b.send.get(), h.data(), h.size(), hipMemcpyHostToDevice));
+    } else {
+      FillSpec fs;
+      fs.pattern = dtype_is_float(t) ? Pattern::Uniform : Pattern::FullRange;
+      fs.seed = c.seed + static_cast<uint64_t>(c.env.rank);  // rank-seeded like reduce.c:38-41
+      fill_device(b.send.get(), b.count, t, fs, c.stream);
+    }
+    bufs.push_back(std::move(b));
+  }
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  auto body_for = [&](B& b, Op o) {
+    return [&c, &b, o] {
+      if (c.collective == "reduce") c.comm->reduce(b.send.get(), b.recv.get(), b.count, b.t, o, c.root, c.stream);
+      else c.comm->allreduce(b.send.get(), b.recv.get(), b.count, b.t, o, c.stream);
+    };
+  };
+  const int saved_iters = c.iters;
+  c.iters = 1;
+  const bool saved_graph = c.graph;
+  c.graph = false;
+  for (int w = 0; w < c.warmup; ++w)
+    for (auto& b : bufs) time_iters(c, body_for(b, Op::Sum));  // reduce.c:61-64
+  c.iters = saved_iters;
+  c.graph = saved_graph;
+  if (c.env.rank == c.root) std::printf("%s\n", gnuplot_header().c_str());
+  bool ok = true;
+  for (int x = 0; x < c.retries; ++x) {
+    for (auto& b : bufs) {
+      for (Op o : ops) {
+        HIP_CHECK(hipMemsetAsync(b.recv.get(), 0, b.recv.bytes(), c.stream));  // bzero (reduce.c:74)
+        const double dt = time_iters(c, body_for(b, o));
+        const double bytes = static_cast<double>(b.count) * c.env.world * dtype_size(b.t);
+        const double algbw = static_cast<double>(b.count) * dtype_size(b.t) / dt / kGB;
+        const double busbw = c.collective == "allreduce" ? algbw * 2.0 * (c.env.world - 1) / c.env.world : algbw;
+        bool vok = true;
+        if (c.verify && x == 0) {
+          switch (b.t) {
+            case DType::Int32: vok = check_samples<int32_t>(c, o, b.send.get(), b.recv.get(), b.count); break;
+            case DType::Int64: vok = check_samples<int64_t>(c, o, b.send.get(), b.recv.get(), b.count); break;
+            case DType::Float32: vok = check_samples<float>(c, o, b.send.get(), b.recv.get(), b.count); break;
+            case DType::Float64: vok = check_samples<double>(c, o, b.send.get(), b.recv.get(), b.count); break;
+          }
+          ok = ok && vok;
+        }
+        Json j;
+        j.set("count_per_rank", b.count).set("algbw_gb_per_s", algbw).set("busbw_gb_per_s", busbw).set("retry", x);
+        if (c.verify && x == 0) j.set("verified", vok);
+        emit(c, b.t, o, bytes, dt, j);
+      }
+    }
+  }
+  return ok;
+}
+
+// ------------------------------------------------------------------------------ scalar mode
+bool run_scalar(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>& ops,
+                const std::vector<uint64_t>& counts) {
+  Workspace ws(c.device);
+  DeviceBuffer out(8), loc(8), oracle(8);
+  if (c.env.rank == c.root) std::printf("%s\n", gnuplot_header().c_str());
+  bool ok = true;
+  for (size_t k = 0; k < dtypes.size(); ++k) {
+    const DType t = dtypes[k];
+    const uint64_t n = counts[k];
+    const uint64_t base = n / c.env.world, rem = n % c.env.world;
+    const uint64_t count = base + (static_cast<uint64_t>(c.env.rank) < rem ? 1 : 0);
+    const uint64_t offset = c.env.rank * base + std::min<uint64_t>(c.env.rank, rem);
+    DeviceBuffer x(std::max<uint64_t>(count, 1) * dtype_size(t));
+    FillSpec fs;
+    fs.pattern = dtype_is_float(t) ? Pattern::Uniform : Pattern::FullRange;
+    fs.seed = c.seed;
+    fs.offset = offset;  // one logical global array, independent of the rank count
+    fill_device(x.get(), count, t, fs, c.stream);
+    HIP_CHECK(hipStreamSynchronize(c.stream));
+    for (Op o : ops) {
+      const DType acc = default_acc(t, o);
+      auto body = [&] {
+        reduce(x.get(), count, t, o, acc, out.get(), ws, c.stream, c.kcfg);
+        c.comm->allreduce(out.get(), out.get(), 1, acc, o, c.stream);
+      };
+      for (int w = 0; w < c.warmup; ++w) {
+        body();
+        c.comm->synchronize(c.stream, c.timeout_s);
+      }
+      for (int x_ = 0; x_ < c.retries; ++x_) {
+        const double dt = time_iters(c, body);
+        Json j;
+        j.set("n_total", n).set("count_per_rank", count).set("retry", x_);
+        bool vok = true;
+        if (c.verify && x_ == 0) {
+          unsigned char g[8] = {0}, l[8] = {0}, orc[8] = {0};
+          HIP_CHECK(hipMemcpy(g, out.get(), 8, hipMemcpyDeviceToHost));
+          reduce(x.get(), count, t, o, acc, loc.get(), ws, c.stream, c.kcfg);
+          ReduceConfig two = c.kcfg;
+          two.single_pass = false;
+          reduce(x.get(), count, t, o, acc, oracle.get(), ws, c.stream, two);
+          HIP_CHECK(hipStreamSynchronize(c.stream));
+          HIP_CHECK(hipMemcpy(l, loc.get(), 8, hipMemcpyDeviceToHost));
+          HIP_CHECK(hipMemcpy(orc, oracle.get(), 8, hipMemcpyDeviceToHost));
+          std::vector<unsigned char> all(8 * static_cast<size_t>(c.env.world));
+          c.boot->allgather(l, all.data(), 8);
+          std::vector<unsigned char> packed(dtype_size(acc) * c.env.world);
+          for (int r = 0; r < c.env.world; ++r) std::memcpy(&packed[r * dtype_size(acc)], &all[r * 8], dtype_size(acc));
+          unsigned char host_fold[8] = {0};
+          cpu_fold(packed.data(), c.env.world, acc, o, host_fold);
+          if (dtype_is_float(acc) && o == Op::Sum) {
+            const double gv = acc_as_double(g, acc), hv = acc_as_double(host_fold, acc);
+            const double lv = acc_as_double(l, acc), ov = acc_as_double(orc, acc);
+            vok = std::fabs(gv - hv) <= 1e-12 * (std::fabs(hv) + 1.0) && std::fabs(lv - ov) <= 1e-9 * (std::fabs(ov) + 1.0);
+          } else {
+            vok = std::memcmp(g, host_fold, dtype_size(acc)) == 0 && std::memcmp(l, orc, dtype_size(acc)) == 0;
+          }
+          std::vector<int> oks(c.env.world);
+          int mine = vok ? 1 : 0;
+          c.boot->allgather(&mine, oks.data(), sizeof mine);
+          vok = std::all_of(oks.begin(), oks.end(), [](int v) { return v != 0; });
+          ok = ok && vok;
+          j.set("verified", vok).set("result", acc_as_double(g, acc));
+        }
+        emit(c, t, o, static_cast<double>(n) * dtype_size(t), dt, j);
+      }
+    }
+  }
+  return ok;
+}
+
+void usage() {
+  std::printf(
+      "reduce_xgmi — RCCL-over-xGMI reduction benchmark (one process per GPU)\n"
+      "  --mode=vector|scalar        reduce.c element-wise reduce | global array -> one value\n"
+      "  --collective=reduce|allreduce (vector default: reduce, like MPI_Reduce; scalar: allreduce)\n"
+      "  --dtypes=INT,DOUBLE  --ops=MAX,MIN,SUM  --retries=5  --warmup=1  --iters=10  --root=0\n"
+      "  --ints=N --doubles=N --longs=N --floats=N   global element counts (reduce.c defaults)\n"
+      "  --n=N                        global count for every dtype (scalar mode north star: 1e9)\n"
+      "  --graph                      replay the timed iterations from a captured hipGraph\n"
+      "  --mt19937                    vector mode: reduce.c's exact per-rank MT19937 data (host-generated)\n"
+      "  --units=gib|gb               GNUPlot column unit (default gib = reduce.c's 2^30)\n"
+      "  --json=PATH  --noverify  --seed=N  --block= --unroll= --wg-per-cu= --policy=nt|default\n"
+      "launch: torchrun --nproc-per-node=8 --master-addr 127.0.0.1 ... | mpirun -np 8 ...\n");
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  CmdArgs args;
+  try {
+    args = CmdArgs(argc, argv);
+  } catch (const CliError& e) {
+    std::fprintf(stderr, "%s\n", e.what());
+    return EXIT_FAILURE;
+  }
+  if (args.has("help")) {
+    usage();
+    return EXIT_SUCCESS;
+  }
+  Ctx c;
+  c.env = launch_env_from_environment();
+  std::vector<DType> dtypes = {DType::Int32, DType::Float64};
+  std::vector<Op> ops = {Op::Max, Op::Min, Op::Sum};
+  uint64_t ints = kNumInts, doubles = kNumDoubles, longs = 0, floats = 0, n_all = 0;
+  try {
+    for (const auto& u : args.unknown(kKnown))
+      if (c.env.rank == 0) std::fprintf(stderr, "warning: unknown flag --%s ignored\n", u.c_str());
+    c.mode = args.str_or("mode", "vector");
+    if (c.mode != "vector" && c.mode != "scalar") throw CliError("--mode must be vector|scalar");
+    c.collective = args.str_or("collective", c.mode == "vector" ? "reduce" : "allreduce");
+    if (c.collective != "reduce" && c.collective != "allreduce") throw CliError("--collective must be reduce|allreduce");
+    if (c.mode == "scalar" && c.collective != "allreduce") throw CliError("scalar mode uses --collective=allreduce");
+    std::vector<std::string> list;
+    if (args.get_list("dtypes", &list)) {
+      dtypes.clear();
+      for (auto& s : list) {
+        DType t;
+        if (!parse_dtype(s, &t)) throw CliError("unknown dtype " + s);
+        dtypes.push_back(t);
+      }
+    }
+    if (args.get_list("ops", &list)) {
+      ops.clear();
+      for (auto& s : list) {
+        Op o;
+        if (!parse_op(s, &o)) throw CliError("unknown op " + s);
+        ops.push_back(o);
+      }
+    }
+    args.get_uint("ints", &ints);
+    args.get_uint("doubles", &doubles);
+    longs = ints;
+    floats = doubles;
+    args.get_uint("longs", &longs);
+    args.get_uint("floats", &floats);
+    if (args.get_uint("n", &n_all)) ints = doubles = longs = floats = n_all;
+    c.retries = args.int_or<int>("retries", c.retries);
+    c.warmup = args.int_or<int>("warmup", c.warmup);
+    c.iters = std::max(1, args.int_or<int>("iters", c.iters));
+    c.root = args.int_or<int>("root", c.root);
+    c.json = args.str_or("json", "");
+    c.graph = args.has("graph");
+    c.mt = args.has("mt19937");
+    c.verify = !args.has("noverify");
+    c.seed = args.int_or<uint64_t>("seed", c.seed);
+    c.units_gb = args.str_or("units", "gib") == "gb";
+    double to = 0;
+    if (args.get_double("timeout", &to)) c.timeout_s = to;
+    c.kcfg.block = args.int_or<int>("block", 0);
+    c.kcfg.unroll = args.int_or<int>("unroll", 0);
+    c.kcfg.wg_per_cu = args.int_or<int>("wg-per-cu", 0);
+    c.kcfg.nontemporal = args.str_or("policy", "nt") != "default";
+    if (c.root < 0 || c.root >= c.env.world) throw CliError("--root out of range");
+  } catch (const CliError& e) {
+    if (c.env.rank == 0) std::fprintf(stderr, "error: %s\n", e.what());
+    return EXIT_FAILURE;
+  }
+
+  const int ndev = device_count();
+  if (ndev == 0) {
+    std::fprintf(stderr, "[rank %d] no HIP device\n", c.env.rank);
+    return EXIT_FAILURE;
+  }
+  c.device = c.env.local_rank % ndev;
+  HIP_CHECK(hipSetDevice(c.device));
+  HIP_CHECK(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+  bool ok = false;
+  try {
+    c.boot = std::make_unique<TcpBootstrap>(c.env);
+    c.comm = std::make_unique<RcclComm>(*c.boot, c.device);
+    install_comm_abort_hook(c.comm.get());
+    if (c.env.rank == 0) {
+      DeviceInfo di = device_info(c.device);
+      std::fprintf(stderr, "[reduce_xgmi] %d ranks (%s), %s %s, RCCL %d, mode=%s collective=%s\n", c.env.world,
+                   c.env.launcher.c_str(), di.name.c_str(), di.arch.c_str(), RcclComm::version(), c.mode.c_str(),
+                   c.collective.c_str());
+    }
+    std::vector<uint64_t> counts;
+    for (DType t : dtypes) counts.push_back(global_count(t, ints, longs, floats, doubles));
+    ok = c.mode == "vector" ? run_vector(c, dtypes, ops, counts) : run_scalar(c, dtypes, ops, counts);
+    if (c.verify && c.env.rank == 0) std::fprintf(stderr, "[reduce_xgmi] verification %s\n", ok ? "PASSED" : "FAILED");
+    c.boot->barrier();
+  } catch (const Error& e) {
+    std::fprintf(stderr, "[rank %d] error: %s\n", c.env.rank, e.what());
+    if (c.comm) c.comm->abort();
+    ok = false;
+  }
+  install_comm_abort_hook(nullptr);
+  c.comm.reset();
+  c.boot.reset();
+  HIP_CHECK(hipStreamDestroy(c.stream));
+  return ok ? EXIT_SUCCESS : EXIT_FAILURE;
+}

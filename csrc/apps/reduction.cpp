@@ -1,0 +1,451 @@
+// reduction — single-GPU SUM/MIN/MAX benchmark, CLI-compatible with the CUDA SDK sample the
+// reference modified (cuda/C/src/reduction/reduction.cpp).
+//
+// Parity map:
+//   main (reduction.cpp:84-204)        -> main: QA banner, log file, --method (required,
+//                                         case-sensitive), --type (case-insensitive, default int),
+//                                         --device, dispatch over (dtype x op), QA exit status
+//   runTest{Sum,Min,Max} (:661-1034)   -> run_test: defaults n=2^24, threads=256, data generation,
+//                                         planning, warm-up, 100 timed iterations, throughput line,
+//                                         CPU verification
+//   benchmarkReduce* (:297-568)        -> time_iterations: first-level kernel + device or host
+//                                         (--cpufinal / --cputhresh) finalisation, per-iteration
+//                                         hipEvent timing
+//   getNumBlocksAndThreads (:272-291)  -> plan_reduce (persistent grid for 256 CUs)
+//   shmoo (:576-657, disabled: B6)     -> run_shmoo (implemented)
+//   sum/min/maxreduceCPU (:214-249)    -> cpu_reduce (compensated / exact)
+// Kernels: --kernel=7 (default) mireduce single-pass streaming kernel; 8 = the same first level +
+// a separate finalize launch (the reference's two-launch structure); 0..6 = the Harris
+// whitepaper ladder re-expressed for wave64 (csrc/kernels/ladder.hip), 6 being the reference's
+// "kernel 6" algorithm (multiple elements per thread, LDS tree, unrolled last wave).
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cinttypes>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "mireduce/check.hpp"
+#include "mireduce/cli.hpp"
+#include "mireduce/cpu_reference.hpp"
+#include "mireduce/device.hpp"
+#include "mireduce/ladder.hpp"
+#include "mireduce/log.hpp"
+#include "mireduce/qa.hpp"
+#include "mireduce/reduce.hpp"
+#include "mireduce/report.hpp"
+#include "mireduce/timer.hpp"
+
+using namespace mireduce;
+
+namespace {
+
+struct Options {
+  DType dtype = DType::Int32;
+  std::string type_name = "int";
+  Op op = Op::Sum;
+  DType acc = DType::Int32;
+  bool acc_given = false;
+  uint64_t n = 1ull << 24;  // reduction.cpp:665
+  int threads = 256;        // reduction.cpp:666
+  int kernel = 7;
+  int max_blocks = 0;       // 0 = persistent grid (reference default 64, reduction.cpp:668)
+  bool cpufinal = false;
+  int cputhresh = 1;        // reduction.cpp:670
+  int iterations = 100;     // reduction.cpp:731
+  int unroll = 0;
+  int wg_per_cu = 0;
+  bool nontemporal = true;
+  Pattern pattern = Pattern::SmallInt;  // rand() & 0xFF (reduction.cpp:698-705)
+  uint64_t seed = 1;
+  bool device_fill = false;
+  bool verify = true;
+  std::string json;
+  int device = 0;
+};
+
+const std::set<std::string> kKnown = {
+    "method", "type", "n", "threads", "kernel", "maxblocks", "cpufinal", "cputhresh", "shmoo",
+    "device", "qatest", "noprompt", "prompt", "help", "quiet", "iterations", "acc", "unroll",
+    "wg-per-cu", "policy", "pattern", "seed", "fill", "noverify", "json", "log", "master-log",
+    "countdown", "shmoo-max"};
+
+void usage() {
+  std::printf(
+      "reduction --method=SUM|MIN|MAX [options]\n"
+      "  --type=int|int64|float|double  element type (case-insensitive, default int)\n"
+      "  --n=N            elements (default 16777216; k/M/G suffixes and 1e9 accepted)\n"
+      "  --threads=256|512  workgroup size   --kernel=0..8 (7 = single-pass, default)\n"
+      "  --maxblocks=N    cap the grid (default: persistent grid, 8 WG/CU)\n"
+      "  --cpufinal       fold the per-workgroup partials on the host\n"
+      "  --cputhresh=N    fold on the host when <= N partials remain\n"
+      "  --shmoo          sweep n = 1..32M (powers of two) over kernels, print CSV\n"
+      "  --iterations=100 --acc=TYPE --unroll=2|4|8 --wg-per-cu=N --policy=nt|default\n"
+      "  --pattern=smallint|uniform|fullrange|iotamod --seed=N --fill=host|device --noverify\n"
+      "  --device=N --json=PATH --log=FILE|none --master-log=FILE --qatest --prompt --countdown\n");
+}
+
+size_t pick_threads_for_fill() {
+  unsigned hc = std::thread::hardware_concurrency();
+  return hc ? std::min<unsigned>(hc, 16) : 1;
+}
+
+// Host fill in parallel (identical values to the serial / device fill: element i = f(seed, i)).
+void parallel_fill_host(void* p, uint64_t n, DType t, const FillSpec& s) {
+  const size_t th = n > (1u << 22) ? pick_threads_for_fill() : 1;
+  const uint64_t chunk = (n + th - 1) / th;
+  std::vector<std::thread> pool;
+  for (size_t k = 0; k < th; ++k) {
+    const uint64_t b = std::min<uint64_t>(n, k * chunk), e = std::min<uint64_t>(n, b + chunk);
+    if (b >= e) continue;
+    FillSpec sk = s;
+    sk.offset = s.offset + b;
+    void* pk = static_cast<char*>(p) + b * dtype_size(t);
+    pool.emplace_back([=] { fill_host(pk, e - b, t, sk); });
+  }
+  for (auto& x : pool) x.join();
+}
+
+struct Buffers {
+  DeviceBuffer in, out, partials, ladder;  // ladder: ping-pong scratch of kernels 0..6
+  std::vector<unsigned char> host;  // input copy (for CPU verification)
+  void* pinned = nullptr;           // --cpufinal partials landing zone
+  ~Buffers() {
+    if (pinned) (void)hipHostFree(pinned);
+  }
+};
+
+// One full reduction of d_in (timed region body). Returns nothing; result lands in out
+// (device) or in *host_result (host finalisation).
+struct Runner {
+  const Options& o;
+  Workspace& ws;
+  Buffers& b;
+  hipStream_t s;
+  LaunchPlan plan{};
+  bool host_fold = false;
+
+  ReduceConfig cfg() const {
+    ReduceConfig c;
+    c.block = o.threads;
+    c.unroll = o.unroll;
+    c.wg_per_cu = o.wg_per_cu;
+    c.max_blocks = o.max_blocks;
+    c.nontemporal = o.nontemporal;
+    c.single_pass = (o.kernel == 7);
+    return c;
+  }
+
+  // Returns true if the result was produced on the host into host_out.
+  bool run_once(uint64_t n, unsigned char* host_out) {
+    const void* in = b.in.get();
+    if (o.kernel <= 6) {
+      const int mb = o.max_blocks > 0 ? o.max_blocks : 64;  // reference default (reduction.cpp:668)
+      const size_t need = ladder_scratch_bytes(o.kernel, n, o.threads, mb);
+      if (b.ladder.bytes() < need) {  // grows during the warm-up call only
+        HIP_CHECK(hipStreamSynchronize(s));
+        b.ladder.allocate(need);
+      }
+      plan.block = o.threads;
+      plan.grid = ladder_reduce(o.kernel, in, n, o.dtype, o.op, o.acc, b.out.get(), b.ladder.get(), o.threads, mb, s);
+      return false;
+    }
+    const bool want_host = o.cpufinal || o.cputhresh > 1;
+    if (!want_host) {
+      plan = reduce(in, n, o.dtype, o.op, o.acc, b.out.get(), ws, s, cfg());
+      return false;
+    }
+    plan = reduce_partials(in, n, o.dtype, o.op, o.acc, b.partials.get(), ws.max_grid(), ws.num_cus(), s, cfg());
+    const size_t es = dtype_size(o.acc);
+    if (!o.cpufinal && plan.grid > o.cputhresh) {  // device finalisation, like the relaunch loop
+      reduce_finalize(b.partials.get(), plan.grid, o.acc, o.op, b.out.get(), s);
+      return false;
+    }
+    HIP_CHECK(hipMemcpyAsync(b.pinned, b.partials.get(), plan.grid * es, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    cpu_fold(b.pinned, plan.grid, o.acc, o.op, host_out);
+    return true;
+  }
+};
+
+struct Timing {
+  std::vector<double> ms;  // per iteration, hipEvent (or host clock for host-folded runs)
+  double avg_ms = 0;
+  bool host_result = false;
+  unsigned char result[8] = {0};
+};
+
+Timing time_iterations(Runner& r, uint64_t n, int iters) {
+  Timing t;
+  EventTimer ev;
+  HIP_CHECK(hipDeviceSynchronize());
+  for (int i = 0; i < iters; ++i) {
+    const double h0 = StopWatch::now_s();
+    ev.start(r.s);
+    const bool host = r.run_once(n, t.result);
+    ev.stop(r.s);
+    if (host) {
+      t.ms.push_back((StopWatch::now_s() - h0) * 1e3);
+      t.host_result = true;
+    } else {
+      t.ms.push_back(ev.elapsed_ms());
+    }
+  }
+  double sum = 0;
+  for (double m : t.ms) sum += m;
+  t.avg_ms = iters ? sum / iters : 0;
+  if (!t.host_result) HIP_CHECK(hipMemcpy(t.result, r.b.out.get(), dtype_size(r.o.acc), hipMemcpyDeviceToHost));
+  return t;
+}
+
+std::string fmt_result(const unsigned char* p, DType acc) {
+  char buf[64];
+  if (dtype_is_float(acc)) std::snprintf(buf, sizeof buf, "%f", acc_as_double(p, acc));
+  else std::snprintf(buf, sizeof buf, "%" PRId64, acc_as_int64(p, acc));
+  return buf;
+}
+
+bool run_test(Options& o, Workspace& ws, hipStream_t s) {
+  Logger& L = Logger::instance();
+  L.log(kLogBoth, "METHOD: %s\n", op_name(o.op));
+  L.log(kLogBoth, "%" PRIu64 " elements\n", o.n);
+  L.log(kLogBoth, "%d threads (max)\n", o.threads);
+
+  Buffers b;
+  const size_t es = dtype_size(o.dtype);
+  b.in.allocate(std::max<uint64_t>(o.n, 1) * es);
+  b.out.allocate(8);
+  b.partials.allocate(static_cast<size_t>(std::max(ws.max_grid(), 1 << 16)) * 8);
+  HIP_CHECK(hipHostMalloc(&b.pinned, static_cast<size_t>(std::max(ws.max_grid(), 1 << 16)) * 8, hipHostMallocDefault));
+
+  FillSpec fs;
+  fs.pattern = o.pattern;
+  fs.seed = o.seed;
+  const bool host_copy = !o.device_fill || (o.verify && o.n <= (1ull << 30));
+  if (host_copy) {
+    b.host.resize(o.n * es);
+    parallel_fill_host(b.host.data(), o.n, o.dtype, fs);
+  }
+  if (o.device_fill) fill_device(b.in.get(), o.n, o.dtype, fs, s);
+  else if (o.n) HIP_CHECK(hipMemcpy(b.in.get(), b.host.data(), o.n * es, hipMemcpyHostToDevice));
+  HIP_CHECK(hipDeviceSynchronize());
+
+  Runner r{o, ws, b, s};
+  unsigned char scratch[8];
+  r.run_once(o.n, scratch);  // warm-up (reduction.cpp:729)
+  HIP_CHECK(hipDeviceSynchronize());
+  L.log(kLogBoth, "%d blocks\n\n", r.plan.grid);
+
+  Timing t = time_iterations(r, o.n, o.iterations);
+  const double secs = t.avg_ms * 1e-3;
+  const double bytes = static_cast<double>(o.n) * es;
+  L.log(kLogBoth | kLogMaster, "%s\n", throughput_line(secs > 0 ? 1.0e-9 * bytes / secs : 0.0, secs, o.n, 1,
+                                                       static_cast<unsigned>(r.plan.block)).c_str());
+
+  bool ok = true;
+  unsigned char cpu[8] = {0};
+  double tol = 0;
+  bool checked = false;
+  if (o.verify && host_copy) {
+    cpu_reduce(b.host.data(), o.n, o.dtype, o.op, o.acc, cpu);
+    checked = true;
+    if (dtype_is_float(o.acc)) {
+      const double g = acc_as_double(t.result, o.acc), c = acc_as_double(cpu, o.acc);
+      tol = (o.op == Op::Sum) ? sum_tolerance(o.dtype, o.acc, o.n, cpu_abs_sum(b.host.data(), o.n, o.dtype)) : 0.0;
+      ok = (o.op == Op::Sum) ? std::fabs(g - c) <= tol : g == c;
+    } else {
+      ok = acc_as_int64(t.result, o.acc) == acc_as_int64(cpu, o.acc);
+    }
+  } else if (o.verify) {
+    // Huge device-filled arrays: the two-launch path (different combine order and code path) is
+    // the oracle for the single-pass kernel.
+    Options o2 = o;
+    o2.kernel = (o.kernel == 8) ? 7 : 8;
+    o2.cpufinal = false;
+    o2.cputhresh = 1;
+    Runner r2{o2, ws, b, s};
+    r2.run_once(o.n, scratch);
+    HIP_CHECK(hipMemcpy(cpu, b.out.get(), dtype_size(o.acc), hipMemcpyDeviceToHost));
+    checked = true;
+    if (dtype_is_float(o.acc) && o.op == Op::Sum) {
+      const double g = acc_as_double(t.result, o.acc), c = acc_as_double(cpu, o.acc);
+      tol = 1e-9 * std::fabs(c) + 1e-12;
+      ok = std::fabs(g - c) <= tol;
+    } else {
+      ok = std::memcmp(t.result, cpu, dtype_size(o.acc)) == 0;
+    }
+  }
+  L.log(kLogBoth, "\nGPU result = %s\n", fmt_result(t.result, o.acc).c_str());
+  if (checked) L.log(kLogBoth, "CPU result = %s\n\n", fmt_result(cpu, o.acc).c_str());
+
+  if (!o.json.empty()) {
+    Stats st = compute_stats(t.ms);
+    DeviceInfo di = device_info(o.device);
+    Json j;
+    j.set("app", "reduction").set("method", op_name(o.op)).set("type", dtype_cli_name(o.dtype))
+        .set("acc", dtype_cli_name(o.acc)).set("n", o.n).set("bytes", static_cast<uint64_t>(bytes))
+        .set("kernel", o.kernel).set("block", r.plan.block).set("grid", r.plan.grid).set("unroll", r.plan.unroll)
+        .set("groups", r.plan.groups).set("nontemporal", r.plan.nontemporal).set("cpufinal", o.cpufinal)
+        .set("iterations", o.iterations).set("avg_ms", t.avg_ms).set("median_ms", st.median).set("min_ms", st.min)
+        .set("max_ms", st.max).set("std_ms", st.stddev).set("gb_per_s", secs > 0 ? bytes / secs / kGB : 0.0)
+        .set("gib_per_s", secs > 0 ? bytes / secs / kGiB : 0.0).set("bytes_per_GB", kGB)
+        .set("gpu_result", acc_as_double(t.result, o.acc)).set("verified", checked ? ok : true)
+        .set("tolerance", tol).set("device", di.name).set("arch", di.arch).set("cus", di.cus)
+        .set("iteration_ms", t.ms);
+    j.write_file(o.json);
+  }
+  return ok;
+}
+
+void run_shmoo(Options o, Workspace& ws, hipStream_t s, uint64_t max_n) {
+  // Reference: shmoo<T>(1, 33554432, ...) over kernels 0..6 (reduction.cpp:576-657, disabled);
+  // the OpenCL twin prints a kernel x size table (oclReduction.cpp:392-455).
+  std::printf("n,bytes,kernel,avg_ms,GB/s\n");
+  const size_t es = dtype_size(o.dtype);
+  Buffers b;
+  b.in.allocate(max_n * es);
+  b.out.allocate(8);
+  b.partials.allocate(static_cast<size_t>(1 << 16) * 8);
+  FillSpec fs;
+  fs.pattern = o.pattern;
+  fs.seed = o.seed;
+  fill_device(b.in.get(), max_n, o.dtype, fs, s);
+  HIP_CHECK(hipDeviceSynchronize());
+  const int kernels[] = {0, 1, 2, 3, 4, 5, 6, 8, 7};
+  for (uint64_t n = 1; n <= max_n; n *= 2) {
+    for (int k : kernels) {
+      o.kernel = k;
+      o.cpufinal = false;
+      o.cputhresh = 1;
+      Runner r{o, ws, b, s};
+      unsigned char scratch[8];
+      r.run_once(n, scratch);
+      Timing t = time_iterations(r, n, o.iterations);
+      const double bytes = static_cast<double>(n) * es;
+      std::printf("%" PRIu64 ",%.0f,%d,%.6f,%.4f\n", n, bytes, k, t.avg_ms,
+                  t.avg_ms > 0 ? 1e-9 * bytes / (t.avg_ms * 1e-3) : 0.0);
+      std::fflush(stdout);
+    }
+  }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const char* const* cargv = argv;
+  qa_start(argc, cargv);
+  CmdArgs args;
+  try {
+    args = CmdArgs(argc, cargv);
+  } catch (const CliError& e) {
+    std::fprintf(stderr, "%s\n", e.what());
+    return EXIT_FAILURE;
+  }
+  if (args.has("help")) {
+    usage();
+    qa_finish_exit(argc, cargv, QaStatus::Passed);
+  }
+  Logger& L = Logger::instance();
+  const std::string log = args.str_or("log", "reduction.txt");
+  if (log != "none") L.set_log_file(log);  // shrSetLogFileName("reduction.txt") (reduction.cpp:88)
+  L.set_master_file(args.str_or("master-log", ""));
+  L.set_quiet(args.has("quiet"));
+  for (const auto& u : args.unknown(kKnown)) std::fprintf(stderr, "warning: unknown flag --%s ignored\n", u.c_str());
+
+  Options o;
+  std::string method;
+  if (!args.has("method")) {  // reduction.cpp:124-128
+    std::fprintf(stderr, "MISSING --method FLAG.\nYou must provide --method={ SUM | MIN | MAX }.\n");
+    std::exit(1);
+  }
+  args.get_str("method", &method);
+  if (!parse_op_strict(method, &o.op)) {  // case-sensitive strcmp (reduction.cpp:165-199)
+    std::fprintf(stderr, "No --method specified!\n");
+    std::exit(1);
+  }
+  try {
+    std::string ty;
+    if (args.get_str("type", &ty)) {
+      if (!parse_dtype(ty, &o.dtype)) {
+        std::fprintf(stderr, "warning: unknown --type=%s, using int (reduction.cpp:106-108)\n", ty.c_str());
+        o.dtype = DType::Int32;
+      }
+      o.type_name = ty;
+    }
+    o.acc = default_acc(o.dtype, o.op);
+    // Parity mode: the reference accumulates int SUM in int (reduction_kernel.cu). Default here
+    // widens (B7); --acc=int restores the 32-bit wrap.
+    std::string acc;
+    if (args.get_str("acc", &acc)) {
+      if (!parse_dtype(acc, &o.acc) || !acc_supported(o.dtype, o.op, o.acc)) throw CliError("unsupported --acc=" + acc);
+      o.acc_given = true;
+    }
+    args.get_uint("n", &o.n);
+    o.threads = args.int_or<int>("threads", o.threads);
+    o.kernel = args.int_or<int>("kernel", o.kernel);
+    o.max_blocks = args.int_or<int>("maxblocks", o.max_blocks);
+    o.cpufinal = args.has("cpufinal");
+    o.cputhresh = args.int_or<int>("cputhresh", o.cputhresh);
+    o.iterations = args.int_or<int>("iterations", o.iterations);
+    o.unroll = args.int_or<int>("unroll", o.unroll);
+    o.wg_per_cu = args.int_or<int>("wg-per-cu", o.wg_per_cu);
+    o.nontemporal = args.str_or("policy", "nt") != "default";
+    std::string pat = args.str_or("pattern", "smallint");
+    if (pat == "smallint") o.pattern = Pattern::SmallInt;
+    else if (pat == "uniform") o.pattern = Pattern::Uniform;
+    else if (pat == "fullrange") o.pattern = Pattern::FullRange;
+    else if (pat == "iotamod") o.pattern = Pattern::IotaMod;
+    else throw CliError("unknown --pattern=" + pat);
+    o.seed = args.int_or<uint64_t>("seed", o.seed);
+    o.device_fill = args.str_or("fill", "host") == "device";
+    o.verify = !args.has("noverify");
+    o.json = args.str_or("json", "");
+    o.device = args.int_or<int>("device", 0);
+    if (o.kernel < 0 || o.kernel > 8) throw CliError("--kernel must be 0..8");
+    if (o.kernel >= 7 && o.threads != 256 && o.threads != 512) throw CliError("--threads must be 256 or 512 for kernels 7/8");
+    if (o.kernel <= 6 && (o.threads < 64 || o.threads > 1024 || (o.threads & (o.threads - 1))))
+      throw CliError("--threads must be a power of two in [64, 1024] for kernels 0..6");
+    if (o.iterations < 1) throw CliError("--iterations must be >= 1");
+  } catch (const CliError& e) {
+    std::fprintf(stderr, "error: %s\n", e.what());
+    return EXIT_FAILURE;
+  }
+
+  const int ndev = device_count();
+  if (ndev == 0 || o.device >= ndev) {
+    L.log(kLogBoth, "Error: no usable HIP device (found %d).\n\n", ndev);
+    qa_finish_exit(argc, cargv, QaStatus::Waived);
+  }
+  DeviceInfo di = device_info(o.device);
+  if (di.arch.rfind("gfx950", 0) != 0) {  // kernels are built for gfx950 only (cf. reduction.cpp:148-155)
+    L.log(kLogBoth, "Error: device %d (%s, %s) is not gfx950 (MI355X).\n\n", o.device, di.name.c_str(), di.arch.c_str());
+    qa_finish_exit(argc, cargv, QaStatus::Waived);
+  }
+  HIP_CHECK(hipSetDevice(o.device));
+  L.log(kLogBoth, "Using Device %d: %s\n\n", o.device, di.name.c_str());
+  L.log(kLogBoth, "Reducing array of type %s\n\n", dtype_cli_name(o.dtype));
+
+  hipStream_t s;
+  HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  bool ok = true;
+  try {
+    Workspace ws(o.device);
+    if (args.has("shmoo")) {
+      run_shmoo(o, ws, s, args.int_or<uint64_t>("shmoo-max", 33554432ull));
+    } else {
+      ok = run_test(o, ws, s);
+    }
+  } catch (const Error& e) {
+    std::fprintf(stderr, "error: %s\n", e.what());
+    ok = false;
+  }
+  HIP_CHECK(hipStreamDestroy(s));
+  L.close();
+  qa_finish_exit(argc, cargv, ok ? QaStatus::Passed : QaStatus::Failed);
+}

@@ -14,6 +14,7 @@
 
 #include "mireduce/check.hpp"
 #include "mireduce/cpu_reference.hpp"
+#include "mireduce/ladder.hpp"
 #include "mireduce/mt19937.hpp"
 #include "mireduce/reduce.hpp"
 #include "mireduce/types.hpp"
@@ -249,6 +250,27 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("acc_supported", [](int dtype, int op, int acc) {
     return acc_supported(static_cast<DType>(dtype), static_cast<Op>(op), static_cast<DType>(acc));
+  });
+
+  m.def(
+      "ladder_reduce",
+      [](int kernel, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out, uintptr_t scratch,
+         int threads, int max_blocks, uintptr_t stream) {
+        return ladder_reduce(kernel, as_ptr<const void>(in), n, static_cast<DType>(dtype), static_cast<Op>(op),
+                             static_cast<DType>(acc), as_ptr<void>(out), as_ptr<void>(scratch), threads, max_blocks,
+                             as_stream(stream));
+      },
+      py::arg("kernel"), py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"), py::arg("acc"),
+      py::arg("out_ptr"), py::arg("scratch_ptr"), py::arg("threads") = 256, py::arg("max_blocks") = 64,
+      py::arg("stream") = 0);
+
+  m.def("ladder_scratch_bytes", &ladder_scratch_bytes, py::arg("kernel"), py::arg("n"), py::arg("threads") = 256,
+        py::arg("max_blocks") = 64);
+
+  m.def("ladder_geometry", [](int kernel, uint64_t n, int threads, int max_blocks) {
+    int b = 0, t = 0;
+    ladder_geometry(kernel, n, threads, max_blocks, &b, &t);
+    return py::make_tuple(b, t);
   });
 
   m.def("compiled_variants", &compiled_variants);

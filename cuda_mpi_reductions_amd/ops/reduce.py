@@ -29,6 +29,7 @@ __all__ = [
     "op_code",
     "cpu_reduce",
     "sum_tolerance",
+    "ladder_reduce",
 ]
 
 DTYPE_CODES = {torch.int32: 0, torch.int64: 1, torch.float32: 2, torch.float64: 3}
@@ -209,3 +210,20 @@ def reduce_partials(x: torch.Tensor, op: str = "sum", acc_dtype=None, max_grid: 
 
 def sum_tolerance(dtype: torch.dtype, acc: torch.dtype, n: int, abs_sum: float) -> float:
     return native().sum_tolerance(dtype_code(dtype), dtype_code(acc), n, abs_sum)
+
+
+def ladder_reduce(x: torch.Tensor, op: str = "sum", kernel: int = 6, acc_dtype=None, threads: int = 256,
+                  max_blocks: int = 64) -> torch.Tensor:
+    """Reduce with one of the Harris-ladder kernels 0..6 (csrc/kernels/ladder.hip), multi-pass like
+    the reference's benchmarkReduce* relaunch loop (reduction.cpp:344-357)."""
+    C = native()
+    if x.device.type != "cuda":
+        raise ValueError("ladder_reduce needs a device tensor")
+    x = x.contiguous()
+    acc = acc_dtype or default_acc_dtype(x.dtype, op)
+    out = torch.empty(1, dtype=acc, device=x.device)
+    nbytes = C.ladder_scratch_bytes(kernel, x.numel(), threads, max_blocks)
+    scratch = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
+    C.ladder_reduce(kernel, x.data_ptr(), x.numel(), dtype_code(x.dtype), op_code(op), dtype_code(acc),
+                    out.data_ptr(), scratch.data_ptr(), threads, max_blocks, _stream_handle(x.device, None))
+    return out

@@ -195,3 +195,42 @@ def test_nan_and_inf_semantics():
     assert math.isnan(reduce(x, "sum").item())
     y = torch.tensor([1.0, float("inf"), -2.0], dtype=torch.float32, device=DEV)
     assert reduce(y, "max").item() == math.inf
+
+
+# ---------------------------------------------------------------------------------------------
+# Harris ladder kernels 0..6 (csrc/kernels/ladder.hip) — the reference's --kernel values.
+from cuda_mpi_reductions_amd.ops import ladder_reduce  # noqa: E402
+
+LADDER_COMBOS = [c for c in COMBOS if c[0] in (torch.int32, torch.float64, torch.int64)]
+
+
+@pytest.mark.parametrize("kernel", range(7))
+@pytest.mark.parametrize("dt,op,acc", LADDER_COMBOS, ids=lambda v: str(v).replace("torch.", ""))
+@pytest.mark.parametrize("n", [1, 63, 65, 1000, 65537, 1_000_003])
+def test_ladder_kernels(kernel, dt, op, acc, n):
+    x = torch.empty(n, dtype=dt, device=DEV)
+    fill_(x, "uniform" if dt.is_floating_point else "fullrange", seed=kernel * 31 + n)
+    got = ladder_reduce(x, op, kernel=kernel, acc_dtype=acc).item()
+    check(got, x, op, acc, n)
+
+
+@pytest.mark.parametrize("threads", [64, 128, 256, 512, 1024])
+@pytest.mark.parametrize("kernel", [0, 3, 4, 5, 6])
+def test_ladder_block_sizes(threads, kernel):
+    n = 3_333_331
+    x = torch.empty(n, dtype=torch.float64, device=DEV)
+    fill_(x, "uniform", seed=threads)
+    for op in ("sum", "min", "max"):
+        check(ladder_reduce(x, op, kernel=kernel, threads=threads).item(), x, op, torch.float64, n)
+
+
+def test_ladder_kernel6_non_pow2_no_oob():
+    # Reference bug B1/B2: min/max kernel 6 read past the end for non-power-of-2 n. Put a huge
+    # sentinel right after the view's end: it must not leak into MAX.
+    n = 1_000_001
+    base = torch.empty(n + 4096, dtype=torch.float64, device=DEV)
+    fill_(base, "uniform", seed=1)
+    base[n:] = 1e300
+    x = base[:n]
+    assert ladder_reduce(x, "max", kernel=6).item() == x.max().item()
+    assert reduce(x, "max").item() == x.max().item()

@@ -41,31 +41,40 @@ def parse_args(argv=None):
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default=NORTH_STAR, choices=sorted(k for k, v in CONFIGS.items() if v.mode == "scalar"))
-    p.add_argument("--n", type=int, default=None, help="override the global element count")
+    p.add_argument("--elements", type=int, default=None, help="override the global element count")
     p.add_argument("--serial", action="store_true", help="no overlap between consecutive steps")
     p.add_argument("--block", type=int, default=0)
     p.add_argument("--unroll", type=int, default=0)
     p.add_argument("--wg-per-cu", type=int, default=0)
     p.add_argument("--groups", type=int, default=0)
-    p.add_argument("--policy", choices=["nt", "default"], default="nt")
+    p.add_argument("--policy", choices=["auto", "nt", "default"], default="auto")
     p.add_argument("--two-pass", action="store_true")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--device", choices=["auto", "cuda", "cpu"], default="auto",
+                   help="cpu: gloo ranks + the native host reducer (tests of the contract only)")
     return p.parse_args(argv)
+
+
+def _sync(dev: torch.device) -> None:
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
 
 
 def main(argv=None) -> int:
     args = parse_args(argv)
     native()  # fail loudly if the HIP extension is missing
-    ctx = pdist.init()
+    device_type = None if args.device == "auto" else args.device
+    ctx = pdist.init(device_type=device_type)
     if args.gpus != ctx.world_size and ctx.is_root:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}; using {ctx.world_size}",
               file=sys.stderr)
     cfg = CONFIGS[args.config]
-    if args.n is not None:
+    if args.elements is not None:
         from dataclasses import replace
-        cfg = replace(cfg, n_total=args.n)
+        cfg = replace(cfg, n_total=args.elements)
     kernel = KernelConfig(block=args.block, unroll=args.unroll, wg_per_cu=args.wg_per_cu,
-                          groups=args.groups, nontemporal=(args.policy == "nt"),
+                          groups=args.groups,
+                          nontemporal=None if args.policy == "auto" else args.policy == "nt",
                           single_pass=not args.two_pass)
     wl = ScalarReduction(cfg, ctx, kernel).setup()
     K, W = args.steps, args.warmup
@@ -85,12 +94,12 @@ def main(argv=None) -> int:
             w.wait()
 
     run(0, W)
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     pdist.barrier(ctx)
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     t0 = time.perf_counter()
     run(W, K)
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     t1 = time.perf_counter()
     pdist.barrier(ctx)
     elapsed = pdist.max_over_ranks(t1 - t0, ctx)
@@ -126,6 +135,7 @@ def main(argv=None) -> int:
             "scaling": "strong",
             "vs_baseline": round(gbps / cfg.baseline, 3) if cfg.baseline else None,
             "dtype": "fp64" if cfg.dtype == torch.float64 else str(cfg.dtype).replace("torch.", ""),
+            "device": dev.type,
             "data": "synthetic (on-device counter-based U[0,1) fill, untimed; random-filled array)",
             "config": {
                 "model": f"{cfg.name}: {cfg.description}",

@@ -314,7 +314,7 @@ void usage() {
       "  --graph                      replay the timed iterations from a captured hipGraph\n"
       "  --mt19937                    vector mode: reduce.c's exact per-rank MT19937 data (host-generated)\n"
       "  --units=gib|gb               GNUPlot column unit (default gib = reduce.c's 2^30)\n"
-      "  --json=PATH  --noverify  --seed=N  --block= --unroll= --wg-per-cu= --policy=nt|default\n"
+      "  --json=PATH  --noverify  --seed=N  --block= --unroll= --wg-per-cu= --policy=auto|nt|default\n"
       "launch: torchrun --nproc-per-node=8 --master-addr 127.0.0.1 ... | mpirun -np 8 ...\n");
 }
 
@@ -384,7 +384,10 @@ int main(int argc, char** argv) {
     c.kcfg.block = args.int_or<int>("block", 0);
     c.kcfg.unroll = args.int_or<int>("unroll", 0);
     c.kcfg.wg_per_cu = args.int_or<int>("wg-per-cu", 0);
-    c.kcfg.nontemporal = args.str_or("policy", "nt") != "default";
+    {
+      const std::string pol = args.str_or("policy", "auto");
+      c.kcfg.policy = pol == "nt" ? 1 : (pol == "default" ? 0 : -1);
+    }
     if (c.root < 0 || c.root >= c.env.world) throw CliError("--root out of range");
   } catch (const CliError& e) {
     if (c.env.rank == 0) std::fprintf(stderr, "error: %s\n", e.what());

@@ -61,7 +61,7 @@ struct Options {
   int iterations = 100;     // reduction.cpp:731
   int unroll = 0;
   int wg_per_cu = 0;
-  bool nontemporal = true;
+  int policy = -1;
   Pattern pattern = Pattern::SmallInt;  // rand() & 0xFF (reduction.cpp:698-705)
   uint64_t seed = 1;
   bool device_fill = false;
@@ -81,12 +81,12 @@ void usage() {
       "reduction --method=SUM|MIN|MAX [options]\n"
       "  --type=int|int64|float|double  element type (case-insensitive, default int)\n"
       "  --n=N            elements (default 16777216; k/M/G suffixes and 1e9 accepted)\n"
-      "  --threads=256|512  workgroup size   --kernel=0..8 (7 = single-pass, default)\n"
+      "  --threads=256|512|1024  workgroup size   --kernel=0..8 (7 = single-pass, default)\n"
       "  --maxblocks=N    cap the grid (default: persistent grid, 8 WG/CU)\n"
       "  --cpufinal       fold the per-workgroup partials on the host\n"
       "  --cputhresh=N    fold on the host when <= N partials remain\n"
       "  --shmoo          sweep n = 1..32M (powers of two) over kernels, print CSV\n"
-      "  --iterations=100 --acc=TYPE --unroll=2|4|8 --wg-per-cu=N --policy=nt|default\n"
+      "  --iterations=100 --acc=TYPE --unroll=2|4|8 --wg-per-cu=N --policy=auto|nt|default\n"
       "  --pattern=smallint|uniform|fullrange|iotamod --seed=N --fill=host|device --noverify\n"
       "  --device=N --json=PATH --log=FILE|none --master-log=FILE --qatest --prompt --countdown\n");
 }
@@ -137,7 +137,7 @@ struct Runner {
     c.unroll = o.unroll;
     c.wg_per_cu = o.wg_per_cu;
     c.max_blocks = o.max_blocks;
-    c.nontemporal = o.nontemporal;
+    c.policy = o.policy;
     c.single_pass = (o.kernel == 7);
     return c;
   }
@@ -395,7 +395,10 @@ int main(int argc, char** argv) {
     o.iterations = args.int_or<int>("iterations", o.iterations);
     o.unroll = args.int_or<int>("unroll", o.unroll);
     o.wg_per_cu = args.int_or<int>("wg-per-cu", o.wg_per_cu);
-    o.nontemporal = args.str_or("policy", "nt") != "default";
+    {
+      const std::string pol = args.str_or("policy", "auto");
+      o.policy = pol == "nt" ? 1 : (pol == "default" ? 0 : -1);
+    }
     std::string pat = args.str_or("pattern", "smallint");
     if (pat == "smallint") o.pattern = Pattern::SmallInt;
     else if (pat == "uniform") o.pattern = Pattern::Uniform;
@@ -408,7 +411,8 @@ int main(int argc, char** argv) {
     o.json = args.str_or("json", "");
     o.device = args.int_or<int>("device", 0);
     if (o.kernel < 0 || o.kernel > 8) throw CliError("--kernel must be 0..8");
-    if (o.kernel >= 7 && o.threads != 256 && o.threads != 512) throw CliError("--threads must be 256 or 512 for kernels 7/8");
+    if (o.kernel >= 7 && o.threads != 0 && o.threads != 256 && o.threads != 512 && o.threads != 1024)
+      throw CliError("--threads must be 256, 512 or 1024 for kernels 7/8");
     if (o.kernel <= 6 && (o.threads < 64 || o.threads > 1024 || (o.threads & (o.threads - 1))))
       throw CliError("--threads must be a power of two in [64, 1024] for kernels 0..6");
     if (o.iterations < 1) throw CliError("--iterations must be >= 1");

@@ -20,14 +20,15 @@
 
 namespace mireduce {
 
-// Tunables of the streaming kernel. 0 means "use the tuned gfx950 default".
+// Tunables of the streaming kernel. 0 (or -1 for `policy`) means "use the tuned gfx950 default",
+// which depends on the array size (docs/TUNING.md, profiles/r1_tuning/).
 struct ReduceConfig {
-  int block = 0;          // threads per workgroup: 256 | 512
-  int unroll = 0;         // independent 16-byte loads in flight per thread: 2 | 4 | 8
+  int block = 0;          // threads per workgroup: 256 | 512 | 1024
+  int unroll = 0;         // independent 16-byte loads in flight per thread: 2 | 4 | 8 | 16
   int wg_per_cu = 0;      // persistent-grid occupancy target
   int max_blocks = 0;     // hard cap on the grid (reference --maxblocks)
   int groups = 0;         // fan-in shards of the arrival ticket (<= 64)
-  bool nontemporal = true;   // streaming loads bypass-allocate (nt) vs default policy
+  int policy = -1;        // streaming-load cache policy: -1 auto, 0 default, 1 non-temporal (nt)
   bool single_pass = true;   // last-arriver finalisation vs a second finalize launch
 };
 

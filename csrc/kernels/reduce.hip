@@ -17,6 +17,7 @@
 //     arrivals costs ~25 us, eight counters ~3 us).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -237,11 +238,13 @@ void launch_stream(const kern::Args& a, int grid, hipStream_t s) {
                      0, s, a);
 }
 
-constexpr int kBlocks[] = {256, 512};
-constexpr int kUnrolls[] = {2, 4, 8};
+constexpr int kBlocks[] = {256, 512, 1024};
+constexpr int kUnrolls[] = {2, 4, 8, 16};
+constexpr int kNumBlocks = 3;
+constexpr int kNumUnrolls = 4;
 
-int block_index(int b) { return b == 512 ? 1 : (b == 256 ? 0 : -1); }
-int unroll_index(int u) { return u == 2 ? 0 : (u == 4 ? 1 : (u == 8 ? 2 : -1)); }
+int block_index(int b) { return b == 256 ? 0 : (b == 512 ? 1 : (b == 1024 ? 2 : -1)); }
+int unroll_index(int u) { return u == 2 ? 0 : (u == 4 ? 1 : (u == 8 ? 2 : (u == 16 ? 3 : -1))); }
 
 // combo index: (op, dtype, acc) → 0..13
 int combo_index(Op op, DType t, DType acc) {
@@ -263,23 +266,30 @@ int combo_index(Op op, DType t, DType acc) {
 constexpr int kCombos = 14;
 
 struct Table {
-  LaunchFn fn[kCombos][2][3][2];
+  LaunchFn fn[kCombos][kNumBlocks][kNumUnrolls][2];
 };
+
+template <class OpT, class T, class AccT, int BI, int UI>
+void fill_one(Table& tb, int c) {
+  constexpr int B = kBlocks[BI];
+  constexpr int U = kUnrolls[UI];
+  tb.fn[c][BI][UI][0] = launch_stream<OpT, T, AccT, B, U, false>;
+  tb.fn[c][BI][UI][1] = launch_stream<OpT, T, AccT, B, U, true>;
+}
+
+template <class OpT, class T, class AccT, int BI>
+void fill_block(Table& tb, int c) {
+  fill_one<OpT, T, AccT, BI, 0>(tb, c);
+  fill_one<OpT, T, AccT, BI, 1>(tb, c);
+  fill_one<OpT, T, AccT, BI, 2>(tb, c);
+  fill_one<OpT, T, AccT, BI, 3>(tb, c);
+}
 
 template <class OpT, class T, class AccT>
 void fill_combo(Table& tb, int c) {
-  tb.fn[c][0][0][0] = launch_stream<OpT, T, AccT, 256, 2, false>;
-  tb.fn[c][0][0][1] = launch_stream<OpT, T, AccT, 256, 2, true>;
-  tb.fn[c][0][1][0] = launch_stream<OpT, T, AccT, 256, 4, false>;
-  tb.fn[c][0][1][1] = launch_stream<OpT, T, AccT, 256, 4, true>;
-  tb.fn[c][0][2][0] = launch_stream<OpT, T, AccT, 256, 8, false>;
-  tb.fn[c][0][2][1] = launch_stream<OpT, T, AccT, 256, 8, true>;
-  tb.fn[c][1][0][0] = launch_stream<OpT, T, AccT, 512, 2, false>;
-  tb.fn[c][1][0][1] = launch_stream<OpT, T, AccT, 512, 2, true>;
-  tb.fn[c][1][1][0] = launch_stream<OpT, T, AccT, 512, 4, false>;
-  tb.fn[c][1][1][1] = launch_stream<OpT, T, AccT, 512, 4, true>;
-  tb.fn[c][1][2][0] = launch_stream<OpT, T, AccT, 512, 8, false>;
-  tb.fn[c][1][2][1] = launch_stream<OpT, T, AccT, 512, 8, true>;
+  fill_block<OpT, T, AccT, 0>(tb, c);
+  fill_block<OpT, T, AccT, 1>(tb, c);
+  fill_block<OpT, T, AccT, 2>(tb, c);
 }
 
 const Table& table() {
@@ -304,10 +314,24 @@ const Table& table() {
   return tb;
 }
 
-// Tuned gfx950 defaults (see docs/TUNING.md; profiles/ holds the rocprofv3 evidence).
-constexpr int kDefaultBlock = 256;
-constexpr int kDefaultUnroll = 4;
-constexpr int kDefaultWgPerCu = 8;
+// Tuned gfx950 defaults, measured on MI355X with tools/tune.py (interleaved rounds, one process;
+// profiles/r1_tuning/). Median read bandwidth of the chosen point vs the best point per size:
+//   8 GB f64 sum   512 x 16, 1 WG/CU, nt   7.29 TB/s (best)
+//   1 GB f64 sum   256 x  2, 3 WG/CU, nt   7.12 TB/s (best)      2 GB i64 min: 7.21 (best)
+//   8 GB f32 sum   256 x  2, 3 WG/CU, nt   7.20 TB/s (best 7.21)
+//   256 MB         512 x 16, 1 WG/CU, default policy (Infinity-Cache re-reads) 6.72 TB/s (best)
+//   128 MB         256 x  4, 3 WG/CU, nt   6.10 TB/s (best; launch + tail dominate)
+// Fewer, fatter workgroups beat the "fill every wave slot" grid (8 WG/CU: 6.91 TB/s at 8 GB).
+struct Defaults {
+  int block, unroll, wg_per_cu, policy;
+};
+Defaults tuned_defaults(size_t bytes, size_t elem_size) {
+  constexpr size_t MB = 1ull << 20;
+  if (elem_size == 8 && bytes >= 3072 * MB) return {512, 16, 1, 1};
+  if (bytes > 384 * MB) return {256, 2, 3, 1};
+  if (bytes > 192 * MB) return {512, 16, 1, 0};
+  return {256, 4, 3, 1};
+}
 constexpr int kDefaultGroups = 8;
 
 template <class OpT, class AccT>
@@ -383,13 +407,14 @@ void Workspace::reset(hipStream_t stream) {
 LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cfg, int num_cus,
                        int max_grid) {
   LaunchPlan p;
-  p.block = cfg.block ? cfg.block : kDefaultBlock;
-  p.unroll = cfg.unroll ? cfg.unroll : kDefaultUnroll;
-  p.nontemporal = cfg.nontemporal;
-  p.single_pass = cfg.single_pass;
-  MIREDUCE_REQUIRE(block_index(p.block) >= 0, "block must be 256 or 512");
-  MIREDUCE_REQUIRE(unroll_index(p.unroll) >= 0, "unroll must be 2, 4 or 8");
   const size_t es = dtype_size(t);
+  const Defaults d = tuned_defaults(n * es, es);
+  p.block = cfg.block ? cfg.block : d.block;
+  p.unroll = cfg.unroll ? cfg.unroll : d.unroll;
+  p.nontemporal = cfg.policy < 0 ? d.policy == 1 : cfg.policy == 1;
+  p.single_pass = cfg.single_pass;
+  MIREDUCE_REQUIRE(block_index(p.block) >= 0, "block must be 256, 512 or 1024");
+  MIREDUCE_REQUIRE(unroll_index(p.unroll) >= 0, "unroll must be 2, 4, 8 or 16");
   const size_t vec = 16 / es;
   const uintptr_t addr = reinterpret_cast<uintptr_t>(in);
   MIREDUCE_REQUIRE(n == 0 || addr % es == 0, "input pointer is not aligned to its element size");
@@ -399,7 +424,9 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   p.head = head;
   p.nvec = (n - head) / vec;
   p.tail = (n - head) - p.nvec * vec;
-  const int wg_per_cu = cfg.wg_per_cu ? cfg.wg_per_cu : kDefaultWgPerCu * 256 / p.block;
+  // wg_per_cu given without block: keep the thread count per CU of the tuned point.
+  int wg_per_cu = cfg.wg_per_cu;
+  if (!wg_per_cu) wg_per_cu = cfg.block ? std::max(1, d.wg_per_cu * d.block / p.block) : d.wg_per_cu;
   const uint64_t tile = static_cast<uint64_t>(p.block) * p.unroll;
   uint64_t want = (p.nvec + tile - 1) / tile;
   const uint64_t cap = static_cast<uint64_t>(num_cus) * wg_per_cu;

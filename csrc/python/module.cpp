@@ -44,14 +44,14 @@ py::dict plan_dict(const LaunchPlan& p) {
 }
 
 ReduceConfig make_cfg(int block, int unroll, int wg_per_cu, int max_blocks, int groups,
-                      bool nontemporal, bool single_pass) {
+                      int policy, bool single_pass) {
   ReduceConfig c;
   c.block = block;
   c.unroll = unroll;
   c.wg_per_cu = wg_per_cu;
   c.max_blocks = max_blocks;
   c.groups = groups;
-  c.nontemporal = nontemporal;
+  c.policy = policy;
   c.single_pass = single_pass;
   return c;
 }
@@ -128,38 +128,38 @@ PYBIND11_MODULE(_C, m) {
       "reduce",
       [](Workspace& ws, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out,
          uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks, int groups,
-         bool nontemporal, bool single_pass) {
+         int policy, bool single_pass) {
         const LaunchPlan p = reduce(as_ptr<const void>(in), n, static_cast<DType>(dtype),
                                     static_cast<Op>(op), static_cast<DType>(acc),
                                     as_ptr<void>(out), ws, as_stream(stream),
                                     make_cfg(block, unroll, wg_per_cu, max_blocks, groups,
-                                             nontemporal, single_pass));
+                                             policy, single_pass));
         return plan_dict(p);
       },
       py::arg("ws"), py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"),
       py::arg("acc"), py::arg("out_ptr"), py::arg("stream") = 0, py::arg("block") = 0,
       py::arg("unroll") = 0, py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0,
-      py::arg("groups") = 0, py::arg("nontemporal") = true, py::arg("single_pass") = true);
+      py::arg("groups") = 0, py::arg("policy") = -1, py::arg("single_pass") = true);
 
   m.def(
       "plan",
       [](uintptr_t in, uint64_t n, int dtype, int num_cus, int max_grid, int block, int unroll,
-         int wg_per_cu, int max_blocks, int groups, bool nontemporal, bool single_pass) {
+         int wg_per_cu, int max_blocks, int groups, int policy, bool single_pass) {
         return plan_dict(plan_reduce(as_ptr<const void>(in), n, static_cast<DType>(dtype),
                                      make_cfg(block, unroll, wg_per_cu, max_blocks, groups,
-                                              nontemporal, single_pass),
+                                              policy, single_pass),
                                      num_cus, max_grid));
       },
       py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("num_cus") = 256,
       py::arg("max_grid") = 16384, py::arg("block") = 0, py::arg("unroll") = 0,
       py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0, py::arg("groups") = 0,
-      py::arg("nontemporal") = true, py::arg("single_pass") = true);
+      py::arg("policy") = -1, py::arg("single_pass") = true);
 
   m.def(
       "reduce_partials",
       [](uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t partials, int max_grid,
-         int num_cus, uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks) {
-        ReduceConfig c = make_cfg(block, unroll, wg_per_cu, max_blocks, 0, true, false);
+         int num_cus, uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks, int policy) {
+        ReduceConfig c = make_cfg(block, unroll, wg_per_cu, max_blocks, 0, policy, false);
         return plan_dict(reduce_partials(as_ptr<const void>(in), n, static_cast<DType>(dtype),
                                          static_cast<Op>(op), static_cast<DType>(acc),
                                          as_ptr<void>(partials), max_grid, num_cus,
@@ -168,7 +168,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"), py::arg("acc"),
       py::arg("partials_ptr"), py::arg("max_grid"), py::arg("num_cus"), py::arg("stream") = 0,
       py::arg("block") = 0, py::arg("unroll") = 0, py::arg("wg_per_cu") = 0,
-      py::arg("max_blocks") = 0);
+      py::arg("max_blocks") = 0, py::arg("policy") = -1);
 
   m.def(
       "reduce_finalize",

@@ -65,8 +65,12 @@ class KernelConfig:
     wg_per_cu: int = 0
     max_blocks: int = 0
     groups: int = 0
-    nontemporal: bool = True
+    nontemporal: Optional[bool] = None  # None: size-dependent tuned choice
     single_pass: bool = True
+
+    @property
+    def policy(self) -> int:
+        return -1 if self.nontemporal is None else int(bool(self.nontemporal))
 
     def kwargs(self) -> dict:
         return dict(
@@ -75,7 +79,7 @@ class KernelConfig:
             wg_per_cu=self.wg_per_cu,
             max_blocks=self.max_blocks,
             groups=self.groups,
-            nontemporal=self.nontemporal,
+            policy=self.policy,
             single_pass=self.single_pass,
         )
 
@@ -204,6 +208,7 @@ def reduce_partials(x: torch.Tensor, op: str = "sum", acc_dtype=None, max_grid: 
         x.data_ptr(), x.numel(), dtype_code(x.dtype), op_code(op), dtype_code(acc), parts.data_ptr(),
         max_grid, info.multi_processor_count, _stream_handle(x.device, None),
         block=cfg.block, unroll=cfg.unroll, wg_per_cu=cfg.wg_per_cu, max_blocks=cfg.max_blocks,
+        policy=cfg.policy,
     )
     return parts[: plan["grid"]], plan
 

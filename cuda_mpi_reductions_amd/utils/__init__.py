@@ -1,1 +1,2 @@
-"""Reference-compatible CLI grammar, output formats, averaging and timing helpers."""
+"""Reference-compatible CLI grammar, output formats, averaging and plotting helpers."""
+from . import cli, formats, getavgs  # noqa: F401

@@ -1,0 +1,38 @@
+"""Shared helpers for the CPU test suite."""
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "build", "bin")
+MPIRUN = "/opt/conda/bin/mpirun"
+
+_built = False
+
+
+def ensure_built():
+    """Build the native tree once per session (no-op when up to date)."""
+    global _built
+    if not _built:
+        subprocess.run(["make", "-C", ROOT, "-j8", "all"], check=True, stdout=subprocess.DEVNULL)
+        _built = True
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run(cmd, timeout=300, cwd=None, env=None):
+    e = dict(os.environ)
+    if env:
+        e.update(env)
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=cwd, env=e)
+
+
+def torchrun(nproc, script_args, timeout=600, cwd=None):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port())] + script_args
+    return run(cmd, timeout=timeout, cwd=cwd)

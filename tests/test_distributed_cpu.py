@@ -1,0 +1,126 @@
+"""Multi-process correctness of the distributed layer on gloo (world_size 2 and 4): the same
+code paths bench.py runs over RCCL on GPUs."""
+import json
+import os
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from helpers import ROOT, free_port, torchrun
+
+
+def _worker(rank, world, port, fn_name, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        q.put((rank, globals()[fn_name](rank, world)))
+    except Exception as e:  # pragma: no cover - surfaced by the assertion in the parent
+        q.put((rank, repr(e)))
+
+
+def _spawn(fn_name, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn_name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    return out
+
+
+def scalar_case(rank, world):
+    from dataclasses import replace
+    from cuda_mpi_reductions_amd.models import CONFIGS, ScalarReduction
+    from cuda_mpi_reductions_amd.parallel import dist as pdist
+    ctx = pdist.init(device_type="cpu")
+    res = {}
+    for name, n in (("xgmi_1b_double_sum", 1_000_003), ("gpu_256m_int64_min", 100_001)):
+        cfg = replace(CONFIGS[name], n_total=n)
+        wl = ScalarReduction(cfg, ctx).setup()
+        out = wl.new_slots(1)
+        w = wl.step(out)
+        if w is not None:
+            w.wait()
+        res[name] = wl.verify(out)
+    # the global value is independent of the rank count: compare with a 1-rank host reduction
+    from cuda_mpi_reductions_amd.ops import synthetic, cpu_reduce
+    full = synthetic(1_000_003, torch.float64)
+    res["global_matches_whole_array"] = abs(res["xgmi_1b_double_sum"]["got"] - cpu_reduce(full)) < 1e-6
+    pdist.shutdown(ctx)
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_scalar_reduction_multi_rank(world):
+    out = _spawn("scalar_case", world)
+    for rank, res in out.items():
+        assert isinstance(res, dict), res
+        assert res["xgmi_1b_double_sum"]["ok"], res
+        assert res["gpu_256m_int64_min"]["ok"], res
+        assert res["global_matches_whole_array"]
+    # all ranks hold the same global value
+    vals = {res["xgmi_1b_double_sum"]["got"] for res in out.values()}
+    assert len(vals) == 1
+
+
+def vector_case(rank, world):
+    from dataclasses import replace
+    from cuda_mpi_reductions_amd.models import CONFIGS, VectorReduction
+    from cuda_mpi_reductions_amd.parallel import dist as pdist
+    ctx = pdist.init(device_type="cpu")
+    cfg = replace(CONFIGS["mpi_1m_int32_sum_cpu2"], n_total=1 << 16)
+    out = {}
+    for op in ("sum", "min", "max"):
+        wl = VectorReduction(replace(cfg, op=op), ctx).setup(mt19937=True)
+        wl.step()
+        # independent check: gather every rank's input and combine on rank 0
+        gathered = [torch.empty_like(wl.x) for _ in range(world)]
+        torch.distributed.all_gather(gathered, wl.x)
+        if rank == 0:
+            st = torch.stack(gathered).long()
+            if op == "sum":
+                exp = st.sum(0)
+                exp = ((exp + 2**31) % 2**32 - 2**31).int()   # MPI_INT wraps
+            elif op == "min":
+                exp = st.min(0).values.int()
+            else:
+                exp = st.max(0).values.int()
+            out[op] = bool(torch.equal(exp, wl.y))
+    pdist.shutdown(ctx)
+    return out
+
+
+def test_vector_reduce_c_semantics_two_ranks():
+    out = _spawn("vector_case", 2)
+    assert out[0] == {"sum": True, "min": True, "max": True}
+
+
+def test_shard_covers_everything():
+    from cuda_mpi_reductions_amd.parallel.dist import shard
+    for n in (0, 1, 7, 1000, 10**9 + 3):
+        for w in (1, 2, 3, 8):
+            parts = [shard(n, r, w) for r in range(w)]
+            assert parts[0][0] == 0 and sum(c for _, c in parts) == n
+            for (o1, c1), (o2, _) in zip(parts, parts[1:]):
+                assert o1 + c1 == o2
+            assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+
+
+def test_bench_contract_on_cpu_ranks(tmp_path):
+    r = torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "1",
+                     "--device", "cpu", "--elements", "200003"], cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+    assert d["n_gpus"] == 2 and d["steps"] == 4 and d["warmup"] == 1 and d["verified"] is True
+    assert d["metric"] == "reduction bandwidth (GB/s, whole node), 1B-double sum at 1/2/4/8 MI355X"
+    assert d["scaling"] == "strong" and d["config"]["parallelism"] == "dp2"
+    assert abs(d["value"] - d["config"]["bytes_per_step"] * 4 / (d["ms_per_step"] * 4e-3) / 1e9) / d["value"] < 0.01

@@ -1,0 +1,90 @@
+"""Launch planning (host side of csrc/kernels/reduce.hip and ladder.hip)."""
+import pytest
+
+from cuda_mpi_reductions_amd._native import native
+
+F64 = 3
+
+
+def test_head_body_tail_split():
+    C = native()
+    for addr in (0x1000, 0x1008):
+        for n in (0, 1, 2, 3, 5, 1001):
+            p = C.plan(addr, n, F64)
+            head = 0 if addr % 16 == 0 else min(1, n)
+            assert p["head"] == head
+            assert p["head"] + 2 * p["nvec"] + p["tail"] == n
+            assert 0 <= p["tail"] < 2
+
+
+def test_int32_vector_split():
+    C = native()
+    p = C.plan(0x1004, 1003, 0)          # int32, 4-byte aligned only
+    assert p["head"] == 3 and p["head"] + 4 * p["nvec"] + p["tail"] == 1003
+
+
+def test_misaligned_element_rejected():
+    C = native()
+    with pytest.raises(C.NativeError):
+        C.plan(0x1001, 10, F64)
+
+
+@pytest.mark.parametrize("n", [0, 1, 100, 10**6, 10**9, 3 * 10**9])
+def test_grid_bounds_and_groups(n):
+    C = native()
+    p = C.plan(0, n, F64, num_cus=256)
+    assert 1 <= p["grid"] <= 256 * 8
+    assert 1 <= p["groups"] <= min(64, p["grid"])
+    tile = p["block"] * p["unroll"]
+    assert p["grid"] <= max(1, -(-p["nvec"] // tile))
+
+
+def test_tuned_defaults_by_size():
+    C = native()
+    big = C.plan(0, 10**9, F64)            # 8 GB of 8-byte elements
+    assert (big["block"], big["unroll"], big["grid"], big["nontemporal"]) == (512, 16, 256, True)
+    mid = C.plan(0, 125_000_000, F64)      # 1 GB: the 8-GPU shard of the north star
+    assert (mid["block"], mid["unroll"], mid["grid"], mid["nontemporal"]) == (256, 2, 768, True)
+    l3 = C.plan(0, 1 << 25, F64)           # 256 MB: Infinity-Cache resident
+    assert l3["nontemporal"] is False
+    f32 = C.plan(0, 2 * 10**9, 2)          # 8 GB of fp32
+    assert (f32["block"], f32["unroll"]) == (256, 2)
+
+
+def test_overrides_and_caps():
+    C = native()
+    p = C.plan(0, 10**9, F64, block=1024, unroll=8, wg_per_cu=2, max_blocks=100, groups=64, policy=0)
+    assert (p["block"], p["unroll"], p["grid"], p["groups"], p["nontemporal"]) == (1024, 8, 100, 64, False)
+    p = C.plan(0, 10**9, F64, single_pass=False)
+    assert p["groups"] == 0 and p["single_pass"] is False
+    with pytest.raises(C.NativeError):
+        C.plan(0, 10, F64, block=384)
+    with pytest.raises(C.NativeError):
+        C.plan(0, 10, F64, unroll=3)
+
+
+def next_pow2(x):
+    return 1 if x <= 1 else 1 << (x - 1).bit_length()
+
+
+@pytest.mark.parametrize("kernel", range(7))
+@pytest.mark.parametrize("n", [1, 2, 33, 64, 1000, 1 << 20, (1 << 24) + 3])
+def test_ladder_geometry_matches_reference_planner(kernel, n):
+    # getNumBlocksAndThreads (cuda/C/src/reduction/reduction.cpp:272-291), with a one-wave floor.
+    C = native()
+    mt, mb = 256, 64
+    if kernel < 3:
+        t = next_pow2(n) if n < mt else mt
+        b = -(-n // t)
+    else:
+        t = next_pow2((n + 1) // 2) if n < 2 * mt else mt
+        b = -(-n // (t * 2))
+    if kernel == 6:
+        b = min(mb, b)
+    assert C.ladder_geometry(kernel, n, mt, mb) == (max(b, 1), max(t, 64))
+
+
+def test_compiled_variants_cover_grid():
+    v = native().compiled_variants()
+    assert len(v) == 3 * 4 * 2
+    assert "block=512 unroll=16 policy=nt" in v

@@ -37,13 +37,45 @@ struct SumOp {
 
 // MIN/MAX on floats follow IEEE-754 minNum/maxNum (a NaN operand is ignored), which is what
 // v_min_f64 / v_max_f32 implement and what std::fmin/std::fmax do on the host.
+//
+// On the device the instructions are emitted directly: llvm.minnum in IEEE mode makes hipcc
+// canonicalise every operand first (an extra `v_max_f64 x, x, x` per element, which doubled the
+// VALU work of the MIN/MAX streaming loop). The hardware ops already return the non-NaN operand
+// for quiet NaNs; only signalling-NaN inputs (never produced by arithmetic) would differ.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ double hw_min(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double hw_max(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float hw_min(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float hw_max(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+#endif
+
 struct MinOp {
   template <class T> MIREDUCE_HD static T identity() {
     if constexpr (std::is_floating_point_v<T>) return std::numeric_limits<T>::infinity();
     else return std::numeric_limits<T>::max();
   }
   template <class T> MIREDUCE_HD static T apply(T a, T b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (std::is_floating_point_v<T>) return hw_min(a, b);
+#else
     if constexpr (std::is_floating_point_v<T>) return std::fmin(a, b);
+#endif
     else return b < a ? b : a;
   }
 };
@@ -54,7 +86,11 @@ struct MaxOp {
     else return std::numeric_limits<T>::lowest();
   }
   template <class T> MIREDUCE_HD static T apply(T a, T b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (std::is_floating_point_v<T>) return hw_max(a, b);
+#else
     if constexpr (std::is_floating_point_v<T>) return std::fmax(a, b);
+#endif
     else return a < b ? b : a;
   }
 };

@@ -314,20 +314,22 @@ const Table& table() {
   return tb;
 }
 
-// Tuned gfx950 defaults, measured on MI355X with tools/tune.py (interleaved rounds, one process;
-// profiles/r1_tuning/). Median read bandwidth of the chosen point vs the best point per size:
-//   8 GB f64 sum   512 x 16, 1 WG/CU, nt   7.29 TB/s (best)
-//   1 GB f64 sum   256 x  2, 3 WG/CU, nt   7.12 TB/s (best)      2 GB i64 min: 7.21 (best)
-//   8 GB f32 sum   256 x  2, 3 WG/CU, nt   7.20 TB/s (best 7.21)
-//   256 MB         512 x 16, 1 WG/CU, default policy (Infinity-Cache re-reads) 6.72 TB/s (best)
-//   128 MB         256 x  4, 3 WG/CU, nt   6.10 TB/s (best; launch + tail dominate)
+// Tuned gfx950 defaults, measured on MI355X with tools/tune.py (interleaved rounds in one
+// process; profiles/r1_tuning/). Median read bandwidth of the chosen point:
+//   8 GB f64 sum / min  512 x 16, 1 WG/CU, nt   7.29 / 7.38 TB/s (best point for both)
+//   1 GB f64 sum        256 x  2, 3 WG/CU, nt   7.12 TB/s (best)
+//   8 GB i64 max        256 x  2, 3 WG/CU, nt   7.30 TB/s (best; 512 x 16 x 1 is not in the top 8)
+//   8 GB f32 sum / max  256 x  2, 3 WG/CU, nt   7.20 / 7.25 TB/s (best 7.21 / 7.25)
+//   8 GB i32 sum        256 x  2, 3 WG/CU, nt   7.20 TB/s (best 7.25)
+//   256 MB              512 x 16, 1 WG/CU, default policy (Infinity-Cache re-reads) 6.72 TB/s
+//   128 MB              256 x  4, 3 WG/CU, nt   6.10 TB/s (best; launch + tail dominate)
 // Fewer, fatter workgroups beat the "fill every wave slot" grid (8 WG/CU: 6.91 TB/s at 8 GB).
 struct Defaults {
   int block, unroll, wg_per_cu, policy;
 };
-Defaults tuned_defaults(size_t bytes, size_t elem_size) {
+Defaults tuned_defaults(size_t bytes, DType t) {
   constexpr size_t MB = 1ull << 20;
-  if (elem_size == 8 && bytes >= 3072 * MB) return {512, 16, 1, 1};
+  if (t == DType::Float64 && bytes >= 3072 * MB) return {512, 16, 1, 1};
   if (bytes > 384 * MB) return {256, 2, 3, 1};
   if (bytes > 192 * MB) return {512, 16, 1, 0};
   return {256, 4, 3, 1};
@@ -408,7 +410,7 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
                        int max_grid) {
   LaunchPlan p;
   const size_t es = dtype_size(t);
-  const Defaults d = tuned_defaults(n * es, es);
+  const Defaults d = tuned_defaults(n * es, t);
   p.block = cfg.block ? cfg.block : d.block;
   p.unroll = cfg.unroll ? cfg.unroll : d.unroll;
   p.nontemporal = cfg.policy < 0 ? d.policy == 1 : cfg.policy == 1;

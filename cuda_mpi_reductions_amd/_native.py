@@ -9,6 +9,12 @@ from __future__ import annotations
 import importlib
 import os
 
+# torch must be imported BEFORE the extension: torch ships its own libamdhip64, and _C must bind
+# to that same HIP runtime (same soname, already loaded) instead of pulling /opt/rocm's copy into
+# the process as a second runtime — two runtimes in one process cannot share a device
+# ("no ROCm-capable device is detected" from the second one).
+import torch  # noqa: F401
+
 _C = None
 _ERR: Exception | None = None
 

@@ -88,3 +88,18 @@ def test_compiled_variants_cover_grid():
     v = native().compiled_variants()
     assert len(v) == 3 * 4 * 2
     assert "block=512 unroll=16 policy=nt" in v
+
+
+def test_single_hip_runtime_in_process():
+    # Regression: importing the package before torch used to load /opt/rocm's libamdhip64 next to
+    # torch's own copy (two HIP runtimes -> "no ROCm-capable device" on the GPU box).
+    import subprocess
+    import sys
+    code = ("import cuda_mpi_reductions_amd, torch, re\n"
+            "maps = open('/proc/self/maps').read()\n"
+            "libs = sorted(set(re.findall(r'(/\\S*libamdhip64\\.so[.0-9]*)', maps)))\n"
+            "print(len(libs), libs)\n")
+    from helpers import ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("1 "), r.stdout

@@ -148,21 +148,27 @@ class ScalarReduction:
         return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op)
 
     # ------------------------------------------------------------------ verify
-    def reference(self):
-        """Independent global result: torch's own reduction of each shard, combined across
-        ranks in fp64 / int64 (parity: the CPU check of reduction.cpp:748-780)."""
+    def reference(self, chunk: int = 1 << 28):
+        """Independent global result: torch's own reduction of each shard (in chunks, so HBM-filling
+        arrays need no full-size temporaries), combined across ranks in fp64 / int64 (parity: the
+        CPU check of reduction.cpp:748-780)."""
         x = self.x
+        dev = x.device
         if self.cfg.op == "sum":
-            if x.dtype.is_floating_point:
-                loc = x.sum(dtype=torch.float64).reshape(1)
-                absl = x.abs().sum(dtype=torch.float64).reshape(1)
-            else:
-                loc = x.sum(dtype=torch.int64).reshape(1)
-                absl = x.abs().sum(dtype=torch.float64).reshape(1)
-        elif self.cfg.op == "min":
-            loc, absl = x.min().reshape(1), torch.zeros(1, dtype=torch.float64, device=x.device)
+            acc_dt = torch.float64 if x.dtype.is_floating_point else torch.int64
+            loc = torch.zeros(1, dtype=acc_dt, device=dev)
+            absl = torch.zeros(1, dtype=torch.float64, device=dev)
+            for i in range(0, x.numel(), chunk):
+                c = x[i:i + chunk]
+                loc += c.sum(dtype=acc_dt)
+                absl += c.abs().sum(dtype=torch.float64) if c.dtype.is_floating_point else \
+                    c.abs().to(torch.float64).sum()
         else:
-            loc, absl = x.max().reshape(1), torch.zeros(1, dtype=torch.float64, device=x.device)
+            parts = [(x[i:i + chunk].min() if self.cfg.op == "min" else x[i:i + chunk].max()).reshape(1)
+                     for i in range(0, x.numel(), chunk)]
+            st = torch.cat(parts)
+            loc = (st.min() if self.cfg.op == "min" else st.max()).reshape(1)
+            absl = torch.zeros(1, dtype=torch.float64, device=dev)
         if self.ctx.world_size > 1:
             torch.distributed.all_reduce(loc, op=pdist.reduce_op(self.cfg.op))
             torch.distributed.all_reduce(absl)

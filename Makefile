@@ -43,8 +43,8 @@ COMMLIB     := $(BUILD)/lib/libmireduce_comm.a
 APPS := $(BUILD)/bin/reduction $(BUILD)/bin/reduce_xgmi $(BUILD)/bin/bandwidth_test
 MPI_APP := $(BUILD)/bin/reduce_mpi
 
-.PHONY: all python apps mpi clean asan
-all: python apps mpi
+.PHONY: all python apps mpi clean asan unit
+all: python apps mpi unit
 
 python: $(PYEXT)
 apps: $(APPS)
@@ -90,6 +90,20 @@ $(MPI_APP): $(MPI_SRCS) $(HEADERS)
 	@mkdir -p $(dir $@)
 	g++ $(CXXSTD) -O3 -Wall -Icsrc/include -DMIREDUCE_NO_HIP -I$(MPI_HOME)/include \
 	    $(MPI_SRCS) -static-libstdc++ -static-libgcc $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,$(MPI_HOME)/lib -o $@
+
+# Native unit tests (host code only) and the bootstrap multi-process test.
+UNIT := $(BUILD)/bin/host_unit $(BUILD)/bin/bootstrap_test
+unit: $(UNIT)
+
+$(BUILD)/bin/host_unit: tests/native/host_unit.cpp $(filter-out csrc/apps/reduce_mpi.cpp,$(MPI_SRCS)) $(HEADERS)
+	@mkdir -p $(dir $@)
+	g++ $(CXXSTD) -O2 -Wall -Icsrc/include -DMIREDUCE_NO_HIP tests/native/host_unit.cpp \
+	    $(filter-out csrc/apps/reduce_mpi.cpp,$(MPI_SRCS)) -o $@
+
+$(BUILD)/bin/bootstrap_test: tests/native/bootstrap_test.cpp $(COMMLIB) $(LIB) $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HOSTCXX) $(HOSTFLAGS) $< -Wl,--whole-archive $(COMMLIB) $(LIB) -Wl,--no-whole-archive \
+	    -L$(ROCM)/lib -lrccl $(LDLIBS) -o $@
 
 # Host sanitizers: CPU-only code paths under ASan+UBSan.
 asan: csrc/apps/reduce_mpi.cpp

@@ -50,6 +50,9 @@ def parse_args(argv=None):
     p.add_argument("--policy", choices=["auto", "nt", "default"], default="auto")
     p.add_argument("--two-pass", action="store_true")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
+                   help="auto: nccl (RCCL) on GPUs, gloo on CPU; gloo + MIREDUCE_FORCE_DEVICE=0 rehearses "
+                        "N ranks on one GPU")
     p.add_argument("--device", choices=["auto", "cuda", "cpu"], default="auto",
                    help="cpu: gloo ranks + the native host reducer (tests of the contract only)")
     return p.parse_args(argv)
@@ -64,7 +67,7 @@ def main(argv=None) -> int:
     args = parse_args(argv)
     native()  # fail loudly if the HIP extension is missing
     device_type = None if args.device == "auto" else args.device
-    ctx = pdist.init(device_type=device_type)
+    ctx = pdist.init(backend=None if args.backend == "auto" else args.backend, device_type=device_type)
     if args.gpus != ctx.world_size and ctx.is_root:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}; using {ctx.world_size}",
               file=sys.stderr)
@@ -142,6 +145,7 @@ def main(argv=None) -> int:
                 "global_batch": wl.n_total,
                 "seq_len": 1,
                 "parallelism": f"dp{ctx.world_size}",
+                "backend": ctx.backend,
                 "n_total_elements": wl.n_total,
                 "bytes_per_step": bytes_step,
                 "op": cfg.op.upper(),

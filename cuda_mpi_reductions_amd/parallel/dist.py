@@ -70,8 +70,11 @@ def init(backend: Optional[str] = None, device_type: Optional[str] = None,
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     if device_type == "cuda":
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        # MIREDUCE_FORCE_DEVICE pins every rank to one GPU: a rehearsal of the multi-rank GPU path
+        # on a 1-GPU box (with backend gloo — RCCL refuses two ranks on one device).
+        dev_index = int(os.environ.get("MIREDUCE_FORCE_DEVICE", local_rank))
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
     else:
         device = torch.device("cpu")
     owns = False
@@ -106,7 +109,7 @@ def shard(n_total: int, rank: int, world: int) -> tuple[int, int]:
 def barrier(ctx: DistContext) -> None:
     if ctx.world_size > 1 or dist.is_initialized():
         if ctx.backend == "nccl":
-            dist.barrier(device_ids=[ctx.local_rank])
+            dist.barrier(device_ids=[ctx.device.index])
         else:
             dist.barrier()
 
@@ -130,6 +133,7 @@ def max_over_ranks(value: float, ctx: DistContext) -> float:
     """MAX of a host float over all ranks (timing: the slowest rank defines the step)."""
     if ctx.world_size == 1:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=ctx.device)
+    t = torch.tensor([value], dtype=torch.float64,
+                     device=ctx.device if ctx.backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -1,0 +1,120 @@
+// Host-only unit tests of the native runtime (CLI grammar, MT19937, report formats, stats, JSON,
+// count parsing). Built twice: plainly (`make unit`) and under ASan+UBSan (`make asan`).
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "mireduce/cli.hpp"
+#include "mireduce/mt19937.hpp"
+#include "mireduce/report.hpp"
+#include "mireduce/timer.hpp"
+#include "mireduce/types.hpp"
+
+using namespace mireduce;
+
+static int g_fail = 0;
+#define CHECK(c)                                                          \
+  do {                                                                    \
+    if (!(c)) {                                                           \
+      std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      ++g_fail;                                                           \
+    }                                                                     \
+  } while (0)
+
+static void test_cli() {
+  const char* argv[] = {"prog", "--method=SUM", "-type=double", "--cpufinal", "-n=16M", "--list=a,b,,c", "--neg=-5"};
+  CmdArgs a(7, argv);
+  std::string s;
+  CHECK(a.program() == "prog");
+  CHECK(a.get_str("method", &s) && s == "SUM");
+  CHECK(a.get_str("type", &s) && s == "double");
+  CHECK(a.has("cpufinal") && !a.get_str("cpufinal", &s));
+  uint64_t n = 0;
+  CHECK(a.get_uint("n", &n) && n == (16ull << 20));
+  std::vector<std::string> l;
+  CHECK(a.get_list("list", &l) && l.size() == 3 && l[2] == "c");
+  int64_t v = 0;
+  CHECK(a.get_int("neg", &v) && v == -5);
+  CHECK(a.unknown({"method", "type", "cpufinal", "n", "list"}).size() == 1);
+  bool threw = false;
+  try {
+    const char* bad[] = {"prog", "method=SUM"};
+    CmdArgs b(2, bad);
+  } catch (const CliError&) {
+    threw = true;
+  }
+  CHECK(threw);
+  threw = false;
+  try {
+    const char* bad[] = {"prog", "--n=12x"};
+    CmdArgs b(2, bad);
+    uint64_t x;
+    b.get_uint("n", &x);
+  } catch (const CliError&) {
+    threw = true;
+  }
+  CHECK(threw);
+  uint64_t c = 0;
+  CHECK(parse_count("1e9", &c) && c == 1000000000ull);
+  CHECK(parse_count("4k", &c) && c == 4096);
+  CHECK(parse_count("2G", &c) && c == (2ull << 30));
+  CHECK(!parse_count("abc", &c) && !parse_count("1.5e0", &c));
+}
+
+static void test_types() {
+  DType t;
+  Op o;
+  CHECK(parse_dtype("DOUBLE", &t) && t == DType::Float64);
+  CHECK(parse_dtype("Int", &t) && t == DType::Int32);
+  CHECK(parse_dtype("int64", &t) && t == DType::Int64);
+  CHECK(!parse_dtype("char", &t));
+  CHECK(parse_op_strict("SUM", &o) && o == Op::Sum);
+  CHECK(!parse_op_strict("sum", &o));
+  CHECK(parse_op("max", &o) && o == Op::Max);
+  CHECK(default_acc(DType::Int32, Op::Sum) == DType::Int64);
+  CHECK(default_acc(DType::Float32, Op::Min) == DType::Float32);
+  CHECK(std::string(dtype_gnuplot_name(DType::Float64)) == "DOUBLE");
+}
+
+static void test_mt() {
+  Mt19937 g;
+  const uint64_t key[4] = {0x123, 0x234, 0x345, 0x456};
+  g.init_by_array(key, 4);
+  const uint32_t expect[5] = {1067595299u, 955945823u, 477289528u, 4107218783u, 4228976476u};
+  for (uint32_t e : expect) CHECK(g.genrand_int32() == e);
+  Mt19937 h(5489u);
+  CHECK(h.genrand_int32() == 3499211612u);  // std::mt19937 default-seed first output
+}
+
+static void test_report() {
+  CHECK(gnuplot_header() == "# DATATYPE OP NODES GB/sec");
+  CHECK(gnuplot_line("INT", "SUM", 1024, 146.684) == "INT SUM 1024    146.684");
+  CHECK(throughput_line(92.7729, 0.00072, 16777216, 1, 256) ==
+        "Reduction, Throughput = 92.7729 GB/s, Time = 0.00072 s, Size = 16777216 Elements, NumDevsUsed = 1, Workgroup = 256");
+  Stats s = compute_stats({3, 1, 2, 4});
+  CHECK(s.count == 4 && s.min == 1 && s.max == 4 && s.median == 2.5 && std::fabs(s.mean - 2.5) < 1e-12);
+  Json j;
+  j.set("a", "x\"y").set("b", 1.5).set("c", static_cast<int64_t>(-3)).set("d", true).set("e", std::vector<double>{1, 2});
+  CHECK(j.str() == "{\"a\": \"x\\\"y\", \"b\": 1.5, \"c\": -3, \"d\": true, \"e\": [1,2]}");
+  StopWatch w;
+  w.start();
+  w.stop();
+  w.start();
+  w.stop();
+  CHECK(w.sessions() == 2 && w.laps_ms().size() == 2 && w.average_ms() >= 0);
+}
+
+int main() {
+  test_cli();
+  test_types();
+  test_mt();
+  test_report();
+  if (g_fail) {
+    std::fprintf(stderr, "host_unit: %d failures\n", g_fail);
+    return 1;
+  }
+  std::printf("host_unit: all checks passed\n");
+  return 0;
+}

@@ -1,0 +1,69 @@
+"""Native C++ unit tests (host code), the TCP bootstrap under torchrun and mpirun, host
+sanitizers (ASan/UBSan on host code), and the resumable sweep orchestration."""
+import os
+import subprocess
+
+import pytest
+
+from helpers import BIN, MPIRUN, ROOT, ensure_built, free_port, run, torchrun
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    ensure_built()
+
+
+def test_host_unit():
+    r = run([os.path.join(BIN, "host_unit")])
+    assert r.returncode == 0, r.stderr
+    assert "all checks passed" in r.stdout
+
+
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_bootstrap_torchrun(nproc):
+    r = torchrun(nproc, ["--no-python", os.path.join(BIN, "bootstrap_test")], timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert f"bootstrap_test world={nproc} launcher=torchrun PASSED" in r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="MPICH not available")
+def test_bootstrap_mpirun():
+    r = run([MPIRUN, "-np", "3", os.path.join(BIN, "bootstrap_test")], timeout=180,
+            env={"MIREDUCE_BOOTSTRAP_PORT": str(free_port())})
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "bootstrap_test world=3 launcher=mpich PASSED" in r.stdout
+
+
+def test_host_sanitizers():
+    subprocess.run(["make", "-C", ROOT, "asan"], check=True, stdout=subprocess.DEVNULL)
+    r = run([os.path.join(ROOT, "build", "asan", "host_unit")], env={"ASAN_OPTIONS": "detect_leaks=1"})
+    assert r.returncode == 0, r.stderr
+    if os.path.exists(MPIRUN):
+        r = run([MPIRUN, "-np", "2", os.path.join(ROOT, "build", "asan", "reduce_mpi"), "--ints=64k",
+                 "--doubles=64k", "--retries=1", "--verify"], timeout=300, env={"ASAN_OPTIONS": "detect_leaks=0"})
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="MPICH not available")
+def test_sweep_resume_and_collect(tmp_path):
+    out = tmp_path / "sweep"
+    cmd = ["python", os.path.join(ROOT, "tools", "sweep.py"), "--app", "reduce_mpi", "--ranks", "1,2",
+           "--out", str(out), "--", "--ints=16k", "--doubles=16k", "--retries=2"]
+    r = run(cmd, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert (out / "stdout-reduce_mpi-P2.txt").exists() and (out / "results" / "DOUBLE_MAX.txt").exists()
+    res = (out / "results" / "INT_SUM.txt").read_text().splitlines()
+    assert res[0] == "" and [ln.split()[2] for ln in res[1:]] == ["1", "2"]
+    r2 = run(cmd, timeout=300)
+    assert "P=1: done, skipping" in r2.stdout and "P=2: done, skipping" in r2.stdout
+
+
+def test_plot_tool(tmp_path):
+    res = tmp_path / "results"
+    res.mkdir()
+    (res / "INT_SUM.txt").write_text("\nINT SUM 1 100.0\nINT SUM 2 190.0\n")
+    r = run(["python", os.path.join(ROOT, "tools", "plot.py"), "--results", str(res), "--out", str(tmp_path / "p"),
+             "--reference-cuda"], timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "p" / "int.png").exists()

@@ -23,7 +23,7 @@ WARN      := -Wall -Wno-unused-result
 COMMON    := $(CXXSTD) $(OPT) $(WARN) -fPIC $(INCLUDES)
 HIPFLAGS  := $(COMMON) -x hip --offload-arch=$(ARCH) -munsafe-fp-atomics $(if $(SAVE_TEMPS),-save-temps=obj,)
 HOSTFLAGS := $(COMMON) -D__HIP_PLATFORM_AMD__
-LDLIBS    := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lpthread
+LDLIBS    := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -lpthread
 
 PY_INC    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_paths()['include'])")
 PYBIND_INC:= $(shell $(PYTHON) -c "import pybind11; print(pybind11.get_include())")

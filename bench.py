@@ -50,6 +50,7 @@ def parse_args(argv=None):
     p.add_argument("--policy", choices=["auto", "nt", "default"], default="auto")
     p.add_argument("--two-pass", action="store_true")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--trace", action="store_true", help="roctx range per step (rocprofv3 --marker-trace)")
     p.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
                    help="auto: nccl (RCCL) on GPUs, gloo on CPU; gloo + MIREDUCE_FORCE_DEVICE=0 rehearses "
                         "N ranks on one GPU")
@@ -65,7 +66,8 @@ def _sync(dev: torch.device) -> None:
 
 def main(argv=None) -> int:
     args = parse_args(argv)
-    native()  # fail loudly if the HIP extension is missing
+    C = native()  # fail loudly if the HIP extension is missing
+    C.set_tracing(args.trace)
     device_type = None if args.device == "auto" else args.device
     ctx = pdist.init(backend=None if args.backend == "auto" else args.backend, device_type=device_type)
     if args.gpus != ctx.world_size and ctx.is_root:
@@ -87,7 +89,9 @@ def main(argv=None) -> int:
     def run(first: int, count: int):
         works = []
         for i in range(first, first + count):
+            C.trace_push("bench.step")
             w = wl.step(slots[i:i + 1], async_op=True)
+            C.trace_pop()
             if w is not None:
                 if args.serial:
                     w.wait()

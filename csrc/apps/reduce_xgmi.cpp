@@ -37,6 +37,7 @@
 #include "mireduce/reduce.hpp"
 #include "mireduce/report.hpp"
 #include "mireduce/timer.hpp"
+#include "mireduce/trace.hpp"
 
 using namespace mireduce;
 
@@ -48,7 +49,7 @@ constexpr uint64_t kNumDoubles = 256ull * 1024 * 1024;  // mpi/constants.h:2
 const std::set<std::string> kKnown = {"mode", "collective", "dtypes", "ops", "ints", "doubles", "longs", "floats",
                                       "n", "retries", "warmup", "iters", "root", "json", "graph", "mt19937",
                                       "noverify", "seed", "help", "unroll", "block", "wg-per-cu", "policy",
-                                      "units", "timeout"};
+                                      "units", "timeout", "trace"};
 
 struct Ctx {
   LaunchEnv env;
@@ -189,6 +190,7 @@ bool run_vector(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>&
   HIP_CHECK(hipStreamSynchronize(c.stream));
   auto body_for = [&](B& b, Op o) {
     return [&c, &b, o] {
+      TraceRange tr("reduce_xgmi.vector_collective");
       if (c.collective == "reduce") c.comm->reduce(b.send.get(), b.recv.get(), b.count, b.t, o, c.root, c.stream);
       else c.comm->allreduce(b.send.get(), b.recv.get(), b.count, b.t, o, c.stream);
     };
@@ -254,6 +256,7 @@ bool run_scalar(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>&
     for (Op o : ops) {
       const DType acc = default_acc(t, o);
       auto body = [&] {
+        TraceRange tr("reduce_xgmi.scalar_step");
         reduce(x.get(), count, t, o, acc, out.get(), ws, c.stream, c.kcfg);
         c.comm->allreduce(out.get(), out.get(), 1, acc, o, c.stream);
       };
@@ -375,6 +378,7 @@ int main(int argc, char** argv) {
     c.root = args.int_or<int>("root", c.root);
     c.json = args.str_or("json", "");
     c.graph = args.has("graph");
+    set_tracing(args.has("trace"));
     c.mt = args.has("mt19937");
     c.verify = !args.has("noverify");
     c.seed = args.int_or<uint64_t>("seed", c.seed);

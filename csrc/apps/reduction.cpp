@@ -41,6 +41,7 @@
 #include "mireduce/reduce.hpp"
 #include "mireduce/report.hpp"
 #include "mireduce/timer.hpp"
+#include "mireduce/trace.hpp"
 
 using namespace mireduce;
 
@@ -74,7 +75,7 @@ const std::set<std::string> kKnown = {
     "method", "type", "n", "threads", "kernel", "maxblocks", "cpufinal", "cputhresh", "shmoo",
     "device", "qatest", "noprompt", "prompt", "help", "quiet", "iterations", "acc", "unroll",
     "wg-per-cu", "policy", "pattern", "seed", "fill", "noverify", "json", "log", "master-log",
-    "countdown", "shmoo-max"};
+    "countdown", "shmoo-max", "trace"};
 
 void usage() {
   std::printf(
@@ -88,7 +89,8 @@ void usage() {
       "  --shmoo          sweep n = 1..32M (powers of two) over kernels, print CSV\n"
       "  --iterations=100 --acc=TYPE --unroll=2|4|8 --wg-per-cu=N --policy=auto|nt|default\n"
       "  --pattern=smallint|uniform|fullrange|iotamod --seed=N --fill=host|device --noverify\n"
-      "  --device=N --json=PATH --log=FILE|none --master-log=FILE --qatest --prompt --countdown\n");
+      "  --device=N --json=PATH --log=FILE|none --master-log=FILE --qatest --prompt --countdown\n"
+      "  --trace          roctx ranges per iteration (rocprofv3 --marker-trace)\n");
 }
 
 size_t pick_threads_for_fill() {
@@ -144,6 +146,7 @@ struct Runner {
 
   // Returns true if the result was produced on the host into host_out.
   bool run_once(uint64_t n, unsigned char* host_out) {
+    TraceRange tr("reduction.iteration");
     const void* in = b.in.get();
     if (o.kernel <= 6) {
       const int mb = o.max_blocks > 0 ? o.max_blocks : 64;  // reference default (reduction.cpp:668)
@@ -356,6 +359,7 @@ int main(int argc, char** argv) {
   if (log != "none") L.set_log_file(log);  // shrSetLogFileName("reduction.txt") (reduction.cpp:88)
   L.set_master_file(args.str_or("master-log", ""));
   L.set_quiet(args.has("quiet"));
+  set_tracing(args.has("trace"));
   for (const auto& u : args.unknown(kKnown)) std::fprintf(stderr, "warning: unknown flag --%s ignored\n", u.c_str());
 
   Options o;

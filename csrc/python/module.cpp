@@ -17,6 +17,7 @@
 #include "mireduce/ladder.hpp"
 #include "mireduce/mt19937.hpp"
 #include "mireduce/reduce.hpp"
+#include "mireduce/trace.hpp"
 #include "mireduce/types.hpp"
 
 namespace py = pybind11;
@@ -274,6 +275,11 @@ PYBIND11_MODULE(_C, m) {
   });
 
   m.def("compiled_variants", &compiled_variants);
+
+  m.def("set_tracing", &set_tracing, "enable roctx ranges (rocprofv3 --marker-trace)");
+  m.def("tracing", &tracing);
+  m.def("trace_push", [](const std::string& name) { if (tracing()) trace_push(name.c_str()); });
+  m.def("trace_pop", [] { if (tracing()) trace_pop(); });
 
   m.def("synchronize", [](int dev) {
     if (dev >= 0) check_hip(hipSetDevice(dev), "hipSetDevice");

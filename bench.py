@@ -40,7 +40,7 @@ def parse_args(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--config", default=NORTH_STAR, choices=sorted(k for k, v in CONFIGS.items() if v.mode == "scalar"))
+    p.add_argument("--config", default=NORTH_STAR, choices=sorted(CONFIGS))
     p.add_argument("--elements", type=int, default=None, help="override the global element count")
     p.add_argument("--serial", action="store_true", help="no overlap between consecutive steps")
     p.add_argument("--block", type=int, default=0)
@@ -64,11 +64,52 @@ def _sync(dev: torch.device) -> None:
         torch.cuda.synchronize(dev)
 
 
+def run_vector(args, ctx, cfg) -> int:
+    """reduce.c semantics (BASELINE config 1): element-wise reduce of an N/P vector per rank to
+    root 0. Each collective is timed on its own between a barrier and a synchronisation (the
+    in-place buffer is restored outside the clock, like reduce.c's bzero, mpi/reduce.c:74-77);
+    the step time is the MAX over ranks; GB = 2^30 B of total data (mpi/reduce.c:79)."""
+    from cuda_mpi_reductions_amd.models import VectorReduction
+    wl = VectorReduction(cfg, ctx).setup(mt19937=(ctx.device.type == "cpu"))
+    dev = ctx.device
+    for _ in range(args.warmup):
+        wl.step()
+    times = []
+    for _ in range(args.steps):
+        wl.restore()
+        _sync(dev)
+        pdist.barrier(ctx)
+        t0 = time.perf_counter()
+        wl.collective()
+        _sync(dev)
+        times.append(pdist.max_over_ranks(time.perf_counter() - t0, ctx))
+    elapsed = sum(times)
+    verified = None if args.no_verify else wl.verify()["ok"]
+    gib = wl.bytes_total * args.steps / elapsed / float(1 << 30)
+    if ctx.is_root:
+        print(json.dumps({
+            "metric": f"MPI_Reduce-style element-wise {cfg.collective} bandwidth (GiB/s of total data, reduce.c units)",
+            "value": round(gib, 3), "unit": "GiB/s", "n_gpus": ctx.world_size if dev.type == "cuda" else 0,
+            "n_ranks": ctx.world_size, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": str(cfg.dtype).replace("torch.", ""), "device": dev.type,
+            "data": "reduce.c MT19937 per-rank data" if dev.type == "cpu" else "synthetic rank-seeded device fill",
+            "config": {"model": f"{cfg.name}: {cfg.description}", "global_batch": wl.count * ctx.world_size,
+                       "seq_len": 1, "parallelism": f"dp{ctx.world_size}", "backend": ctx.backend,
+                       "op": cfg.op.upper(), "count_per_rank": wl.count},
+            "verified": verified,
+        }), flush=True)
+    return 0 if verified in (None, True) else 1
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     C = native()  # fail loudly if the HIP extension is missing
     C.set_tracing(args.trace)
-    device_type = None if args.device == "auto" else args.device
+    if args.device != "auto":
+        device_type = args.device
+    else:  # CPU-rank configs (reduce.c plumbing) run on CPU ranks even on a GPU box
+        device_type = "cpu" if CONFIGS[args.config].device == "cpu" else None
     ctx = pdist.init(backend=None if args.backend == "auto" else args.backend, device_type=device_type)
     if args.gpus != ctx.world_size and ctx.is_root:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}; using {ctx.world_size}",
@@ -77,6 +118,10 @@ def main(argv=None) -> int:
     if args.elements is not None:
         from dataclasses import replace
         cfg = replace(cfg, n_total=args.elements)
+    if cfg.mode == "vector":
+        rc = run_vector(args, ctx, cfg)
+        pdist.shutdown(ctx)
+        return rc
     kernel = KernelConfig(block=args.block, unroll=args.unroll, wg_per_cu=args.wg_per_cu,
                           groups=args.groups,
                           nontemporal=None if args.policy == "auto" else args.policy == "nt",

@@ -216,8 +216,48 @@ class VectorReduction:
         # we count the bytes actually reduced (count * P), which equals it when P divides N.
         return self.count * self.ctx.world_size * element_size(self.cfg.dtype)
 
-    def step(self, async_op: bool = False):
+    def restore(self) -> None:
+        """Reset the in-place collective buffer (reduce.c's bzero of the receive buffer)."""
         self.y.copy_(self.x)
+
+    def collective(self, async_op: bool = False):
         if self.cfg.collective == "reduce":
             return pdist.vector_reduce(self.y, self.cfg.op, root=0, async_op=async_op)
         return pdist.vector_allreduce(self.y, self.cfg.op, async_op=async_op)
+
+    def step(self, async_op: bool = False):
+        self.restore()
+        return self.collective(async_op=async_op)
+
+    def verify(self) -> dict:
+        """Gather every rank's input and combine on the result holders; integer SUM wraps like
+        MPI_INT / ncclInt32 (two's complement)."""
+        world = self.ctx.world_size
+        gathered = [torch.empty_like(self.x) for _ in range(world)]
+        if world > 1:
+            torch.distributed.all_gather(gathered, self.x)
+        else:
+            gathered[0].copy_(self.x)
+        holder = self.cfg.collective == "allreduce" or self.ctx.rank == 0
+        ok = True
+        if holder:
+            st = torch.stack(gathered)
+            if self.cfg.op == "sum":
+                if st.dtype.is_floating_point:
+                    exp = st.double().sum(0)
+                    tol = 1e-12 * world * (exp.abs() + 1.0)
+                    ok = bool(((self.y.double() - exp).abs() <= tol).all())
+                else:
+                    bits = 8 * st.element_size()
+                    exp = st.long().sum(0) if bits == 32 else st.sum(0)
+                    if bits == 32:
+                        exp = ((exp + 2 ** 31) % 2 ** 32 - 2 ** 31).to(st.dtype)
+                    ok = bool(torch.equal(exp, self.y))
+            else:
+                exp = st.min(0).values if self.cfg.op == "min" else st.max(0).values
+                ok = bool(torch.equal(exp, self.y))
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                         device=self.ctx.device if self.ctx.backend == "nccl" else "cpu")
+        if world > 1:
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
+        return {"ok": bool(t.item())}

@@ -124,3 +124,13 @@ def test_bench_contract_on_cpu_ranks(tmp_path):
     assert d["metric"] == "reduction bandwidth (GB/s, whole node), 1B-double sum at 1/2/4/8 MI355X"
     assert d["scaling"] == "strong" and d["config"]["parallelism"] == "dp2"
     assert abs(d["value"] - d["config"]["bytes_per_step"] * 4 / (d["ms_per_step"] * 4e-3) / 1e9) / d["value"] < 0.01
+
+
+def test_bench_vector_config1_two_cpu_ranks(tmp_path):
+    # BASELINE config 1 through bench.py: 1M int32 SUM, element-wise reduce to root, 2 CPU ranks.
+    r = torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "1",
+                     "--config", "mpi_1m_int32_sum_cpu2"], cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["unit"] == "GiB/s" and d["n_ranks"] == 2 and d["verified"] is True
+    assert d["config"]["global_batch"] == 1 << 20 and d["device"] == "cpu"

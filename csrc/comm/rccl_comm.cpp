@@ -1,7 +1,10 @@
 // RCCL communicator wrapper; see comm.hpp.
 #include <hip/hip_runtime_api.h>
 
+#include <unistd.h>
+
 #include <chrono>
+#include <cstdio>
 #include <string>
 #include <thread>
 
@@ -42,9 +45,33 @@ ncclRedOp_t nccl_op(Op o) {
   return ncclSum;
 }
 
+namespace {
+// RCCL prints a version banner on stdout when a communicator is created; our stdout carries
+// reduce.c-format data lines, so the banner is sent to stderr instead.
+class StdoutToStderr {
+ public:
+  StdoutToStderr() {
+    std::fflush(stdout);
+    saved_ = dup(1);
+    if (saved_ >= 0) dup2(2, 1);
+  }
+  ~StdoutToStderr() {
+    std::fflush(stdout);
+    if (saved_ >= 0) {
+      dup2(saved_, 1);
+      close(saved_);
+    }
+  }
+
+ private:
+  int saved_ = -1;
+};
+}  // namespace
+
 RcclComm::RcclComm(TcpBootstrap& boot, int device) : rank_(boot.rank()), world_(boot.world()) {
   (void)device;
   ncclUniqueId id;
+  StdoutToStderr quiet;
   if (rank_ == 0) check(ncclGetUniqueId(&id), "ncclGetUniqueId");
   boot.broadcast(&id, sizeof id, 0);
   check(ncclCommInitRank(&comm_, world_, id, rank_), "ncclCommInitRank");

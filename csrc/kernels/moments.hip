@@ -1,0 +1,158 @@
+// Fused multi-statistic reduction: one streaming pass computes Σ(x-K), Σ(x-K)², min and max
+// (K = x[0], the shifted-data algorithm, so the variance does not cancel catastrophically when
+// |mean| >> std). Pattern reference: the fused Σx / Σx² tree of the vendored MonteCarlo sample
+// (cuda/C/src/MonteCarlo/MonteCarlo_reduction.cuh:20-38,47-63), SURVEY.md §2.4.
+//
+// Same streaming structure as reduce_stream (16-byte nt loads, UNROLL loads in flight, wave64
+// butterflies); four accumulators per lane. Two launches: per-workgroup partials (4 doubles),
+// then one workgroup folds them — the partial block is only 32 B x grid.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "mireduce/check.hpp"
+#include "mireduce/moments.hpp"
+#include "mireduce/ops.hpp"
+
+namespace mireduce {
+namespace kern {
+
+struct Mom {
+  double s, q, mn, mx;
+};
+
+__device__ __forceinline__ Mom mom_combine(Mom a, Mom b) {
+  return {a.s + b.s, a.q + b.q, MinOp::apply(a.mn, b.mn), MaxOp::apply(a.mx, b.mx)};
+}
+
+__device__ __forceinline__ Mom mom_shfl(Mom v, int off) {
+  return {__shfl_xor(v.s, off, 64), __shfl_xor(v.q, off, 64), __shfl_xor(v.mn, off, 64), __shfl_xor(v.mx, off, 64)};
+}
+
+template <int BLOCK>
+__device__ __forceinline__ Mom block_mom(Mom v, Mom* lds) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = mom_combine(v, mom_shfl(v, off));
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) lds[wave] = v;
+  __syncthreads();
+  if (wave == 0) {
+    const Mom id{0.0, 0.0, MinOp::identity<double>(), MaxOp::identity<double>()};
+    v = lane < BLOCK / 64 ? lds[lane] : id;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = mom_combine(v, mom_shfl(v, off));
+  }
+  return v;
+}
+
+template <class T, int BLOCK, int UNROLL>
+__global__ __launch_bounds__(BLOCK) void moments_stream(const T* __restrict__ in, uint64_t n, Mom* __restrict__ partials) {
+  constexpr int N = 16 / sizeof(T);
+  using V = T __attribute__((ext_vector_type(N)));
+  __shared__ Mom lds[BLOCK / 64];
+  const double K = n ? static_cast<double>(in[0]) : 0.0;
+  double s[UNROLL], q[UNROLL], mn[UNROLL], mx[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    s[u] = 0.0;
+    q[u] = 0.0;
+    mn[u] = MinOp::identity<double>();
+    mx[u] = MaxOp::identity<double>();
+  }
+  const uint64_t nvec = n / N;
+  const V* vin = reinterpret_cast<const V*>(in);
+  constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
+  const uint64_t ntiles = nvec / kTile;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const V* p = vin + t * kTile + threadIdx.x;
+    V v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) v[u] = __builtin_nontemporal_load(p + u * BLOCK);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        const double x = static_cast<double>(v[u][k]);
+        const double d = x - K;
+        s[u] += d;
+        q[u] = __builtin_fma(d, d, q[u]);
+        mn[u] = MinOp::apply(mn[u], x);
+        mx[u] = MaxOp::apply(mx[u], x);
+      }
+    }
+  }
+  // remaining vectors, then the < N scalar tail (input is 16-byte aligned: checked on the host)
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * BLOCK;
+  for (uint64_t i = ntiles * kTile + static_cast<uint64_t>(blockIdx.x) * BLOCK + threadIdx.x; i < nvec; i += stride) {
+    const V v = vin[i];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const double x = static_cast<double>(v[k]);
+      const double d = x - K;
+      s[0] += d;
+      q[0] = __builtin_fma(d, d, q[0]);
+      mn[0] = MinOp::apply(mn[0], x);
+      mx[0] = MaxOp::apply(mx[0], x);
+    }
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x < n - nvec * N) {
+    const double x = static_cast<double>(in[nvec * N + threadIdx.x]);
+    const double d = x - K;
+    s[0] += d;
+    q[0] = __builtin_fma(d, d, q[0]);
+    mn[0] = MinOp::apply(mn[0], x);
+    mx[0] = MaxOp::apply(mx[0], x);
+  }
+  Mom m{s[0], q[0], mn[0], mx[0]};
+#pragma unroll
+  for (int u = 1; u < UNROLL; ++u) m = mom_combine(m, Mom{s[u], q[u], mn[u], mx[u]});
+  m = block_mom<BLOCK>(m, lds);
+  if (threadIdx.x == 0) partials[blockIdx.x] = m;
+}
+
+__global__ __launch_bounds__(256) void moments_finalize(const Mom* __restrict__ partials, int count,
+                                                        const void* __restrict__ first, int is_f64, uint64_t n,
+                                                        double* __restrict__ out) {
+  __shared__ Mom lds[4];
+  Mom m{0.0, 0.0, MinOp::identity<double>(), MaxOp::identity<double>()};
+  for (int i = threadIdx.x; i < count; i += 256) m = mom_combine(m, partials[i]);
+  m = block_mom<256>(m, lds);
+  if (threadIdx.x == 0) {
+    double K = 0.0;
+    if (n) K = is_f64 ? *static_cast<const double*>(first) : static_cast<double>(*static_cast<const float*>(first));
+    out[0] = K;
+    out[1] = m.s;
+    out[2] = m.q;
+    out[3] = m.mn;
+    out[4] = m.mx;
+  }
+}
+
+}  // namespace kern
+
+void moments_device(const void* in, size_t n, DType t, double* out5, void* partials, int max_grid, int num_cus,
+                    hipStream_t stream) {
+  MIREDUCE_REQUIRE(t == DType::Float32 || t == DType::Float64, "moments: float32 or float64 input");
+  MIREDUCE_REQUIRE(reinterpret_cast<uintptr_t>(in) % 16 == 0, "moments: input must be 16-byte aligned");
+  constexpr int kBlock = 256, kUnroll = 4;
+  const size_t vec = 16 / dtype_size(t);
+  const uint64_t tiles = (n / vec + kBlock * kUnroll - 1) / (kBlock * kUnroll);
+  int grid = static_cast<int>(std::min<uint64_t>(std::max<uint64_t>(tiles, 1), static_cast<uint64_t>(num_cus) * 3));
+  grid = std::min(grid, max_grid);
+  auto* p = static_cast<kern::Mom*>(partials);
+  if (t == DType::Float64)
+    hipLaunchKernelGGL((kern::moments_stream<double, kBlock, kUnroll>), dim3(grid), dim3(kBlock), 0, stream,
+                       static_cast<const double*>(in), static_cast<uint64_t>(n), p);
+  else
+    hipLaunchKernelGGL((kern::moments_stream<float, kBlock, kUnroll>), dim3(grid), dim3(kBlock), 0, stream,
+                       static_cast<const float*>(in), static_cast<uint64_t>(n), p);
+  MIREDUCE_HIP_THROW(hipGetLastError());
+  hipLaunchKernelGGL(kern::moments_finalize, dim3(1), dim3(256), 0, stream, p, grid, in, t == DType::Float64 ? 1 : 0,
+                     static_cast<uint64_t>(n), out5);
+  MIREDUCE_HIP_THROW(hipGetLastError());
+}
+
+size_t moments_partials_bytes(int max_grid) { return static_cast<size_t>(max_grid) * sizeof(kern::Mom); }
+
+}  // namespace mireduce

@@ -15,6 +15,7 @@
 #include "mireduce/check.hpp"
 #include "mireduce/cpu_reference.hpp"
 #include "mireduce/ladder.hpp"
+#include "mireduce/moments.hpp"
 #include "mireduce/mt19937.hpp"
 #include "mireduce/reduce.hpp"
 #include "mireduce/trace.hpp"
@@ -275,6 +276,17 @@ PYBIND11_MODULE(_C, m) {
   });
 
   m.def("compiled_variants", &compiled_variants);
+
+  m.def(
+      "moments",
+      [](uintptr_t in, uint64_t n, int dtype, uintptr_t out5, uintptr_t partials, int max_grid, int num_cus,
+         uintptr_t stream) {
+        moments_device(as_ptr<const void>(in), n, static_cast<DType>(dtype), as_ptr<double>(out5),
+                       as_ptr<void>(partials), max_grid, num_cus, as_stream(stream));
+      },
+      py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("out_ptr"), py::arg("partials_ptr"),
+      py::arg("max_grid"), py::arg("num_cus"), py::arg("stream") = 0);
+  m.def("moments_partials_bytes", &moments_partials_bytes);
 
   m.def("set_tracing", &set_tracing, "enable roctx ranges (rocprofv3 --marker-trace)");
   m.def("tracing", &tracing);

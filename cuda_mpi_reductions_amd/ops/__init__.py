@@ -4,3 +4,4 @@ from .reduce import (  # noqa: F401
     ladder_reduce, op_code, reduce, reduce_partials, sum_tolerance,
 )
 from .fill import PATTERNS, fill_, mt19937_fill_, synthetic  # noqa: F401
+from .moments import combine_moments, moments  # noqa: F401

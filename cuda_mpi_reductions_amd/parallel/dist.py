@@ -13,9 +13,11 @@ Reference parity:
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import os
 import socket
+import sys
 from dataclasses import dataclass
 from typing import Optional
 
@@ -47,6 +49,21 @@ class DistContext:
     @property
     def is_root(self) -> bool:
         return self.rank == 0
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Route fd 1 to stderr: RCCL prints a version banner on stdout when a communicator is
+    created, and stdout of our tools carries data (JSON / GNUPlot lines)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def _free_port() -> int:
@@ -86,8 +103,11 @@ def init(backend: Optional[str] = None, device_type: Optional[str] = None,
         kwargs = dict(backend=backend, rank=rank, world_size=world,
                       timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
-            kwargs["device_id"] = device
-        dist.init_process_group(**kwargs)
+            kwargs["device_id"] = device  # eager communicator creation, inside the redirect
+        with stdout_to_stderr():
+            dist.init_process_group(**kwargs)
+            if backend == "nccl":
+                dist.barrier(device_ids=[device.index])
         owns = True
     return DistContext(rank, world, local_rank, backend, device, owns)
 

@@ -1,0 +1,89 @@
+"""The native apps on a real MI355X: QA protocol, CLI parity paths, verification, output formats."""
+import json
+import os
+import re
+
+import pytest
+
+from helpers import BIN, ensure_built, run
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    ensure_built()
+
+
+def reduction(tmp_path, *args, timeout=600):
+    r = run([os.path.join(BIN, "reduction"), "--qatest", "--log=none", *args], cwd=tmp_path, timeout=timeout)
+    return r
+
+
+@pytest.mark.parametrize("method", ["SUM", "MIN", "MAX"])
+@pytest.mark.parametrize("type_", ["int", "int64", "float", "double"])
+def test_reduction_app_methods_types(tmp_path, method, type_):
+    r = reduction(tmp_path, f"--method={method}", f"--type={type_}", "--n=3000017", "--iterations=5")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert re.search(r"&&&& PASSED reduction", r.stderr)
+    assert re.search(r"Reduction, Throughput = [0-9.]+ GB/s, Time = [0-9.]+ s, Size = 3000017 Elements, "
+                     r"NumDevsUsed = 1, Workgroup = \d+", r.stdout)
+    assert "GPU result = " in r.stdout and "CPU result = " in r.stdout
+
+
+@pytest.mark.parametrize("kernel", range(9))
+def test_reduction_app_every_kernel(tmp_path, kernel):
+    r = reduction(tmp_path, "--method=SUM", "--type=double", f"--kernel={kernel}", "--n=1000001", "--iterations=3")
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("flags", [["--cpufinal"], ["--cputhresh=100000"], ["--maxblocks=7"],
+                                   ["--threads=1024", "--unroll=16"], ["--policy=default", "--unroll=2"],
+                                   ["--acc=int"], ["--fill=device", "--pattern=iotamod"]])
+def test_reduction_app_paths(tmp_path, flags):
+    r = reduction(tmp_path, "--method=MAX" if "--acc=int" not in flags else "--method=SUM", "--n=2000003",
+                  "--iterations=3", *flags)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_reduction_app_json_and_log(tmp_path):
+    r = run([os.path.join(BIN, "reduction"), "--method=SUM", "--type=double", "--n=1M", "--iterations=4",
+             "--json=out.jsonl", "--master-log=master.csv"], cwd=tmp_path, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "reduction.txt").exists()           # shrSetLogFileName("reduction.txt")
+    assert "Reduction, Throughput" in (tmp_path / "master.csv").read_text()
+    d = json.loads((tmp_path / "out.jsonl").read_text().splitlines()[0])
+    assert d["verified"] is True and len(d["iteration_ms"]) == 4 and d["bytes_per_GB"] == 1e9
+
+
+def test_reduction_shmoo(tmp_path):
+    r = run([os.path.join(BIN, "reduction"), "--method=SUM", "--type=float", "--shmoo", "--shmoo-max=65536",
+             "--iterations=2", "--log=none"], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr
+    rows = [ln for ln in r.stdout.splitlines() if re.match(r"^\d+,", ln)]
+    assert len(rows) == 17 * 9   # n = 1..65536 (powers of two) x kernels {0..6, 8, 7}
+
+
+def test_reduce_xgmi_single_rank_scalar_and_graph(tmp_path):
+    for extra in ([], ["--graph"]):
+        r = run([os.path.join(BIN, "reduce_xgmi"), "--mode=scalar", "--n=20000003", "--dtypes=INT,LONG,FLOAT,DOUBLE",
+                 "--retries=1", "--iters=3", *extra], timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert "verification PASSED" in r.stderr
+        rows = [ln for ln in r.stdout.splitlines() if re.match(r"^(INT|LONG|FLOAT|DOUBLE) (MAX|MIN|SUM) 1 +[0-9.]+$", ln)]
+        assert len(rows) == 12
+
+
+def test_reduce_xgmi_single_rank_vector_mt19937(tmp_path):
+    r = run([os.path.join(BIN, "reduce_xgmi"), "--mode=vector", "--ints=1M", "--doubles=1M", "--retries=2",
+             "--mt19937", f"--json={tmp_path / 'x.jsonl'}"], timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.splitlines()[0] == "# DATATYPE OP NODES GB/sec"
+    recs = [json.loads(x) for x in (tmp_path / "x.jsonl").read_text().splitlines()]
+    assert len(recs) == 12 and all(x.get("verified", True) for x in recs)
+
+
+def test_bandwidth_test_app():
+    r = run([os.path.join(BIN, "bandwidth_test"), "--size=256M", "--iters=5"], timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "Device to Device copy" in r.stdout and "Read stream" in r.stdout

@@ -33,10 +33,11 @@ PYEXT     := cuda_mpi_reductions_amd/_C$(PY_EXT)
 KERNEL_SRC  := $(wildcard csrc/kernels/*.hip)
 RUNTIME_SRC := $(wildcard csrc/runtime/*.cpp)
 COMM_SRC    := $(wildcard csrc/comm/*.cpp)
+COMM_HIP    := $(wildcard csrc/comm/*.hip)
 
 KERNEL_OBJ  := $(patsubst csrc/%.hip,$(BUILD)/obj/%.o,$(KERNEL_SRC))
 RUNTIME_OBJ := $(patsubst csrc/%.cpp,$(BUILD)/obj/%.o,$(RUNTIME_SRC))
-COMM_OBJ    := $(patsubst csrc/%.cpp,$(BUILD)/obj/%.o,$(COMM_SRC))
+COMM_OBJ    := $(patsubst csrc/%.cpp,$(BUILD)/obj/%.o,$(COMM_SRC)) $(patsubst csrc/%.hip,$(BUILD)/obj/%.o,$(COMM_HIP))
 LIB         := $(BUILD)/lib/libmireduce.a
 COMMLIB     := $(BUILD)/lib/libmireduce_comm.a
 

@@ -33,6 +33,7 @@
 #include "mireduce/comm.hpp"
 #include "mireduce/cpu_reference.hpp"
 #include "mireduce/device.hpp"
+#include "mireduce/direct.hpp"
 #include "mireduce/mt19937.hpp"
 #include "mireduce/reduce.hpp"
 #include "mireduce/report.hpp"
@@ -55,7 +56,8 @@ struct Ctx {
   LaunchEnv env;
   int device = 0;
   std::unique_ptr<TcpBootstrap> boot;
-  std::unique_ptr<RcclComm> comm;
+  std::unique_ptr<RcclComm> comm;      // RCCL collectives
+  std::unique_ptr<DirectPeers> direct;  // --collective=direct|direct-reduce (peer reads over xGMI)
   hipStream_t stream = nullptr;
   int retries = 5, warmup = 1, iters = 10, root = 0;
   std::string mode = "vector", collective, json;
@@ -76,6 +78,13 @@ uint64_t global_count(DType t, uint64_t ints, uint64_t longs, uint64_t floats, u
   return 0;
 }
 
+void sync_stream(Ctx& c) {
+  if (c.comm) c.comm->synchronize(c.stream, c.timeout_s);
+  else HIP_CHECK(hipStreamSynchronize(c.stream));
+}
+
+bool is_direct(const Ctx& c) { return c.collective == "direct" || c.collective == "direct-reduce"; }
+
 // Time `iters` repetitions of `body` on the stream (optionally as one hipGraph replay).
 template <class F>
 double time_iters(Ctx& c, F&& body) {
@@ -87,14 +96,14 @@ double time_iters(Ctx& c, F&& body) {
     HIP_CHECK(hipStreamEndCapture(c.stream, &graph));
     HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
     HIP_CHECK(hipGraphLaunch(exec, c.stream));  // upload / first replay outside the clock
-    c.comm->synchronize(c.stream, c.timeout_s);
+    sync_stream(c);
   }
   c.boot->barrier();
   const double t0 = StopWatch::now_s();
   if (c.graph) HIP_CHECK(hipGraphLaunch(exec, c.stream));
   else
     for (int i = 0; i < c.iters; ++i) body();
-  c.comm->synchronize(c.stream, c.timeout_s);
+  sync_stream(c);
   const double dt = (StopWatch::now_s() - t0) / c.iters;
   if (exec) HIP_CHECK(hipGraphExecDestroy(exec));
   if (graph) HIP_CHECK(hipGraphDestroy(graph));
@@ -130,7 +139,7 @@ bool check_samples(Ctx& c, Op o, const void* d_send, const void* d_recv, uint64_
     HIP_CHECK(hipMemcpy(&got[s], static_cast<const T*>(d_recv) + idx[s], sizeof(T), hipMemcpyDeviceToHost));
   }
   c.boot->allgather(mine.data(), all.data(), kS * sizeof(T));
-  const bool holder = c.collective == "allreduce" || c.env.rank == c.root;
+  const bool holder = c.collective == "allreduce" || c.collective == "direct" || c.env.rank == c.root;
   int ok = 1;
   if (holder) {
     for (int s = 0; s < kS; ++s) {
@@ -188,38 +197,58 @@ bool run_vector(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>&
     bufs.push_back(std::move(b));
   }
   HIP_CHECK(hipStreamSynchronize(c.stream));
+  if (is_direct(c)) {  // registered (IPC-shared) buffers sized for the largest dtype
+    size_t mx = 0;
+    for (auto& b : bufs) mx = std::max(mx, b.count * dtype_size(b.t));
+    c.direct = std::make_unique<DirectPeers>(*c.boot, c.device, mx);
+  }
   auto body_for = [&](B& b, Op o) {
     return [&c, &b, o] {
       TraceRange tr("reduce_xgmi.vector_collective");
       if (c.collective == "reduce") c.comm->reduce(b.send.get(), b.recv.get(), b.count, b.t, o, c.root, c.stream);
-      else c.comm->allreduce(b.send.get(), b.recv.get(), b.count, b.t, o, c.stream);
+      else if (c.collective == "allreduce") c.comm->allreduce(b.send.get(), b.recv.get(), b.count, b.t, o, c.stream);
+      else if (c.collective == "direct") c.direct->allreduce(b.count, b.t, o, c.stream);
+      else c.direct->reduce(b.count, b.t, o, c.root, c.stream);
     };
   };
+  auto stage = [&](B& b) {  // direct mode: this dtype's data into the registered input buffer
+    if (c.direct) {
+      HIP_CHECK(hipMemcpyAsync(c.direct->in(), b.send.get(), b.count * dtype_size(b.t), hipMemcpyDeviceToDevice, c.stream));
+      HIP_CHECK(hipStreamSynchronize(c.stream));
+    }
+  };
+  const void* (*in_ptr)(Ctx&, B&) = [](Ctx& cc, B& bb) -> const void* { return cc.direct ? cc.direct->in() : bb.send.get(); };
+  const void* (*out_ptr)(Ctx&, B&) = [](Ctx& cc, B& bb) -> const void* { return cc.direct ? cc.direct->out() : bb.recv.get(); };
   const int saved_iters = c.iters;
   c.iters = 1;
   const bool saved_graph = c.graph;
   c.graph = false;
   for (int w = 0; w < c.warmup; ++w)
-    for (auto& b : bufs) time_iters(c, body_for(b, Op::Sum));  // reduce.c:61-64
+    for (auto& b : bufs) {
+      stage(b);
+      time_iters(c, body_for(b, Op::Sum));  // reduce.c:61-64
+    }
   c.iters = saved_iters;
   c.graph = saved_graph;
   if (c.env.rank == c.root) std::printf("%s\n", gnuplot_header().c_str());
   bool ok = true;
   for (int x = 0; x < c.retries; ++x) {
     for (auto& b : bufs) {
+      stage(b);
       for (Op o : ops) {
-        HIP_CHECK(hipMemsetAsync(b.recv.get(), 0, b.recv.bytes(), c.stream));  // bzero (reduce.c:74)
+        HIP_CHECK(hipMemsetAsync(const_cast<void*>(out_ptr(c, b)), 0, b.count * dtype_size(b.t), c.stream));  // bzero (reduce.c:74)
         const double dt = time_iters(c, body_for(b, o));
         const double bytes = static_cast<double>(b.count) * c.env.world * dtype_size(b.t);
         const double algbw = static_cast<double>(b.count) * dtype_size(b.t) / dt / kGB;
-        const double busbw = c.collective == "allreduce" ? algbw * 2.0 * (c.env.world - 1) / c.env.world : algbw;
+        const bool all = c.collective == "allreduce" || c.collective == "direct";
+        const double busbw = all ? algbw * 2.0 * (c.env.world - 1) / c.env.world : algbw;
         bool vok = true;
         if (c.verify && x == 0) {
           switch (b.t) {
-            case DType::Int32: vok = check_samples<int32_t>(c, o, b.send.get(), b.recv.get(), b.count); break;
-            case DType::Int64: vok = check_samples<int64_t>(c, o, b.send.get(), b.recv.get(), b.count); break;
-            case DType::Float32: vok = check_samples<float>(c, o, b.send.get(), b.recv.get(), b.count); break;
-            case DType::Float64: vok = check_samples<double>(c, o, b.send.get(), b.recv.get(), b.count); break;
+            case DType::Int32: vok = check_samples<int32_t>(c, o, in_ptr(c, b), out_ptr(c, b), b.count); break;
+            case DType::Int64: vok = check_samples<int64_t>(c, o, in_ptr(c, b), out_ptr(c, b), b.count); break;
+            case DType::Float32: vok = check_samples<float>(c, o, in_ptr(c, b), out_ptr(c, b), b.count); break;
+            case DType::Float64: vok = check_samples<double>(c, o, in_ptr(c, b), out_ptr(c, b), b.count); break;
           }
           ok = ok && vok;
         }
@@ -310,7 +339,8 @@ void usage() {
   std::printf(
       "reduce_xgmi — RCCL-over-xGMI reduction benchmark (one process per GPU)\n"
       "  --mode=vector|scalar        reduce.c element-wise reduce | global array -> one value\n"
-      "  --collective=reduce|allreduce (vector default: reduce, like MPI_Reduce; scalar: allreduce)\n"
+      "  --collective=reduce|allreduce|direct|direct-reduce (vector default: reduce, like MPI_Reduce;\n"
+      "               scalar: allreduce; direct*: one-shot peer reads over xGMI via IPC, no RCCL)\n"
       "  --dtypes=INT,DOUBLE  --ops=MAX,MIN,SUM  --retries=5  --warmup=1  --iters=10  --root=0\n"
       "  --ints=N --doubles=N --longs=N --floats=N   global element counts (reduce.c defaults)\n"
       "  --n=N                        global count for every dtype (scalar mode north star: 1e9)\n"
@@ -346,7 +376,10 @@ int main(int argc, char** argv) {
     c.mode = args.str_or("mode", "vector");
     if (c.mode != "vector" && c.mode != "scalar") throw CliError("--mode must be vector|scalar");
     c.collective = args.str_or("collective", c.mode == "vector" ? "reduce" : "allreduce");
-    if (c.collective != "reduce" && c.collective != "allreduce") throw CliError("--collective must be reduce|allreduce");
+    if (c.collective != "reduce" && c.collective != "allreduce" && c.collective != "direct" && c.collective != "direct-reduce")
+      throw CliError("--collective must be reduce|allreduce|direct|direct-reduce");
+    if (c.mode == "scalar" && (c.collective == "direct" || c.collective == "direct-reduce"))
+      throw CliError("direct collectives are vector-mode only");
     if (c.mode == "scalar" && c.collective != "allreduce") throw CliError("scalar mode uses --collective=allreduce");
     std::vector<std::string> list;
     if (args.get_list("dtypes", &list)) {
@@ -378,6 +411,8 @@ int main(int argc, char** argv) {
     c.root = args.int_or<int>("root", c.root);
     c.json = args.str_or("json", "");
     c.graph = args.has("graph");
+    if (c.graph && (c.collective == "direct" || c.collective == "direct-reduce"))
+      throw CliError("--graph cannot capture the host-synchronised direct collectives");
     set_tracing(args.has("trace"));
     c.mt = args.has("mt19937");
     c.verify = !args.has("noverify");
@@ -409,8 +444,10 @@ int main(int argc, char** argv) {
   bool ok = false;
   try {
     c.boot = std::make_unique<TcpBootstrap>(c.env);
-    c.comm = std::make_unique<RcclComm>(*c.boot, c.device);
-    install_comm_abort_hook(c.comm.get());
+    if (!is_direct(c)) {  // the direct path needs no RCCL (and may share one GPU between ranks)
+      c.comm = std::make_unique<RcclComm>(*c.boot, c.device);
+      install_comm_abort_hook(c.comm.get());
+    }
     if (c.env.rank == 0) {
       DeviceInfo di = device_info(c.device);
       std::fprintf(stderr, "[reduce_xgmi] %d ranks (%s), %s %s, RCCL %d, mode=%s collective=%s\n", c.env.world,
@@ -428,6 +465,7 @@ int main(int argc, char** argv) {
     ok = false;
   }
   install_comm_abort_hook(nullptr);
+  c.direct.reset();
   c.comm.reset();
   c.boot.reset();
   HIP_CHECK(hipStreamDestroy(c.stream));

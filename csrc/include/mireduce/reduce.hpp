@@ -29,6 +29,7 @@ struct ReduceConfig {
   int max_blocks = 0;     // hard cap on the grid (reference --maxblocks)
   int groups = 0;         // fan-in shards of the arrival ticket (<= 64)
   int policy = -1;        // streaming-load cache policy: -1 auto, 0 default, 1 non-temporal (nt)
+  int pipeline = -1;      // software-pipelined body: -1 auto, 0 off, 1 on (BLOCK*UNROLL <= 8192)
   bool single_pass = true;   // last-arriver finalisation vs a second finalize launch
 };
 
@@ -39,6 +40,7 @@ struct LaunchPlan {
   int grid = 0;
   int groups = 0;
   bool nontemporal = true;
+  bool pipelined = false;
   bool single_pass = true;
   uint64_t head = 0;   // scalar elements before the first 16-B aligned vector
   uint64_t nvec = 0;   // 16-byte vectors in the streaming body

@@ -93,7 +93,28 @@ struct Args {
   int groups;            // 0: two-pass mode (write partials only)
 };
 
-template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT>
+template <class V, int BLOCK, int UNROLL, bool NT>
+__device__ __forceinline__ void load_tile(V (&v)[UNROLL], const V* p) {
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    if constexpr (NT) v[u] = __builtin_nontemporal_load(p + u * BLOCK);
+    else v[u] = p[u * BLOCK];
+  }
+}
+
+template <class OpT, class AccT, class V, int N, int UNROLL>
+__device__ __forceinline__ void consume_tile(AccT (&acc)[UNROLL], const V (&v)[UNROLL]) {
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], static_cast<AccT>(v[u][k]));
+  }
+}
+
+// PIPE: software-pipelined body — tile t+grid's loads are issued before tile t is consumed, so
+// a wave always has UNROLL loads in flight while it computes (two register sets). The loop has
+// no per-load condition (the last tile is peeled), see cdna_hip_programming.md §5 trap (c).
+template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT, bool PIPE>
 __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   using V = typename Vec16<T>::type;
   constexpr int N = Vec16<T>::N;
@@ -107,18 +128,24 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   const V* __restrict__ vin = static_cast<const V*>(a.body);
   constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
   const uint64_t ntiles = a.nvec / kTile;
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const V* p = vin + t * kTile + threadIdx.x;
-    V v[UNROLL];
+  if constexpr (PIPE) {
+    if (blockIdx.x < ntiles) {
+      V cur[UNROLL];
+      load_tile<V, BLOCK, UNROLL, NT>(cur, vin + blockIdx.x * kTile + threadIdx.x);
+      for (uint64_t tn = blockIdx.x + static_cast<uint64_t>(gridDim.x); tn < ntiles; tn += gridDim.x) {
+        V nxt[UNROLL];
+        load_tile<V, BLOCK, UNROLL, NT>(nxt, vin + tn * kTile + threadIdx.x);
+        consume_tile<OpT, AccT, V, N, UNROLL>(acc, cur);
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      if constexpr (NT) v[u] = __builtin_nontemporal_load(p + u * BLOCK);
-      else v[u] = p[u * BLOCK];
+        for (int u = 0; u < UNROLL; ++u) cur[u] = nxt[u];
+      }
+      consume_tile<OpT, AccT, V, N, UNROLL>(acc, cur);
     }
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-#pragma unroll
-      for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], static_cast<AccT>(v[u][k]));
+  } else {
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+      V v[UNROLL];
+      load_tile<V, BLOCK, UNROLL, NT>(v, vin + t * kTile + threadIdx.x);
+      consume_tile<OpT, AccT, V, N, UNROLL>(acc, v);
     }
   }
   // Vectors past the last full tile, grid-strided.
@@ -232,9 +259,9 @@ namespace {
 
 using LaunchFn = void (*)(const kern::Args&, int grid, hipStream_t);
 
-template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT>
+template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT, bool PIPE>
 void launch_stream(const kern::Args& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((kern::reduce_stream<OpT, T, AccT, BLOCK, UNROLL, NT>), dim3(grid), dim3(BLOCK),
+  hipLaunchKernelGGL((kern::reduce_stream<OpT, T, AccT, BLOCK, UNROLL, NT, PIPE>), dim3(grid), dim3(BLOCK),
                      0, s, a);
 }
 
@@ -266,15 +293,22 @@ int combo_index(Op op, DType t, DType acc) {
 constexpr int kCombos = 14;
 
 struct Table {
-  LaunchFn fn[kCombos][kNumBlocks][kNumUnrolls][2];
+  LaunchFn fn[kCombos][kNumBlocks][kNumUnrolls][2][2];  // [..][policy nt][pipelined]
 };
+
+// Pipelined variants need two register sets of UNROLL 16-byte vectors: only where the
+// per-SIMD register budget allows it (BLOCK * UNROLL <= 8192); elsewhere the plain body.
+constexpr bool pipe_ok(int b, int u) { return b * u <= 8192; }
 
 template <class OpT, class T, class AccT, int BI, int UI>
 void fill_one(Table& tb, int c) {
   constexpr int B = kBlocks[BI];
   constexpr int U = kUnrolls[UI];
-  tb.fn[c][BI][UI][0] = launch_stream<OpT, T, AccT, B, U, false>;
-  tb.fn[c][BI][UI][1] = launch_stream<OpT, T, AccT, B, U, true>;
+  constexpr bool P = pipe_ok(B, U);
+  tb.fn[c][BI][UI][0][0] = launch_stream<OpT, T, AccT, B, U, false, false>;
+  tb.fn[c][BI][UI][1][0] = launch_stream<OpT, T, AccT, B, U, true, false>;
+  tb.fn[c][BI][UI][0][1] = launch_stream<OpT, T, AccT, B, U, false, P>;
+  tb.fn[c][BI][UI][1][1] = launch_stream<OpT, T, AccT, B, U, true, P>;
 }
 
 template <class OpT, class T, class AccT, int BI>
@@ -325,14 +359,14 @@ const Table& table() {
 //   128 MB              256 x  4, 3 WG/CU, nt   6.10 TB/s (best; launch + tail dominate)
 // Fewer, fatter workgroups beat the "fill every wave slot" grid (8 WG/CU: 6.91 TB/s at 8 GB).
 struct Defaults {
-  int block, unroll, wg_per_cu, policy;
+  int block, unroll, wg_per_cu, policy, pipeline;
 };
 Defaults tuned_defaults(size_t bytes, DType t) {
   constexpr size_t MB = 1ull << 20;
-  if (t == DType::Float64 && bytes >= 3072 * MB) return {512, 16, 1, 1};
-  if (bytes > 384 * MB) return {256, 2, 3, 1};
-  if (bytes > 192 * MB) return {512, 16, 1, 0};
-  return {256, 4, 3, 1};
+  if (t == DType::Float64 && bytes >= 3072 * MB) return {512, 16, 1, 1, 0};
+  if (bytes > 384 * MB) return {256, 2, 3, 1, 0};
+  if (bytes > 192 * MB) return {512, 16, 1, 0, 0};
+  return {256, 4, 3, 1, 0};
 }
 constexpr int kDefaultGroups = 8;
 
@@ -415,6 +449,7 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   p.unroll = cfg.unroll ? cfg.unroll : d.unroll;
   p.nontemporal = cfg.policy < 0 ? d.policy == 1 : cfg.policy == 1;
   p.single_pass = cfg.single_pass;
+  p.pipelined = (cfg.pipeline < 0 ? d.pipeline == 1 : cfg.pipeline == 1) && p.block * p.unroll <= 8192;
   MIREDUCE_REQUIRE(block_index(p.block) >= 0, "block must be 256, 512 or 1024");
   MIREDUCE_REQUIRE(unroll_index(p.unroll) >= 0, "unroll must be 2, 4, 8 or 16");
   const size_t vec = 16 / es;
@@ -466,7 +501,7 @@ LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out
   a.tickets = ws.tickets();
   a.out = out;
   a.groups = p.groups;
-  const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0];
+  const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0];
   fn(a, p.grid, stream);
   MIREDUCE_HIP_THROW(hipGetLastError());
   if (!p.single_pass) reduce_finalize(ws.partials(), p.grid, acc, op, out, stream);
@@ -483,7 +518,7 @@ LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, 
   kern::Args a = make_args(in, p, t);
   a.partials = partials;
   a.groups = 0;
-  const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0];
+  const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0];
   fn(a, p.grid, stream);
   MIREDUCE_HIP_THROW(hipGetLastError());
   return p;
@@ -518,8 +553,10 @@ std::vector<std::string> compiled_variants() {
   for (int b : kBlocks)
     for (int u : kUnrolls)
       for (int nt = 0; nt < 2; ++nt)
-        v.push_back("block=" + std::to_string(b) + " unroll=" + std::to_string(u) +
-                    (nt ? " policy=nt" : " policy=default"));
+        for (int pp = 0; pp < 2; ++pp)
+          if (!pp || b * u <= 8192)
+            v.push_back("block=" + std::to_string(b) + " unroll=" + std::to_string(u) +
+                        (nt ? " policy=nt" : " policy=default") + (pp ? " pipelined" : ""));
   return v;
 }
 

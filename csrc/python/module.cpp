@@ -38,6 +38,7 @@ py::dict plan_dict(const LaunchPlan& p) {
   d["grid"] = p.grid;
   d["groups"] = p.groups;
   d["nontemporal"] = p.nontemporal;
+  d["pipelined"] = p.pipelined;
   d["single_pass"] = p.single_pass;
   d["head"] = p.head;
   d["nvec"] = p.nvec;
@@ -46,7 +47,7 @@ py::dict plan_dict(const LaunchPlan& p) {
 }
 
 ReduceConfig make_cfg(int block, int unroll, int wg_per_cu, int max_blocks, int groups,
-                      int policy, bool single_pass) {
+                      int policy, bool single_pass, int pipeline = -1) {
   ReduceConfig c;
   c.block = block;
   c.unroll = unroll;
@@ -54,6 +55,7 @@ ReduceConfig make_cfg(int block, int unroll, int wg_per_cu, int max_blocks, int 
   c.max_blocks = max_blocks;
   c.groups = groups;
   c.policy = policy;
+  c.pipeline = pipeline;
   c.single_pass = single_pass;
   return c;
 }
@@ -130,32 +132,33 @@ PYBIND11_MODULE(_C, m) {
       "reduce",
       [](Workspace& ws, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out,
          uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks, int groups,
-         int policy, bool single_pass) {
+         int policy, bool single_pass, int pipeline) {
         const LaunchPlan p = reduce(as_ptr<const void>(in), n, static_cast<DType>(dtype),
                                     static_cast<Op>(op), static_cast<DType>(acc),
                                     as_ptr<void>(out), ws, as_stream(stream),
                                     make_cfg(block, unroll, wg_per_cu, max_blocks, groups,
-                                             policy, single_pass));
+                                             policy, single_pass, pipeline));
         return plan_dict(p);
       },
       py::arg("ws"), py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"),
       py::arg("acc"), py::arg("out_ptr"), py::arg("stream") = 0, py::arg("block") = 0,
       py::arg("unroll") = 0, py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0,
-      py::arg("groups") = 0, py::arg("policy") = -1, py::arg("single_pass") = true);
+      py::arg("groups") = 0, py::arg("policy") = -1, py::arg("single_pass") = true,
+      py::arg("pipeline") = -1);
 
   m.def(
       "plan",
       [](uintptr_t in, uint64_t n, int dtype, int num_cus, int max_grid, int block, int unroll,
-         int wg_per_cu, int max_blocks, int groups, int policy, bool single_pass) {
+         int wg_per_cu, int max_blocks, int groups, int policy, bool single_pass, int pipeline) {
         return plan_dict(plan_reduce(as_ptr<const void>(in), n, static_cast<DType>(dtype),
                                      make_cfg(block, unroll, wg_per_cu, max_blocks, groups,
-                                              policy, single_pass),
+                                              policy, single_pass, pipeline),
                                      num_cus, max_grid));
       },
       py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("num_cus") = 256,
       py::arg("max_grid") = 16384, py::arg("block") = 0, py::arg("unroll") = 0,
       py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0, py::arg("groups") = 0,
-      py::arg("policy") = -1, py::arg("single_pass") = true);
+      py::arg("policy") = -1, py::arg("single_pass") = true, py::arg("pipeline") = -1);
 
   m.def(
       "reduce_partials",

@@ -67,6 +67,7 @@ class KernelConfig:
     groups: int = 0
     nontemporal: Optional[bool] = None  # None: size-dependent tuned choice
     single_pass: bool = True
+    pipelined: Optional[bool] = None    # None: tuned choice
 
     @property
     def policy(self) -> int:
@@ -81,6 +82,7 @@ class KernelConfig:
             groups=self.groups,
             policy=self.policy,
             single_pass=self.single_pass,
+            pipeline=-1 if self.pipelined is None else int(bool(self.pipelined)),
         )
 
 

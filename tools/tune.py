@@ -39,6 +39,7 @@ def main():
     p.add_argument("--wgs", default="0,2,4,8")
     p.add_argument("--groups", default="8")
     p.add_argument("--policies", default="nt,default")
+    p.add_argument("--pipes", default="0", help="comma list of 0/1: software-pipelined body off/on")
     p.add_argument("--json", default="")
     p.add_argument("--top", type=int, default=12)
     a = p.parse_args()
@@ -58,10 +59,14 @@ def main():
 def sweep(a, x, n, dt, dev):
     es = x.element_size()
     variants = []
-    for b, u, w, g, pol in itertools.product(
+    for b, u, w, g, pol, pp in itertools.product(
         [int(v) for v in a.blocks.split(",")], [int(v) for v in a.unrolls.split(",")],
-        [int(v) for v in a.wgs.split(",")], [int(v) for v in a.groups.split(",")], a.policies.split(",")):
-        variants.append(KernelConfig(block=b, unroll=u, wg_per_cu=w, groups=g, nontemporal=None if pol == "auto" else pol == "nt"))
+        [int(v) for v in a.wgs.split(",")], [int(v) for v in a.groups.split(",")], a.policies.split(","),
+        [int(v) for v in a.pipes.split(",")]):
+        if pp and b * u > 8192:
+            continue
+        variants.append(KernelConfig(block=b, unroll=u, wg_per_cu=w, groups=g,
+                                     nontemporal=None if pol == "auto" else pol == "nt", pipelined=bool(pp)))
     r = Reducer(dev)
     out = torch.empty(1, dtype=torch.float64 if dt.is_floating_point else torch.int64, device=dev)
     if a.op != "sum":
@@ -95,15 +100,16 @@ def sweep(a, x, n, dt, dev):
         mn = min(times[i])
         rows.append({
             "block": cfg.block, "unroll": cfg.unroll, "wg_per_cu": cfg.wg_per_cu, "groups": cfg.groups,
-            "policy": {None: "auto", True: "nt", False: "default"}[cfg.nontemporal], "median_ms": med, "min_ms": mn,
+            "policy": {None: "auto", True: "nt", False: "default"}[cfg.nontemporal], "pipe": int(bool(cfg.pipelined)),
+            "median_ms": med, "min_ms": mn,
             "median_TBps": n * es / (med * 1e-3) / 1e12, "best_TBps": n * es / (mn * 1e-3) / 1e12,
         })
     rows.sort(key=lambda r_: r_["median_ms"])
     print(f"dtype={a.dtype} op={a.op} n={n} bytes={n * es} rounds={a.rounds} iters={a.iters}")
     top = a.top if a.top > 0 else len(rows)
-    print(f"{'block':>5} {'unroll':>6} {'wg/cu':>5} {'grp':>3} {'policy':>7} {'median ms':>10} {'TB/s med':>9} {'TB/s best':>9}")
+    print(f"{'block':>5} {'unroll':>6} {'wg/cu':>5} {'grp':>3} {'policy':>7} {'pipe':>4} {'median ms':>10} {'TB/s med':>9} {'TB/s best':>9}")
     for row in rows[:top]:
-        print(f"{row['block']:>5} {row['unroll']:>6} {row['wg_per_cu']:>5} {row['groups']:>3} {row['policy']:>7} "
+        print(f"{row['block']:>5} {row['unroll']:>6} {row['wg_per_cu']:>5} {row['groups']:>3} {row['policy']:>7} {row['pipe']:>4} "
               f"{row['median_ms']:>10.4f} {row['median_TBps']:>9.3f} {row['best_TBps']:>9.3f}")
     return {"n": n, "bytes": n * es, "rows": rows}
 

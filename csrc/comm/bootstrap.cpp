@@ -98,6 +98,8 @@ LaunchEnv launch_env_from_environment() {
 
 TcpBootstrap::TcpBootstrap(const LaunchEnv& env_, double timeout_s) : rank_(env_.rank), world_(env_.world) {
   if (world_ <= 1) return;
+  if (const char* t = env("MIREDUCE_BOOTSTRAP_TIMEOUT")) timeout_s = std::atof(t);  // failure detection knob
+  timeout_s_ = timeout_s;
   addrinfo hints{};
   hints.ai_family = AF_INET;
   hints.ai_socktype = SOCK_STREAM;
@@ -169,12 +171,12 @@ void TcpBootstrap::broadcast(void* data, size_t bytes, int root) {
   if (world_ <= 1) return;
   if (root != 0) {  // relay through rank 0
     if (rank_ == root) send_all(root_fd_, data, bytes);
-    if (rank_ == 0) recv_all(peer_fds_[root], data, bytes, 300.0);
+    if (rank_ == 0) recv_all(peer_fds_[root], data, bytes, timeout_s_);
   }
   if (rank_ == 0) {
     for (int r = 1; r < world_; ++r) send_all(peer_fds_[r], data, bytes);
   } else {
-    recv_all(root_fd_, data, bytes, 300.0);
+    recv_all(root_fd_, data, bytes, timeout_s_);
   }
 }
 
@@ -183,11 +185,11 @@ void TcpBootstrap::allgather(const void* mine, void* all, size_t bytes) {
   std::memcpy(out + static_cast<size_t>(rank_) * bytes, mine, bytes);
   if (world_ <= 1) return;
   if (rank_ == 0) {
-    for (int r = 1; r < world_; ++r) recv_all(peer_fds_[r], out + static_cast<size_t>(r) * bytes, bytes, 300.0);
+    for (int r = 1; r < world_; ++r) recv_all(peer_fds_[r], out + static_cast<size_t>(r) * bytes, bytes, timeout_s_);
     for (int r = 1; r < world_; ++r) send_all(peer_fds_[r], out, bytes * world_);
   } else {
     send_all(root_fd_, mine, bytes);
-    recv_all(root_fd_, out, bytes * world_, 300.0);
+    recv_all(root_fd_, out, bytes * world_, timeout_s_);
   }
 }
 

@@ -53,6 +53,7 @@ class TcpBootstrap {
 
  private:
   int rank_ = 0, world_ = 1;
+  double timeout_s_ = 300.0;  // every exchange fails after this long without progress
   int listen_fd_ = -1;
   int root_fd_ = -1;            // non-root: connection to rank 0
   std::vector<int> peer_fds_;   // rank 0: fd of rank r at [r]

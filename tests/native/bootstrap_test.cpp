@@ -4,12 +4,24 @@
 #include <cstring>
 #include <vector>
 
+#include "mireduce/check.hpp"
 #include "mireduce/comm.hpp"
 
 using namespace mireduce;
 
+int run(const LaunchEnv& env);
+
 int main() {
   LaunchEnv env = launch_env_from_environment();
+  try {
+    return run(env);
+  } catch (const Error& e) {  // failure detection: a missing peer is an error, never a hang
+    std::fprintf(stderr, "bootstrap_test rank %d: %s\n", env.rank, e.what());
+    return 2;
+  }
+}
+
+int run(const LaunchEnv& env) {
   TcpBootstrap boot(env, 60.0);
   int ok = 1;
   char id[128];

@@ -67,3 +67,17 @@ def test_plot_tool(tmp_path):
              "--reference-cuda"], timeout=300)
     assert r.returncode == 0, r.stderr
     assert (tmp_path / "p" / "int.png").exists()
+
+
+@pytest.mark.parametrize("rank", [0, 1])
+def test_bootstrap_missing_peer_fails_fast(rank):
+    # SURVEY §5.3 failure detection: a rank whose peer never shows up gets an error after the
+    # bootstrap timeout instead of hanging.
+    import time
+    t0 = time.time()
+    r = run([os.path.join(BIN, "bootstrap_test")], timeout=60,
+            env={"RANK": str(rank), "WORLD_SIZE": "2", "LOCAL_RANK": str(rank), "MASTER_ADDR": "127.0.0.1",
+                 "MIREDUCE_BOOTSTRAP_PORT": str(free_port()), "MIREDUCE_BOOTSTRAP_TIMEOUT": "2"})
+    assert r.returncode == 2, (r.returncode, r.stderr)
+    assert ("timed out" in r.stderr) or ("cannot connect" in r.stderr)
+    assert time.time() - t0 < 30

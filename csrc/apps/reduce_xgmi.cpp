@@ -50,7 +50,7 @@ constexpr uint64_t kNumDoubles = 256ull * 1024 * 1024;  // mpi/constants.h:2
 const std::set<std::string> kKnown = {"mode", "collective", "dtypes", "ops", "ints", "doubles", "longs", "floats",
                                       "n", "retries", "warmup", "iters", "root", "json", "graph", "mt19937",
                                       "noverify", "seed", "help", "unroll", "block", "wg-per-cu", "policy",
-                                      "units", "timeout", "trace"};
+                                      "units", "timeout", "trace", "single-process"};
 
 struct Ctx {
   LaunchEnv env;
@@ -335,6 +335,145 @@ bool run_scalar(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>&
   return ok;
 }
 
+// ------------------------------------------------------------------------------ single process
+// One process drives every visible GPU (simpleMultiGPU.cpp:185-310): per-GPU local
+// reduce on its own stream, then either one grouped ncclAllReduce over an ncclCommInitAll set
+// (--collective=allreduce) or a host fold of the per-GPU scalars (--collective=host, the
+// simpleMultiGPU way). Scalar mode only.
+bool run_single_process(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>& ops,
+                        const std::vector<uint64_t>& counts, int ndev_req) {
+  const int avail = device_count();
+  const int ndev = ndev_req > 0 ? std::min(ndev_req, avail) : avail;
+  std::vector<int> devs(ndev);
+  for (int i = 0; i < ndev; ++i) devs[i] = i;
+  const bool host_fold = c.collective == "host";
+  c.env.world = ndev;  // the NODES column / JSON "ranks" count GPUs in this mode
+  std::unique_ptr<RcclGroup> group;
+  if (!host_fold) group = std::make_unique<RcclGroup>(devs);
+  struct Dev {
+    hipStream_t s = nullptr;
+    std::unique_ptr<Workspace> ws;
+    DeviceBuffer x, out, oracle;
+    uint64_t count = 0, offset = 0;
+  };
+  std::vector<Dev> d(ndev);
+  for (int i = 0; i < ndev; ++i) {
+    HIP_CHECK(hipSetDevice(devs[i]));
+    HIP_CHECK(hipStreamCreateWithFlags(&d[i].s, hipStreamNonBlocking));
+    d[i].ws = std::make_unique<Workspace>(devs[i]);
+    d[i].out.allocate(8);
+    d[i].oracle.allocate(8);
+  }
+  std::vector<hipStream_t> streams;
+  for (auto& x : d) streams.push_back(x.s);
+  auto sync_all = [&] {
+    for (int i = 0; i < ndev; ++i) {
+      HIP_CHECK(hipSetDevice(devs[i]));
+      HIP_CHECK(hipStreamSynchronize(d[i].s));
+    }
+  };
+  std::printf("%s\n", gnuplot_header().c_str());
+  bool ok = true;
+  for (size_t k = 0; k < dtypes.size(); ++k) {
+    const DType t = dtypes[k];
+    const uint64_t n = counts[k];
+    for (int i = 0; i < ndev; ++i) {
+      const uint64_t base = n / ndev, rem = n % ndev;
+      d[i].count = base + (static_cast<uint64_t>(i) < rem ? 1 : 0);
+      d[i].offset = i * base + std::min<uint64_t>(i, rem);
+      HIP_CHECK(hipSetDevice(devs[i]));
+      d[i].x.allocate(std::max<uint64_t>(d[i].count, 1) * dtype_size(t));
+      FillSpec fs;
+      fs.pattern = dtype_is_float(t) ? Pattern::Uniform : Pattern::FullRange;
+      fs.seed = c.seed;
+      fs.offset = d[i].offset;
+      fill_device(d[i].x.get(), d[i].count, t, fs, d[i].s);
+    }
+    sync_all();
+    for (Op o : ops) {
+      const DType acc = default_acc(t, o);
+      const size_t as = dtype_size(acc);
+      unsigned char folded[8] = {0};
+      auto step = [&] {
+        for (int i = 0; i < ndev; ++i) {
+          HIP_CHECK(hipSetDevice(devs[i]));
+          reduce(d[i].x.get(), d[i].count, t, o, acc, d[i].out.get(), *d[i].ws, d[i].s, c.kcfg);
+        }
+        if (group) {
+          std::vector<const void*> snd;
+          std::vector<void*> rcv;
+          for (auto& x : d) {
+            snd.push_back(x.out.get());
+            rcv.push_back(x.out.get());
+          }
+          group->allreduce(snd, rcv, 1, acc, o, streams);
+        }
+      };
+      auto finish = [&] {  // host fold of the per-GPU scalars (simpleMultiGPU.cpp:263-275)
+        sync_all();
+        if (!host_fold) return;
+        std::vector<unsigned char> parts(as * ndev);
+        for (int i = 0; i < ndev; ++i) {
+          HIP_CHECK(hipSetDevice(devs[i]));
+          HIP_CHECK(hipMemcpy(&parts[i * as], d[i].out.get(), as, hipMemcpyDeviceToHost));
+        }
+        cpu_fold(parts.data(), ndev, acc, o, folded);
+      };
+      for (int w = 0; w < c.warmup; ++w) {
+        step();
+        finish();
+      }
+      for (int x_ = 0; x_ < c.retries; ++x_) {
+        const double t0 = StopWatch::now_s();
+        for (int it = 0; it < c.iters; ++it) {
+          step();
+          if (host_fold) finish();
+        }
+        finish();
+        const double dt = (StopWatch::now_s() - t0) / c.iters;
+        const double bytes = static_cast<double>(n) * dtype_size(t);
+        Json j;
+        j.set("single_process", true).set("devices", ndev).set("n_total", n).set("retry", x_);
+        if (c.verify && x_ == 0) {
+          // oracle: the two-launch path per GPU, folded on the host
+          std::vector<unsigned char> parts(as * ndev);
+          ReduceConfig two = c.kcfg;
+          two.single_pass = false;
+          for (int i = 0; i < ndev; ++i) {
+            HIP_CHECK(hipSetDevice(devs[i]));
+            reduce(d[i].x.get(), d[i].count, t, o, acc, d[i].oracle.get(), *d[i].ws, d[i].s, two);
+            HIP_CHECK(hipStreamSynchronize(d[i].s));
+            HIP_CHECK(hipMemcpy(&parts[i * as], d[i].oracle.get(), as, hipMemcpyDeviceToHost));
+          }
+          unsigned char expect[8] = {0}, got[8] = {0};
+          cpu_fold(parts.data(), ndev, acc, o, expect);
+          if (host_fold) {
+            std::memcpy(got, folded, as);
+          } else {
+            HIP_CHECK(hipSetDevice(devs[0]));
+            HIP_CHECK(hipMemcpy(got, d[0].out.get(), as, hipMemcpyDeviceToHost));
+          }
+          bool vok;
+          if (dtype_is_float(acc) && o == Op::Sum) {
+            const double gv = acc_as_double(got, acc), ev = acc_as_double(expect, acc);
+            vok = std::fabs(gv - ev) <= 1e-9 * (std::fabs(ev) + 1.0);
+          } else {
+            vok = std::memcmp(got, expect, as) == 0;
+          }
+          ok = ok && vok;
+          j.set("verified", vok);
+        }
+        emit(c, t, o, bytes, dt, j);
+      }
+    }
+  }
+  for (int i = 0; i < ndev; ++i) {
+    HIP_CHECK(hipSetDevice(devs[i]));
+    HIP_CHECK(hipStreamDestroy(d[i].s));
+  }
+  return ok;
+}
+
 void usage() {
   std::printf(
       "reduce_xgmi — RCCL-over-xGMI reduction benchmark (one process per GPU)\n"
@@ -345,6 +484,8 @@ void usage() {
       "  --ints=N --doubles=N --longs=N --floats=N   global element counts (reduce.c defaults)\n"
       "  --n=N                        global count for every dtype (scalar mode north star: 1e9)\n"
       "  --graph                      replay the timed iterations from a captured hipGraph\n"
+      "  --single-process[=N]         one process drives N (all) GPUs, scalar mode: grouped RCCL over\n"
+      "                               ncclCommInitAll (--collective=allreduce) or host fold (--collective=host)\n"
       "  --mt19937                    vector mode: reduce.c's exact per-rank MT19937 data (host-generated)\n"
       "  --units=gib|gb               GNUPlot column unit (default gib = reduce.c's 2^30)\n"
       "  --json=PATH  --noverify  --seed=N  --block= --unroll= --wg-per-cu= --policy=auto|nt|default\n"
@@ -376,8 +517,15 @@ int main(int argc, char** argv) {
     c.mode = args.str_or("mode", "vector");
     if (c.mode != "vector" && c.mode != "scalar") throw CliError("--mode must be vector|scalar");
     c.collective = args.str_or("collective", c.mode == "vector" ? "reduce" : "allreduce");
-    if (c.collective != "reduce" && c.collective != "allreduce" && c.collective != "direct" && c.collective != "direct-reduce")
+    if (args.has("single-process")) {
+      if (c.mode != "scalar") throw CliError("--single-process is scalar-mode only");
+      if (c.collective != "allreduce" && c.collective != "host")
+        throw CliError("--single-process takes --collective=allreduce|host");
+      if (c.env.world != 1) throw CliError("--single-process runs without a multi-process launcher");
+    } else if (c.collective != "reduce" && c.collective != "allreduce" && c.collective != "direct" &&
+               c.collective != "direct-reduce") {
       throw CliError("--collective must be reduce|allreduce|direct|direct-reduce");
+    }
     if (c.mode == "scalar" && (c.collective == "direct" || c.collective == "direct-reduce"))
       throw CliError("direct collectives are vector-mode only");
     if (c.mode == "scalar" && c.collective != "allreduce") throw CliError("scalar mode uses --collective=allreduce");
@@ -437,6 +585,19 @@ int main(int argc, char** argv) {
   if (ndev == 0) {
     std::fprintf(stderr, "[rank %d] no HIP device\n", c.env.rank);
     return EXIT_FAILURE;
+  }
+  if (args.has("single-process")) {
+    bool sp_ok = false;
+    try {
+      c.boot = std::make_unique<TcpBootstrap>(c.env);  // world 1: no sockets
+      std::vector<uint64_t> counts;
+      for (DType t : dtypes) counts.push_back(global_count(t, ints, longs, floats, doubles));
+      sp_ok = run_single_process(c, dtypes, ops, counts, args.int_or<int>("single-process", 0));
+      if (c.verify) std::fprintf(stderr, "[reduce_xgmi] verification %s\n", sp_ok ? "PASSED" : "FAILED");
+    } catch (const Error& e) {
+      std::fprintf(stderr, "error: %s\n", e.what());
+    }
+    return sp_ok ? EXIT_SUCCESS : EXIT_FAILURE;
   }
   c.device = c.env.local_rank % ndev;
   HIP_CHECK(hipSetDevice(c.device));

@@ -127,6 +127,32 @@ int RcclComm::version() {
   return v;
 }
 
+RcclGroup::RcclGroup(const std::vector<int>& devices) : devices_(devices), comms_(devices.size(), nullptr) {
+  StdoutToStderr quiet;
+  check(ncclCommInitAll(comms_.data(), static_cast<int>(devices_.size()), devices_.data()), "ncclCommInitAll");
+}
+
+RcclGroup::~RcclGroup() {
+  for (ncclComm_t c : comms_)
+    if (c) ncclCommDestroy(c);
+}
+
+void RcclGroup::allreduce(const std::vector<const void*>& send, const std::vector<void*>& recv, size_t count, DType t,
+                          Op o, const std::vector<hipStream_t>& streams) {
+  check(ncclGroupStart(), "ncclGroupStart");
+  for (size_t i = 0; i < comms_.size(); ++i)
+    check(ncclAllReduce(send[i], recv[i], count, nccl_type(t), nccl_op(o), comms_[i], streams[i]), "ncclAllReduce");
+  check(ncclGroupEnd(), "ncclGroupEnd");
+}
+
+void RcclGroup::reduce(const std::vector<const void*>& send, const std::vector<void*>& recv, size_t count, DType t,
+                       Op o, int root, const std::vector<hipStream_t>& streams) {
+  check(ncclGroupStart(), "ncclGroupStart");
+  for (size_t i = 0; i < comms_.size(); ++i)
+    check(ncclReduce(send[i], recv[i], count, nccl_type(t), nccl_op(o), root, comms_[i], streams[i]), "ncclReduce");
+  check(ncclGroupEnd(), "ncclGroupEnd");
+}
+
 void install_comm_abort_hook(RcclComm* comm) {
   g_abort_comm = comm;
   set_fatal_hook(comm ? abort_hook : nullptr);

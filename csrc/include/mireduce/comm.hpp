@@ -88,6 +88,27 @@ class RcclComm {
   int rank_ = 0, world_ = 1;
 };
 
+// Single-process multi-GPU communicator set (ncclCommInitAll over `devices`): the
+// simpleMultiGPU / P9 layout (cuda/C/src/simpleMultiGPU/simpleMultiGPU.cpp:185-310), with the
+// per-device collectives issued inside one ncclGroupStart/End.
+class RcclGroup {
+ public:
+  explicit RcclGroup(const std::vector<int>& devices);
+  ~RcclGroup();
+  RcclGroup(const RcclGroup&) = delete;
+  RcclGroup& operator=(const RcclGroup&) = delete;
+  int size() const { return static_cast<int>(devices_.size()); }
+  int device(int i) const { return devices_[i]; }
+  void allreduce(const std::vector<const void*>& send, const std::vector<void*>& recv, size_t count, DType t, Op o,
+                 const std::vector<hipStream_t>& streams);
+  void reduce(const std::vector<const void*>& send, const std::vector<void*>& recv, size_t count, DType t, Op o,
+              int root, const std::vector<hipStream_t>& streams);
+
+ private:
+  std::vector<int> devices_;
+  std::vector<ncclComm_t> comms_;
+};
+
 // Register `comm` for the fatal-error hook: HIP_CHECK failures abort it before exiting.
 void install_comm_abort_hook(RcclComm* comm);
 

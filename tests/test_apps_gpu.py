@@ -122,3 +122,14 @@ def test_bench_rehearsal_two_ranks_one_gpu(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["verified"] is True and d["n_gpus"] == 2 and d["config"]["backend"] == "gloo"
+
+
+@pytest.mark.parametrize("collective", ["allreduce", "host"])
+def test_reduce_xgmi_single_process(collective):
+    # simpleMultiGPU / P9: one process drives every visible GPU (one on this box).
+    r = run([os.path.join(BIN, "reduce_xgmi"), "--single-process", "--mode=scalar", f"--collective={collective}",
+             "--n=30000001", "--dtypes=INT,DOUBLE", "--retries=2", "--iters=3"], timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "verification PASSED" in r.stderr
+    rows = [ln for ln in r.stdout.splitlines() if re.match(r"^(INT|DOUBLE) (MAX|MIN|SUM) \d+ +[0-9.]+$", ln)]
+    assert len(rows) == 12 and r.stdout.splitlines()[0] == "# DATATYPE OP NODES GB/sec"

@@ -134,3 +134,23 @@ def test_bench_vector_config1_two_cpu_ranks(tmp_path):
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["unit"] == "GiB/s" and d["n_ranks"] == 2 and d["verified"] is True
     assert d["config"]["global_batch"] == 1 << 20 and d["device"] == "cpu"
+
+
+def moments_case(rank, world):
+    from cuda_mpi_reductions_amd.ops import moments, synthetic
+    from cuda_mpi_reductions_amd.parallel import dist as pdist
+    ctx = pdist.init(device_type="cpu")
+    full = synthetic(100_003, torch.float64, seed=11) * 4 + 10
+    off, cnt = pdist.shard(full.numel(), rank, world)
+    m = moments(full[off:off + cnt])       # combined across ranks (Chan update)
+    pdist.shutdown(ctx)
+    return {"mean": m["mean"], "var": m["var"], "min": m["min"], "max": m["max"], "count": m["count"],
+            "ref": (full.mean().item(), full.var(unbiased=False).item(), full.min().item(), full.max().item())}
+
+
+def test_moments_across_ranks():
+    out = _spawn("moments_case", 3)
+    for res in out.values():
+        mean, var, mn, mx = res["ref"]
+        assert res["count"] == 100_003 and res["min"] == mn and res["max"] == mx
+        assert abs(res["mean"] - mean) < 1e-12 and abs(res["var"] - var) < 1e-12

@@ -528,7 +528,8 @@ int main(int argc, char** argv) {
     }
     if (c.mode == "scalar" && (c.collective == "direct" || c.collective == "direct-reduce"))
       throw CliError("direct collectives are vector-mode only");
-    if (c.mode == "scalar" && c.collective != "allreduce") throw CliError("scalar mode uses --collective=allreduce");
+    if (c.mode == "scalar" && c.collective != "allreduce" && !(args.has("single-process") && c.collective == "host"))
+      throw CliError("scalar mode uses --collective=allreduce (or host with --single-process)");
     std::vector<std::string> list;
     if (args.get_list("dtypes", &list)) {
       dtypes.clear();

@@ -54,7 +54,7 @@ struct Options {
   DType acc = DType::Int32;
   bool acc_given = false;
   uint64_t n = 1ull << 24;  // reduction.cpp:665
-  int threads = 256;        // reduction.cpp:666
+  int threads = 0;          // 0 = tuned plan (kernels 7/8) / 256 (ladder); reference 256 (reduction.cpp:666)
   int kernel = 7;
   int max_blocks = 0;       // 0 = persistent grid (reference default 64, reduction.cpp:668)
   bool cpufinal = false;
@@ -82,7 +82,8 @@ void usage() {
       "reduction --method=SUM|MIN|MAX [options]\n"
       "  --type=int|int64|float|double  element type (case-insensitive, default int)\n"
       "  --n=N            elements (default 16777216; k/M/G suffixes and 1e9 accepted)\n"
-      "  --threads=256|512|1024  workgroup size   --kernel=0..8 (7 = single-pass, default)\n"
+      "  --threads=256|512|1024  workgroup size (default: tuned plan; 256 = reference)\n"
+      "  --kernel=0..8    7 = single-pass (default), 8 = two-launch, 0..6 = Harris ladder\n"
       "  --maxblocks=N    cap the grid (default: persistent grid, 8 WG/CU)\n"
       "  --cpufinal       fold the per-workgroup partials on the host\n"
       "  --cputhresh=N    fold on the host when <= N partials remain\n"
@@ -218,7 +219,8 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
   Logger& L = Logger::instance();
   L.log(kLogBoth, "METHOD: %s\n", op_name(o.op));
   L.log(kLogBoth, "%" PRIu64 " elements\n", o.n);
-  L.log(kLogBoth, "%d threads (max)\n", o.threads);
+  if (o.threads) L.log(kLogBoth, "%d threads (max)\n", o.threads);
+  else L.log(kLogBoth, "tuned threads (max)\n");
 
   Buffers b;
   const size_t es = dtype_size(o.dtype);
@@ -417,6 +419,7 @@ int main(int argc, char** argv) {
     if (o.kernel < 0 || o.kernel > 8) throw CliError("--kernel must be 0..8");
     if (o.kernel >= 7 && o.threads != 0 && o.threads != 256 && o.threads != 512 && o.threads != 1024)
       throw CliError("--threads must be 256, 512 or 1024 for kernels 7/8");
+    if (o.kernel <= 6 && o.threads == 0) o.threads = 256;
     if (o.kernel <= 6 && (o.threads < 64 || o.threads > 1024 || (o.threads & (o.threads - 1))))
       throw CliError("--threads must be a power of two in [64, 1024] for kernels 0..6");
     if (o.iterations < 1) throw CliError("--iterations must be >= 1");

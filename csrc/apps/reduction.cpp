@@ -151,13 +151,14 @@ struct Runner {
     const void* in = b.in.get();
     if (o.kernel <= 6) {
       const int mb = o.max_blocks > 0 ? o.max_blocks : 64;  // reference default (reduction.cpp:668)
-      const size_t need = ladder_scratch_bytes(o.kernel, n, o.threads, mb);
+      const int th = o.threads ? o.threads : 256;            // reference default (reduction.cpp:666)
+      const size_t need = ladder_scratch_bytes(o.kernel, n, th, mb);
       if (b.ladder.bytes() < need) {  // grows during the warm-up call only
         HIP_CHECK(hipStreamSynchronize(s));
         b.ladder.allocate(need);
       }
-      plan.block = o.threads;
-      plan.grid = ladder_reduce(o.kernel, in, n, o.dtype, o.op, o.acc, b.out.get(), b.ladder.get(), o.threads, mb, s);
+      plan.block = th;
+      plan.grid = ladder_reduce(o.kernel, in, n, o.dtype, o.op, o.acc, b.out.get(), b.ladder.get(), th, mb, s);
       return false;
     }
     const bool want_host = o.cpufinal || o.cputhresh > 1;

@@ -43,6 +43,8 @@ def parse_args(argv=None):
     p.add_argument("--config", default=NORTH_STAR, choices=sorted(CONFIGS))
     p.add_argument("--elements", type=int, default=None, help="override the global element count")
     p.add_argument("--serial", action="store_true", help="no overlap between consecutive steps")
+    p.add_argument("--streams", type=int, default=1,
+                   help="alternate independent steps over this many HIP streams (each with its own workspace)")
     p.add_argument("--block", type=int, default=0)
     p.add_argument("--unroll", type=int, default=0)
     p.add_argument("--wg-per-cu", type=int, default=0)
@@ -126,7 +128,7 @@ def main(argv=None) -> int:
                           groups=args.groups,
                           nontemporal=None if args.policy == "auto" else args.policy == "nt",
                           single_pass=not args.two_pass)
-    wl = ScalarReduction(cfg, ctx, kernel).setup()
+    wl = ScalarReduction(cfg, ctx, kernel, streams=1 if args.serial else args.streams).setup()
     K, W = args.steps, args.warmup
     slots = wl.new_slots(W + K)
     dev = ctx.device
@@ -199,6 +201,7 @@ def main(argv=None) -> int:
                 "bytes_per_step": bytes_step,
                 "op": cfg.op.upper(),
                 "overlap": "serial" if args.serial else "pipelined (step i+1 local reduce || step i all-reduce)",
+                "streams": len(wl.lanes) if wl.lanes else 1,
                 "kernel_plan": wl.reducer.last_plan if wl.reducer else None,
             },
             "per_gpu_gbps": round(gbps / ctx.world_size, 3),

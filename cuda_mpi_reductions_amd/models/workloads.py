@@ -82,7 +82,7 @@ class ScalarReduction:
 
     def __init__(self, cfg: WorkloadConfig, ctx: pdist.DistContext,
                  kernel: Optional[KernelConfig] = None, seed: int = 0x5EED,
-                 acc_dtype: Optional[torch.dtype] = None):
+                 acc_dtype: Optional[torch.dtype] = None, streams: int = 1):
         if cfg.mode != "scalar":
             raise ValueError("ScalarReduction needs a scalar-mode config")
         self.cfg = cfg
@@ -95,6 +95,11 @@ class ScalarReduction:
         self.count = 0
         self.n_total = 0
         self.reducer: Optional[Reducer] = None
+        # Independent steps may alternate over `streams` HIP streams (one Reducer — one ticket
+        # workspace — per stream), so step i+1's ramp-up overlaps step i's tail.
+        self.n_streams = max(1, int(streams))
+        self.lanes: list = []
+        self._next = 0
 
     # ------------------------------------------------------------------ setup
     def _size_for_hbm(self) -> int:
@@ -122,6 +127,9 @@ class ScalarReduction:
         fill_(self.x, self.cfg.pattern, seed=self.seed, offset=self.offset)
         if dev.type == "cuda":
             self.reducer = Reducer(dev, config=self.kernel)
+            self.lanes = [(torch.cuda.current_stream(dev), self.reducer)]
+            for _ in range(self.n_streams - 1):
+                self.lanes.append((torch.cuda.Stream(dev), Reducer(dev, config=self.kernel)))
             torch.cuda.synchronize(dev)
         return self
 
@@ -142,6 +150,14 @@ class ScalarReduction:
     def step(self, out: torch.Tensor, async_op: bool = True):
         """Local reduce into ``out`` (1 element) then all-reduce it across ranks. Returns the
         collective's work handle (``None`` for a single rank)."""
+        if len(self.lanes) > 1:
+            stream, reducer = self.lanes[self._next % len(self.lanes)]
+            self._next += 1
+            with torch.cuda.stream(stream):
+                reducer(self.x, self.cfg.op, self.acc, out=out)
+                if self.ctx.world_size == 1:
+                    return None
+                return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op)
         self.local(out)
         if self.ctx.world_size == 1:
             return None

@@ -1,0 +1,46 @@
+"""Examples and the Python CLI front-end."""
+import os
+import re
+import sys
+
+import pytest
+
+from helpers import ROOT, run, torchrun
+
+
+def test_example_distributed_sum_cpu(tmp_path):
+    r = torchrun(2, [os.path.join(ROOT, "examples", "02_distributed_sum.py"), "--cpu"], cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert re.search(r"2 ranks: sum = [0-9.]+  verified=True", r.stdout)
+
+
+def test_example_vector_reduce_cpu(tmp_path):
+    r = torchrun(2, [os.path.join(ROOT, "examples", "03_vector_reduce.py")], cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.count("verified=True") == 3
+
+
+def test_python_cli_grammar_errors(tmp_path):
+    r = run([sys.executable, "-m", "cuda_mpi_reductions_amd", "--type=double"], cwd=ROOT)
+    assert r.returncode == 1 and "MISSING --method FLAG." in r.stderr
+    r = run([sys.executable, "-m", "cuda_mpi_reductions_amd", "--method=sum"], cwd=ROOT)
+    assert r.returncode == 1 and "No --method specified!" in r.stderr
+    r = run([sys.executable, "-m", "cuda_mpi_reductions_amd", "--method=SUM", "oops"], cwd=ROOT)
+    assert r.returncode == 1 and "Invalid command line argument" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,type_", [("SUM", "double"), ("MIN", "int64"), ("MAX", "float"), ("SUM", "int")])
+def test_python_cli_gpu(method, type_):
+    r = run([sys.executable, "-m", "cuda_mpi_reductions_amd", f"--method={method}", f"--type={type_}",
+             "--n=4000037", "--iterations=5", "--qatest"], cwd=ROOT, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "&&&& PASSED" in r.stderr
+    assert re.search(r"Reduction, Throughput = [0-9.]+ GB/s, Time = [0-9.]+ s, Size = 4000037 Elements", r.stdout)
+
+
+@pytest.mark.gpu
+def test_example_single_gpu():
+    r = run([sys.executable, os.path.join(ROOT, "examples", "01_single_gpu.py")], cwd=ROOT, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "GB/s" in r.stdout

@@ -90,7 +90,8 @@ void usage() {
       "  --shmoo          sweep n = 1..32M (powers of two) over kernels, print CSV\n"
       "  --iterations=100 --acc=TYPE --unroll=2|4|8 --wg-per-cu=N --policy=auto|nt|default\n"
       "  --pattern=smallint|uniform|fullrange|iotamod --seed=N --fill=host|device --noverify\n"
-      "  --device=N --json=PATH --log=FILE|none --master-log=FILE --qatest --prompt --countdown\n"
+      "  --device=N --json=PATH --log=FILE|none --master-log=FILE|none (default SdkMasterLog.csv) --qatest\n"
+      "  --prompt --countdown\n"
       "  --trace          roctx ranges per iteration (rocprofv3 --marker-trace)\n");
 }
 
@@ -360,7 +361,9 @@ int main(int argc, char** argv) {
   Logger& L = Logger::instance();
   const std::string log = args.str_or("log", "reduction.txt");
   if (log != "none") L.set_log_file(log);  // shrSetLogFileName("reduction.txt") (reduction.cpp:88)
-  L.set_master_file(args.str_or("master-log", ""));
+  // shrLogEx(LOGBOTH | MASTER) appends to SdkMasterLog.csv by default (shrUtils.h:86)
+  const std::string master = args.str_or("master-log", "SdkMasterLog.csv");
+  if (master != "none") L.set_master_file(master);
   L.set_quiet(args.has("quiet"));
   set_tracing(args.has("trace"));
   for (const auto& u : args.unknown(kKnown)) std::fprintf(stderr, "warning: unknown flag --%s ignored\n", u.c_str());

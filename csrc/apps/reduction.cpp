@@ -60,6 +60,7 @@ struct Options {
   bool cpufinal = false;
   int cputhresh = 1;        // reduction.cpp:670
   int iterations = 100;     // reduction.cpp:731
+  bool batch_timing = false;  // one event pair around all iterations (throughput) vs per iteration
   int unroll = 0;
   int wg_per_cu = 0;
   int policy = -1;
@@ -75,7 +76,7 @@ const std::set<std::string> kKnown = {
     "method", "type", "n", "threads", "kernel", "maxblocks", "cpufinal", "cputhresh", "shmoo",
     "device", "qatest", "noprompt", "prompt", "help", "quiet", "iterations", "acc", "unroll",
     "wg-per-cu", "policy", "pattern", "seed", "fill", "noverify", "json", "log", "master-log",
-    "countdown", "shmoo-max", "trace"};
+    "countdown", "shmoo-max", "trace", "timing"};
 
 void usage() {
   std::printf(
@@ -87,7 +88,8 @@ void usage() {
       "  --maxblocks=N    cap the grid (default: persistent grid, 8 WG/CU)\n"
       "  --cpufinal       fold the per-workgroup partials on the host\n"
       "  --cputhresh=N    fold on the host when <= N partials remain\n"
-      "  --shmoo          sweep n = 1..32M (powers of two) over kernels, print CSV\n"
+      "  --shmoo          sweep n = 1..32M (powers of two, --shmoo-max=N) over kernels, print CSV\n"
+      "  --timing=per-iter|batch  event pair per iteration (reference, default) or around all (shmoo default)\n"
       "  --iterations=100 --acc=TYPE --unroll=2|4|8 --wg-per-cu=N --policy=auto|nt|default\n"
       "  --pattern=smallint|uniform|fullrange|iotamod --seed=N --fill=host|device --noverify\n"
       "  --device=N --json=PATH --log=FILE|none --master-log=FILE|none (default SdkMasterLog.csv) --qatest\n"
@@ -191,6 +193,17 @@ Timing time_iterations(Runner& r, uint64_t n, int iters) {
   Timing t;
   EventTimer ev;
   HIP_CHECK(hipDeviceSynchronize());
+  const bool host_path = r.o.kernel >= 7 && (r.o.cpufinal || r.o.cputhresh > 1);
+  if (r.o.batch_timing && !host_path) {  // back-to-back launches, one event pair: throughput
+    ev.start(r.s);
+    for (int i = 0; i < iters; ++i) r.run_once(n, t.result);
+    ev.stop(r.s);
+    const double ms = ev.elapsed_ms();
+    t.ms.assign(iters, ms / iters);
+    t.avg_ms = ms / iters;
+    HIP_CHECK(hipMemcpy(t.result, r.b.out.get(), dtype_size(r.o.acc), hipMemcpyDeviceToHost));
+    return t;
+  }
   for (int i = 0; i < iters; ++i) {
     const double h0 = StopWatch::now_s();
     ev.start(r.s);
@@ -420,6 +433,11 @@ int main(int argc, char** argv) {
     o.verify = !args.has("noverify");
     o.json = args.str_or("json", "");
     o.device = args.int_or<int>("device", 0);
+    {
+      const std::string tm = args.str_or("timing", args.has("shmoo") ? "batch" : "per-iter");
+      if (tm != "batch" && tm != "per-iter") throw CliError("--timing must be per-iter|batch");
+      o.batch_timing = tm == "batch";
+    }
     if (o.kernel < 0 || o.kernel > 8) throw CliError("--kernel must be 0..8");
     if (o.kernel >= 7 && o.threads != 0 && o.threads != 256 && o.threads != 512 && o.threads != 1024)
       throw CliError("--threads must be 256, 512 or 1024 for kernels 7/8");

@@ -12,6 +12,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("-o", "--out", default="shmoo.png")
+    ap.add_argument("--title", default="MI355X reduction shmoo (float64 SUM)")
     a = ap.parse_args()
     import matplotlib
     matplotlib.use("Agg")
@@ -34,7 +35,7 @@ def main():
     ax.set_yscale("log")
     ax.set_xlabel("array bytes")
     ax.set_ylabel("GB/s (1e9 B)")
-    ax.set_title("MI355X reduction shmoo (float64 SUM)")
+    ax.set_title(a.title)
     ax.legend(fontsize=7, loc="upper left")
     fig.tight_layout()
     fig.savefig(a.out, dpi=120)

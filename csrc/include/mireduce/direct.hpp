@@ -38,6 +38,7 @@ class DirectPeers {
   void* out() const { return out_; }
   size_t bytes() const { return bytes_; }
   bool finegrained() const { return finegrained_; }
+  int device() const { return device_; }
 
   // out[i] = op over ranks of in[i], on every rank (one-shot reduce-scatter + all-gather).
   void allreduce(size_t count, DType t, Op op, hipStream_t s);

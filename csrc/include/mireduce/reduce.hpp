@@ -87,6 +87,26 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
 LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
                   hipStream_t stream, const ReduceConfig& cfg = {});
 
+// A reduction whose plan, kernel variant and arguments are resolved once. launch() is a single
+// kernel launch (plus the finalize launch in two-pass mode) with no planning or argument
+// marshalling: the per-step path of bench loops and hipGraph capture. The buffers and the
+// workspace must outlive the object; same concurrency rule as Workspace.
+class BoundReduce {
+ public:
+  BoundReduce(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
+              const ReduceConfig& cfg = {});
+  ~BoundReduce();
+  BoundReduce(const BoundReduce&) = delete;
+  BoundReduce& operator=(const BoundReduce&) = delete;
+  // `out` (optional) redirects the result to another accumulator slot for this launch.
+  void launch(hipStream_t stream, void* out = nullptr) const;
+  const LaunchPlan& plan() const;
+
+ private:
+  struct Impl;
+  Impl* impl_;
+};
+
 // First level only: writes plan.grid partials (element type `acc`) to `partials`.
 LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, void* partials,
                            int max_grid, int num_cus, hipStream_t stream,

@@ -508,6 +508,43 @@ LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out
   return p;
 }
 
+struct BoundReduce::Impl {
+  kern::Args args;
+  LaunchFn fn;
+  LaunchPlan plan;
+  Op op;
+  DType acc;
+};
+
+BoundReduce::BoundReduce(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
+                         const ReduceConfig& cfg)
+    : impl_(nullptr) {
+  const int c = combo_index(op, t, acc);
+  MIREDUCE_REQUIRE(c >= 0, "unsupported (dtype, op, accumulator) combination");
+  MIREDUCE_REQUIRE(out != nullptr, "output pointer is null");
+  const LaunchPlan p = plan_reduce(in, n, t, cfg, ws.num_cus(), ws.max_grid());
+  kern::Args a = make_args(in, p, t);
+  a.partials = ws.partials();
+  a.group_partials = ws.group_partials();
+  a.tickets = ws.tickets();
+  a.out = out;
+  a.groups = p.groups;
+  impl_ = new Impl{a, table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0],
+                   p, op, acc};
+}
+
+BoundReduce::~BoundReduce() { delete impl_; }
+
+void BoundReduce::launch(hipStream_t stream, void* out) const {
+  kern::Args a = impl_->args;
+  if (out) a.out = out;
+  impl_->fn(a, impl_->plan.grid, stream);
+  MIREDUCE_HIP_THROW(hipGetLastError());
+  if (!impl_->plan.single_pass) reduce_finalize(a.partials, impl_->plan.grid, impl_->acc, impl_->op, a.out, stream);
+}
+
+const LaunchPlan& BoundReduce::plan() const { return impl_->plan; }
+
 LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, void* partials,
                            int max_grid, int num_cus, hipStream_t stream, const ReduceConfig& cfg) {
   const int c = combo_index(op, t, acc);

@@ -85,6 +85,29 @@ PYBIND11_MODULE(_C, m) {
   m.attr("OP_MAX") = static_cast<int>(Op::Max);
   m.attr("TICKET_STRIDE") = kTicketStride;
 
+  // Read and clear the calling thread's sticky HIP error (e.g. left behind by an aborted
+  // stream capture, which would otherwise fail the next unrelated kernel-launch check).
+  m.def("hip_get_last_error", [] {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? std::string() : std::string(hipGetErrorName(e)) + ": " + hipGetErrorString(e);
+  });
+
+  // Capture state of a stream (0 none, 1 active, 2 invalidated) and a forced end of capture:
+  // recovery after a capture aborted by an exception (bench falls back to eager issue).
+  m.def("stream_capture_status", [](uintptr_t stream) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    const hipError_t e = hipStreamIsCapturing(as_stream(stream), &st);
+    if (e != hipSuccess) (void)hipGetLastError();
+    return static_cast<int>(st);
+  });
+  m.def("end_capture", [](uintptr_t stream) {
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(as_stream(stream), &g);
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    return e == hipSuccess ? std::string() : std::string(hipGetErrorName(e));
+  });
+
   m.def("device_count", [] {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -127,6 +150,24 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("max_grid", &Workspace::max_grid)
       .def_property_readonly("partials_ptr", [](const Workspace& w) { return reinterpret_cast<uintptr_t>(w.partials()); })
       .def("reset", [](Workspace& w, uintptr_t stream) { w.reset(as_stream(stream)); }, py::arg("stream") = 0);
+
+  // Prepared launch for per-step loops: launch(stream) is one positional-argument call.
+  py::class_<BoundReduce>(m, "BoundReduce")
+      .def(py::init([](Workspace& ws, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out,
+                       int block, int unroll, int wg_per_cu, int max_blocks, int groups, int policy,
+                       bool single_pass, int pipeline) {
+             return new BoundReduce(as_ptr<const void>(in), n, static_cast<DType>(dtype), static_cast<Op>(op),
+                                    static_cast<DType>(acc), as_ptr<void>(out), ws,
+                                    make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass,
+                                             pipeline));
+           }),
+           py::arg("ws"), py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"), py::arg("acc"),
+           py::arg("out_ptr"), py::arg("block") = 0, py::arg("unroll") = 0, py::arg("wg_per_cu") = 0,
+           py::arg("max_blocks") = 0, py::arg("groups") = 0, py::arg("policy") = -1,
+           py::arg("single_pass") = true, py::arg("pipeline") = -1, py::keep_alive<1, 2>())
+      .def("launch", [](const BoundReduce& b, uintptr_t stream, uintptr_t out) { b.launch(as_stream(stream), as_ptr<void>(out)); },
+           py::arg("stream"), py::arg("out_ptr") = 0)
+      .def_property_readonly("plan", [](const BoundReduce& b) { return plan_dict(b.plan()); });
 
   m.def(
       "reduce",

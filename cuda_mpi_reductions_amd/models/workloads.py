@@ -77,6 +77,13 @@ CONFIGS: dict[str, WorkloadConfig] = {
 NORTH_STAR = "xgmi_1b_double_sum"
 
 
+def _current_stream_handle(device: torch.device) -> int:
+    try:
+        return torch._C._cuda_getCurrentRawStream(device.index)
+    except AttributeError:  # older torch
+        return int(torch.cuda.current_stream(device).cuda_stream)
+
+
 class ScalarReduction:
     """Global reduction of a sharded array to one value on every rank."""
 
@@ -100,6 +107,7 @@ class ScalarReduction:
         self.n_streams = max(1, int(streams))
         self.lanes: list = []
         self._next = 0
+        self.bound = None  # _C.BoundReduce of lane 0 (prepared launch), set by setup()
 
     # ------------------------------------------------------------------ setup
     def _size_for_hbm(self) -> int:
@@ -130,6 +138,8 @@ class ScalarReduction:
             self.lanes = [(torch.cuda.current_stream(dev), self.reducer)]
             for _ in range(self.n_streams - 1):
                 self.lanes.append((torch.cuda.Stream(dev), Reducer(dev, config=self.kernel)))
+            self._bound_out = self.new_slots(1)  # default target; steps pass their own slot
+            self.bound = self.reducer.bind(self.x, self.cfg.op, self.acc, out=self._bound_out)
             torch.cuda.synchronize(dev)
         return self
 
@@ -158,7 +168,10 @@ class ScalarReduction:
                 if self.ctx.world_size == 1:
                     return None
                 return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op)
-        self.local(out)
+        if self.bound is not None:  # prepared launch on the *current* stream (graph-capturable)
+            self.bound.launch(_current_stream_handle(self.ctx.device), out.data_ptr())
+        else:
+            self.local(out)
         if self.ctx.world_size == 1:
             return None
         return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op)

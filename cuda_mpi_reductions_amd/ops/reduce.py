@@ -148,6 +148,28 @@ class Reducer:
         )
         return out
 
+    def bind(self, x: torch.Tensor, op: str = "sum", acc_dtype: Optional[torch.dtype] = None,
+             out: Optional[torch.Tensor] = None, config: Optional[KernelConfig] = None):
+        """Resolve plan, kernel variant and arguments once (``_C.BoundReduce``).
+
+        ``bound.launch(stream_handle[, out_ptr])`` is then a single kernel launch with no planning
+        or argument marshalling — the per-step path of bench loops and hipGraph capture. ``x``,
+        ``out`` and this Reducer must outlive the returned object.
+        """
+        C = native()
+        if x.device != self.device or not x.is_contiguous():
+            raise ValueError("bind needs a contiguous tensor on the reducer's device")
+        acc = acc_dtype or default_acc_dtype(x.dtype, op)
+        if out is None:
+            out = torch.empty(1, dtype=acc, device=self.device)
+        elif out.dtype != acc or out.device != self.device or out.numel() < 1:
+            raise ValueError("out must be a 1+ element tensor of the accumulator dtype on the same device")
+        cfg = config or self.config
+        b = C.BoundReduce(self.ws, x.data_ptr(), x.numel(), dtype_code(x.dtype), op_code(op), dtype_code(acc),
+                          out.data_ptr(), **cfg.kwargs())
+        self.last_plan = b.plan
+        return b
+
 
 _reducers: dict = {}
 _lock = threading.Lock()

@@ -1,0 +1,90 @@
+"""hipGraph replay of independent benchmark steps.
+
+A bench step at N GPUs is a 0.14 ms local reduce plus a 1-element RCCL all-reduce. Issued
+eagerly from Python, the all-reduce's stream/event bookkeeping costs ~22 us of GPU-side gaps per
+step even on one rank (profiles/r1_bench/host_overhead.jsonl: 0.165 vs 0.141 ms/step at a 1 GB
+shard); replaying a captured graph of the same steps brings it back to 0.1417 ms. The reference
+had no equivalent (one blocking MPI_Reduce per measurement, mpi/reduce.c:76,90); this is the
+"HIP graphs instead of a tracing compiler" part of the MI355X design.
+
+:class:`StepGraph` captures ``chunk`` consecutive steps (each enqueued by ``step_fn(j)``, which may
+return a ``torch.distributed`` work handle) into one graph — the all-reduce of step j overlaps
+the local reduce of step j+1 inside the graph — plus a remainder graph, so ``run()`` executes
+exactly ``n_steps`` steps. All ranks must capture (``capture`` is collective when a process group
+is given): capture success is agreed with an all-reduce so either every rank replays graphs or
+every rank falls back to eager issue.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+
+__all__ = ["StepGraph", "pick_chunk"]
+
+
+def pick_chunk(n_steps: int, max_chunk: int = 32) -> int:
+    return max(1, min(int(n_steps), int(max_chunk)))
+
+
+class StepGraph:
+    def __init__(self, step_fn: Callable[[int], object], n_steps: int, device: torch.device,
+                 chunk: Optional[int] = None):
+        self.step_fn = step_fn
+        self.n_steps = int(n_steps)
+        self.device = device
+        self.chunk = pick_chunk(self.n_steps) if chunk is None else max(1, min(int(chunk), self.n_steps))
+        self.reps, self.rem = divmod(self.n_steps, self.chunk)
+        self.graphs: list = []
+        self.error: Optional[str] = None
+
+    def _capture_one(self, count: int) -> "torch.cuda.CUDAGraph":
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            works = [self.step_fn(j) for j in range(count)]
+            for w in works:
+                if w is not None:
+                    w.wait()
+        return g
+
+    def capture(self, group_agree: bool = False) -> bool:
+        """Capture the chunk graph (and the remainder graph). Returns True if graphs will be used."""
+        ok = True
+        prev = torch.cuda.current_stream(self.device)
+        try:
+            torch.cuda.synchronize(self.device)
+            self.graphs = [self._capture_one(self.chunk)]
+            if self.rem:
+                self.graphs.append(self._capture_one(self.rem))
+            torch.cuda.synchronize(self.device)
+        except Exception as e:  # fall back to eager issue, recorded in the bench JSON
+            ok = False
+            self.error = f"{type(e).__name__}: {e}"[:300]
+            self.graphs = []
+            # A capture aborted by an exception leaves torch's capture stream (invalidated) as the
+            # current stream — torch.cuda.graph's __exit__ raises before restoring it — so every
+            # later launch would fail; restore the caller's stream and clear the thread's HIP error.
+            torch.cuda.set_stream(prev)
+            from .._native import native
+            native().hip_get_last_error()
+            torch.cuda.synchronize(self.device)
+        if group_agree:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device)
+            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
+            if not bool(flag.item()):
+                ok = False
+                self.error = self.error or "capture failed on another rank"
+                self.graphs = []
+        return ok
+
+    @property
+    def captured(self) -> bool:
+        return bool(self.graphs)
+
+    def run(self) -> None:
+        """Enqueue exactly n_steps steps (graph replays)."""
+        g = self.graphs[0]
+        for _ in range(self.reps):
+            g.replay()
+        if self.rem:
+            self.graphs[1].replay()

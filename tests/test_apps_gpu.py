@@ -2,6 +2,7 @@
 import json
 import os
 import re
+import sys
 
 import pytest
 
@@ -122,6 +123,19 @@ def test_bench_rehearsal_two_ranks_one_gpu(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["verified"] is True and d["n_gpus"] == 2 and d["config"]["backend"] == "gloo"
+
+
+@pytest.mark.parametrize("launch", ["graph", "eager"])
+def test_bench_launch_modes(tmp_path, launch):
+    # Default launch on a GPU is graph replay of the timed steps; both modes verify every slot.
+    r = run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "37", "--warmup", "3", "--elements",
+             "50000017", "--launch", launch, "--graph-chunk", "16"], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["verified"] is True and d["steps"] == 37
+    assert d["config"]["launch"].startswith(launch)
+    if launch == "graph":
+        assert d["config"]["launch"] == "graph (chunk 16, 2 replays + 1 of 5)"
 
 
 @pytest.mark.parametrize("collective", ["allreduce", "host"])

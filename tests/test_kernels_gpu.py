@@ -234,3 +234,73 @@ def test_ladder_kernel6_non_pow2_no_oob():
     x = base[:n]
     assert ladder_reduce(x, "max", kernel=6).item() == x.max().item()
     assert reduce(x, "max").item() == x.max().item()
+
+
+@pytest.mark.parametrize("dt,op,acc", COMBOS, ids=lambda v: str(v).replace("torch.", ""))
+@pytest.mark.parametrize("single_pass", [True, False])
+def test_bound_reduce_matches_reference(dt, op, acc, single_pass):
+    # The prepared launch (_C.BoundReduce) resolves the plan once; launch() may redirect the output.
+    n = 3_000_017
+    x = torch.empty(n + 1, dtype=dt, device=DEV)[1:]  # misaligned view
+    fill_(x, "fullrange" if not dt.is_floating_point else "uniform", seed=41)
+    r = Reducer(DEV, config=KernelConfig(single_pass=single_pass))
+    out = torch.empty(4, dtype=acc, device=DEV)
+    b = r.bind(x, op, acc, out=out[0:1])
+    assert b.plan["single_pass"] == single_pass and r.last_plan == b.plan
+    stream = torch.cuda.current_stream().cuda_stream
+    b.launch(stream)
+    for i in (1, 2, 3):
+        b.launch(stream, out[i:i + 1].data_ptr())
+    torch.cuda.synchronize()
+    for i in range(4):
+        check(out[i].item(), x, op, acc, n)
+
+
+def test_bound_reduce_graph_capture_and_replay():
+    # Captured launches replay with the self-resetting tickets: no memset node needed.
+    n = 5_000_001
+    x = torch.empty(n, dtype=torch.float64, device=DEV)
+    fill_(x, "uniform", seed=9)
+    r = Reducer(DEV)
+    slots = torch.zeros(6, dtype=torch.float64, device=DEV)
+    b = r.bind(x, "sum", out=slots[0:1])
+    b.launch(torch.cuda.current_stream().cuda_stream)  # warm-up outside capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(6):
+            b.launch(torch.cuda.current_stream().cuda_stream, slots[i:i + 1].data_ptr())
+    slots.zero_()
+    for _ in range(25):
+        g.replay()
+    torch.cuda.synchronize()
+    for i in range(6):
+        check(slots[i].item(), x, "sum", torch.float64, n)
+
+
+@pytest.mark.parametrize("n_steps,chunk", [(7, 3), (32, 32), (5, 8), (1, 32)])
+def test_step_graph_runs_exactly_n_steps(n_steps, chunk):
+    from cuda_mpi_reductions_amd.utils.graphs import StepGraph
+    counter = torch.zeros(1, dtype=torch.int64, device=DEV)
+
+    def step(j):
+        counter.add_(1)
+    sg = StepGraph(step, n_steps, torch.device(DEV), chunk=chunk)
+    assert sg.capture(), sg.error
+    assert sg.captured
+    counter.zero_()
+    sg.run()
+    torch.cuda.synchronize()
+    assert counter.item() == n_steps
+    assert sg.reps * sg.chunk + sg.rem == n_steps
+
+
+def test_step_graph_failed_capture_falls_back():
+    from cuda_mpi_reductions_amd.utils.graphs import StepGraph
+
+    def bad_step(j):
+        torch.cuda.synchronize()  # not allowed while capturing
+    sg = StepGraph(bad_step, 4, torch.device(DEV), chunk=2)
+    assert not sg.capture() and not sg.captured and sg.error
+    # the device is still usable afterwards
+    assert torch.ones(3, device=DEV).sum().item() == 3.0

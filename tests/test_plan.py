@@ -86,8 +86,13 @@ def test_ladder_geometry_matches_reference_planner(kernel, n):
 
 def test_compiled_variants_cover_grid():
     v = native().compiled_variants()
-    assert len(v) == 3 * 4 * 2
+    plain = [s for s in v if not s.endswith("pipelined")]
+    piped = [s for s in v if s.endswith("pipelined")]
+    assert len(plain) == 3 * 4 * 2  # block x unroll x policy
+    # software-pipelined bodies exist where BLOCK * UNROLL <= 8192 (two register sets)
+    assert len(piped) == 2 * sum(1 for b in (256, 512, 1024) for u in (2, 4, 8, 16) if b * u <= 8192)
     assert "block=512 unroll=16 policy=nt" in v
+    assert "block=1024 unroll=16 policy=nt pipelined" not in v
 
 
 def test_single_hip_runtime_in_process():

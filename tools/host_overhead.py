@@ -12,6 +12,7 @@ size, the host time to enqueue K steps (GPU kept busy) and the GPU time per step
   bound+ar       prepared launch + all_reduce
   graph          torch.cuda.CUDAGraph of CHUNK eager steps, replayed K/CHUNK times
   graph+ar       same with the all-reduce captured too
+  graph2         two lanes (own workspaces) alternating on two forked streams inside the graph
 
 Usage (GPU box): python tools/host_overhead.py [--sizes 1048576,125000000] [--steps 400]
 Prints one JSON line per (variant, size).
@@ -38,7 +39,7 @@ def main() -> int:
     ap.add_argument("--sizes", default="1048576,125000000")
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--chunk", type=int, default=8)
-    ap.add_argument("--variants", default="eager,eager+ar,bound,bound+ar,graph,graph+ar")
+    ap.add_argument("--variants", default="eager,eager+ar,bound,bound+ar,graph,graph+ar,graph2")
     a = ap.parse_args()
     ctx = pdist.init()
     dev = ctx.device
@@ -51,6 +52,8 @@ def main() -> int:
         slots = torch.zeros(a.chunk, dtype=torch.float64, device=dev)
         bound = [C.BoundReduce(r.ws, x.data_ptr(), n, 3, 0, 3, slots[i:i + 1].data_ptr())
                  for i in range(a.chunk)] if hasattr(C, "BoundReduce") else None
+        r2 = Reducer(dev)  # second workspace for the two-lane graph
+        lane2 = C.BoundReduce(r2.ws, x.data_ptr(), n, 3, 0, 3, slots[0:1].data_ptr())
         ref = x.sum().item()
 
         def eager(i, ar):
@@ -61,13 +64,32 @@ def main() -> int:
             bound[i % a.chunk].launch(torch.cuda.current_stream(dev).cuda_stream)
             return pdist.scalar_allreduce(slots[i % a.chunk:i % a.chunk + 1], "sum", async_op=True) if ar else None
 
+        def graph2_capture():
+            # two lanes (own workspace each) on two forked streams, alternating steps: kernel j+1
+            # may start while kernel j drains / finalises
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(dev)
+            with torch.cuda.graph(g):
+                main = torch.cuda.current_stream(dev)
+                side.wait_stream(main)
+                for i in range(a.chunk):
+                    if i % 2 == 0:
+                        bound[0].launch(main.cuda_stream, slots[i:i + 1].data_ptr())
+                    else:
+                        lane2.launch(side.cuda_stream, slots[i:i + 1].data_ptr())
+                main.wait_stream(side)
+            return g
+
         for v in a.variants.split(","):
             ar = v.endswith("+ar")
             base = v.split("+")[0]
             if base == "bound" and bound is None:
                 continue
             try:
-                if base == "graph":
+                if base == "graph2":
+                    g = graph2_capture()
+                    fn = lambda: [g.replay() for _ in range(K // a.chunk)]  # noqa: E731
+                elif base == "graph":
                     g = torch.cuda.CUDAGraph()
                     s = torch.cuda.Stream(dev)
                     s.wait_stream(torch.cuda.current_stream(dev))

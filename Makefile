@@ -86,7 +86,7 @@ $(BUILD)/bin/%: csrc/apps/%.cpp $(LIB) $(COMMLIB) $(HEADERS)
 	    -L$(ROCM)/lib -lrccl $(LDLIBS) -o $@
 
 # reduce.c parity app: plain C++ against MPICH (CPU buffers only; no HIP needed).
-MPI_SRCS := csrc/apps/reduce_mpi.cpp csrc/runtime/mt19937.cpp csrc/runtime/cli.cpp csrc/runtime/report.cpp csrc/runtime/timer.cpp csrc/runtime/types.cpp
+MPI_SRCS := csrc/apps/reduce_mpi.cpp csrc/runtime/fault.cpp csrc/runtime/mt19937.cpp csrc/runtime/cli.cpp csrc/runtime/report.cpp csrc/runtime/timer.cpp csrc/runtime/types.cpp
 $(MPI_APP): $(MPI_SRCS) $(HEADERS)
 	@mkdir -p $(dir $@)
 	g++ $(CXXSTD) -O3 -Wall -Icsrc/include -DMIREDUCE_NO_HIP -I$(MPI_HOME)/include \

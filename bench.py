@@ -34,6 +34,7 @@ from cuda_mpi_reductions_amd._native import native, native_path
 from cuda_mpi_reductions_amd.models import CONFIGS, NORTH_STAR, ScalarReduction
 from cuda_mpi_reductions_amd.ops import KernelConfig
 from cuda_mpi_reductions_amd.parallel import dist as pdist
+from cuda_mpi_reductions_amd.utils.fault import FaultInjector
 from cuda_mpi_reductions_amd.utils.graphs import StepGraph
 
 METRIC = "reduction bandwidth (GB/s, whole node), 1B-double sum at 1/2/4/8 MI355X"
@@ -59,6 +60,10 @@ def parse_args(argv=None):
                    help="graph: replay the timed steps as captured hipGraphs (chunks of --graph-chunk steps); "
                         "eager: issue every step from Python; auto: graph on GPUs when capturable")
     p.add_argument("--graph-chunk", type=int, default=32, help="steps per captured graph")
+    p.add_argument("--inject-fault", default=None,
+                   help="failure-detection test: KIND[@RANK][:STEP], KIND = exit|hang|corrupt|delay=<ms> "
+                        "(steps count warm-up first; forces --launch eager)")
+    p.add_argument("--pg-timeout", type=float, default=600.0, help="process-group collective timeout (s)")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--trace", action="store_true", help="roctx range per step (rocprofv3 --marker-trace)")
     p.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
@@ -74,7 +79,7 @@ def _sync(dev: torch.device) -> None:
         torch.cuda.synchronize(dev)
 
 
-def run_vector(args, ctx, cfg) -> int:
+def run_vector(args, ctx, cfg, fault) -> int:
     """reduce.c semantics (BASELINE config 1): element-wise reduce of an N/P vector per rank to
     root 0. Each collective is timed on its own between a barrier and a synchronisation (the
     in-place buffer is restored outside the clock, like reduce.c's bzero, mpi/reduce.c:74-77);
@@ -82,19 +87,31 @@ def run_vector(args, ctx, cfg) -> int:
     from cuda_mpi_reductions_amd.models import VectorReduction
     wl = VectorReduction(cfg, ctx).setup(mt19937=(ctx.device.type == "cpu"))
     dev = ctx.device
-    for _ in range(args.warmup):
-        wl.step()
-    times = []
-    for _ in range(args.steps):
+    for i in range(args.warmup):
         wl.restore()
+        if fault.enabled and fault.at(ctx.rank, i, "bench step"):
+            wl.y.view(-1)[0] += 1
+        wl.collective()
+    times, checks = [], []
+    holder = cfg.collective == "allreduce" or ctx.rank == 0
+    for i in range(args.warmup, args.warmup + args.steps):
+        wl.restore()
+        if fault.enabled and fault.at(ctx.rank, i, "bench step"):
+            wl.y.view(-1)[0] += 1  # this rank contributes a wrong element: verification must fail
         _sync(dev)
         pdist.barrier(ctx)
         t0 = time.perf_counter()
         wl.collective()
         _sync(dev)
         times.append(pdist.max_over_ranks(time.perf_counter() - t0, ctx))
+        if not args.no_verify and holder:  # per-step checksum (untimed): every step must agree
+            checks.append(wl.y.to(torch.float64).sum().reshape(1))
     elapsed = sum(times)
-    verified = None if args.no_verify else wl.verify()["ok"]
+    verified = None
+    if not args.no_verify:
+        same = bool((torch.cat(checks) == checks[-1]).all().item()) if checks else True
+        same = -pdist.max_over_ranks(-float(same), ctx) > 0.5  # AND over ranks
+        verified = wl.verify()["ok"] and same
     gib = wl.bytes_total * args.steps / elapsed / float(1 << 30)
     if ctx.is_root:
         print(json.dumps({
@@ -120,7 +137,9 @@ def main(argv=None) -> int:
         device_type = args.device
     else:  # CPU-rank configs (reduce.c plumbing) run on CPU ranks even on a GPU box
         device_type = "cpu" if CONFIGS[args.config].device == "cpu" else None
-    ctx = pdist.init(backend=None if args.backend == "auto" else args.backend, device_type=device_type)
+    fault = FaultInjector.from_flag_or_env(args.inject_fault)
+    ctx = pdist.init(backend=None if args.backend == "auto" else args.backend, device_type=device_type,
+                     timeout_s=args.pg_timeout)
     if args.gpus != ctx.world_size and ctx.is_root:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}; using {ctx.world_size}",
               file=sys.stderr)
@@ -129,7 +148,7 @@ def main(argv=None) -> int:
         from dataclasses import replace
         cfg = replace(cfg, n_total=args.elements)
     if cfg.mode == "vector":
-        rc = run_vector(args, ctx, cfg)
+        rc = run_vector(args, ctx, cfg, fault)
         pdist.shutdown(ctx)
         return rc
     kernel = KernelConfig(block=args.block, unroll=args.unroll, wg_per_cu=args.wg_per_cu,
@@ -145,7 +164,8 @@ def main(argv=None) -> int:
         works = []
         for i in range(first, first + count):
             C.trace_push("bench.step")
-            w = wl.step(slots[i:i + 1], async_op=True)
+            corrupt = fault.at(ctx.rank, i, "bench step") if fault.enabled else False
+            w = wl.step(slots[i:i + 1], async_op=True, corrupt=corrupt)
             C.trace_pop()
             if w is not None:
                 if args.serial:
@@ -159,8 +179,9 @@ def main(argv=None) -> int:
     launch = "eager"
     sg = None
     capturable = dev.type == "cuda" and len(wl.lanes) == 1 and not args.serial and not args.trace and \
+        not fault.enabled and \
         (ctx.world_size == 1 or ctx.backend == "nccl")
-    if args.launch == "graph" or (args.launch == "auto" and capturable):
+    if (args.launch == "graph" and not fault.enabled) or (args.launch == "auto" and capturable):
         # Capture the K timed steps as graph replays of --graph-chunk-step chunks (all ranks agree
         # on success or all fall back to eager issue); one untimed replay uploads the graphs.
         sg = StepGraph(lambda j: wl.step(slots[W + j:W + j + 1], async_op=True), K, dev, chunk=args.graph_chunk)
@@ -189,7 +210,8 @@ def main(argv=None) -> int:
     verified = None
     if not args.no_verify:
         # every timed slot must hold the same global value (all steps reduce the same data)
-        written = slots[W:W + sg.chunk] if sg is not None else slots[W:]
+        # (warm-up slots too: a wrong warm-up result is a failure as well)
+        written = slots[:W + sg.chunk] if sg is not None else slots
         ref = wl.verify(written[-1:])
         ok = ref["ok"]
         if written.numel() > 1:

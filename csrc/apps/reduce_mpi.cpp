@@ -21,6 +21,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
+#include <stdexcept>
 #include <set>
 #include <string>
 #include <type_traits>
@@ -28,6 +30,7 @@
 #include <cmath>
 
 #include "mireduce/cli.hpp"
+#include "mireduce/fault.hpp"
 #include "mireduce/mt19937.hpp"
 #include "mireduce/report.hpp"
 #include "mireduce/timer.hpp"
@@ -133,6 +136,31 @@ bool verify(DType t, Op o, const void* send, const void* recv, uint64_t count, i
   return false;
 }
 
+template <class T>
+void corrupt_first_t(Op o, T* p) {
+  if (o == Op::Sum) p[0] = static_cast<T>(p[0] + T(1));
+  else p[0] = o == Op::Min ? std::numeric_limits<T>::lowest() : std::numeric_limits<T>::max();
+}
+
+void corrupt_first(DType t, Op o, void* p) {
+  switch (t) {
+    case DType::Int32: {  // wrap like MPI_INT instead of signed overflow
+      auto* q = static_cast<int32_t*>(p);
+      if (o == Op::Sum) q[0] = static_cast<int32_t>(static_cast<uint32_t>(q[0]) + 1u);
+      else corrupt_first_t(o, q);
+      break;
+    }
+    case DType::Int64: {
+      auto* q = static_cast<int64_t*>(p);
+      if (o == Op::Sum) q[0] = static_cast<int64_t>(static_cast<uint64_t>(q[0]) + 1u);
+      else corrupt_first_t(o, q);
+      break;
+    }
+    case DType::Float32: corrupt_first_t(o, static_cast<float*>(p)); break;
+    case DType::Float64: corrupt_first_t(o, static_cast<double*>(p)); break;
+  }
+}
+
 void usage() {
   std::printf(
       "reduce_mpi — element-wise MPI_Reduce benchmark (reduce.c semantics)\n"
@@ -144,7 +172,8 @@ void usage() {
       "  --retries=5  --warmup=1  --root=0  --collective=reduce|allreduce\n"
       "  --timing=max|root      max over ranks after a barrier (default) or reduce.c's root clock\n"
       "  --verify               check the reduced vector at sampled indices\n"
-      "  --json=PATH            append one JSON record per measurement\n");
+      "  --json=PATH            append one JSON record per measurement\n"
+      "  --inject-fault=KIND[@RANK][:STEP]  exit|hang|corrupt|delay=<ms> before timed collective STEP\n");
 }
 
 }  // namespace
@@ -169,7 +198,7 @@ int main(int argc, char** argv) {
     return EXIT_SUCCESS;
   }
   const std::set<std::string> known = {"ints", "doubles", "longs", "floats", "dtypes", "ops", "retries", "warmup",
-                                       "root", "collective", "timing", "verify", "json", "help"};
+                                       "root", "collective", "timing", "verify", "json", "help", "inject-fault"};
   for (const auto& u : args.unknown(known))
     if (rank == 0) std::fprintf(stderr, "warning: unknown flag --%s ignored\n", u.c_str());
 
@@ -210,6 +239,13 @@ int main(int argc, char** argv) {
     if (collective != "reduce" && collective != "allreduce") throw CliError("--collective must be reduce|allreduce");
     if (timing != "max" && timing != "root") throw CliError("--timing must be max|root");
     if (root < 0 || root >= size) throw CliError("--root out of range");
+    FaultInjector fault;
+    try {
+      fault = FaultInjector::from_flag_or_env(args.str_or("inject-fault", ""));
+    } catch (const std::invalid_argument& e) {
+      throw CliError(e.what());
+    }
+    long fault_step = 0;
 
     // per-dtype global counts
     auto global_count = [&](DType t) -> uint64_t {
@@ -267,7 +303,15 @@ int main(int argc, char** argv) {
     for (int x = 0; x < retries; ++x) {
       for (auto& b : bufs) {
         for (Op o : ops) {
+          // fault injection: a wrong contribution at element 0 (a sampled index) for this collective
+          unsigned char saved[8];
+          const bool corrupt = fault.at(rank, fault_step++, "MPI collective") && b.count;
+          if (corrupt) {
+            std::memcpy(saved, b.send.data(), dtype_size(b.t));
+            corrupt_first(b.t, o, b.send.data());
+          }
           const double dt = run_one(b, o);
+          if (corrupt) std::memcpy(b.send.data(), saved, dtype_size(b.t));
           const double bytes = static_cast<double>(b.total) * dtype_size(b.t);
           const double gib = bytes / dt / kGiB;
           if (rank == root) {

@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <memory>
 #include <set>
 #include <string>
@@ -34,6 +35,7 @@
 #include "mireduce/cpu_reference.hpp"
 #include "mireduce/device.hpp"
 #include "mireduce/direct.hpp"
+#include "mireduce/fault.hpp"
 #include "mireduce/mt19937.hpp"
 #include "mireduce/reduce.hpp"
 #include "mireduce/report.hpp"
@@ -50,7 +52,7 @@ constexpr uint64_t kNumDoubles = 256ull * 1024 * 1024;  // mpi/constants.h:2
 const std::set<std::string> kKnown = {"mode", "collective", "dtypes", "ops", "ints", "doubles", "longs", "floats",
                                       "n", "retries", "warmup", "iters", "root", "json", "graph", "mt19937",
                                       "noverify", "seed", "help", "unroll", "block", "wg-per-cu", "policy",
-                                      "units", "timeout", "trace", "single-process"};
+                                      "units", "timeout", "trace", "single-process", "inject-fault"};
 
 struct Ctx {
   LaunchEnv env;
@@ -66,7 +68,44 @@ struct Ctx {
   double timeout_s = 300;
   bool units_gb = false;  // gnuplot column in 2^30 (reduce.c) unless --units=gb
   ReduceConfig kcfg;
+  FaultInjector fault;  // --inject-fault / MIREDUCE_INJECT_FAULT (failure-detection tests)
+  long fault_step = 0;  // counts timed collectives / steps on this rank
 };
+
+// Fault injection "corrupt": make this rank's contribution at element `i` wrong for one timed
+// batch (SUM: +1, MIN: lowest, MAX: highest); returns the original bytes for restore.
+template <class T>
+T corrupt_element(void* d, uint64_t i, Op o) {
+  T v;
+  HIP_CHECK(hipMemcpy(&v, static_cast<T*>(d) + i, sizeof(T), hipMemcpyDeviceToHost));
+  const T bad = o == Op::Sum ? wrap_add(v, T(1))
+                             : (o == Op::Min ? std::numeric_limits<T>::lowest() : std::numeric_limits<T>::max());
+  HIP_CHECK(hipMemcpy(static_cast<T*>(d) + i, &bad, sizeof(T), hipMemcpyHostToDevice));
+  return v;
+}
+
+struct SavedElement {
+  void* ptr = nullptr;
+  unsigned char bytes[8] = {0};
+  size_t size = 0;
+};
+
+SavedElement corrupt_any(void* d, uint64_t i, DType t, Op o) {
+  SavedElement s;
+  s.size = dtype_size(t);
+  s.ptr = static_cast<unsigned char*>(d) + i * s.size;
+  switch (t) {
+    case DType::Int32: { const int32_t v = corrupt_element<int32_t>(d, i, o); std::memcpy(s.bytes, &v, 4); break; }
+    case DType::Int64: { const int64_t v = corrupt_element<int64_t>(d, i, o); std::memcpy(s.bytes, &v, 8); break; }
+    case DType::Float32: { const float v = corrupt_element<float>(d, i, o); std::memcpy(s.bytes, &v, 4); break; }
+    case DType::Float64: { const double v = corrupt_element<double>(d, i, o); std::memcpy(s.bytes, &v, 8); break; }
+  }
+  return s;
+}
+
+void restore_element(const SavedElement& s) {
+  if (s.ptr) HIP_CHECK(hipMemcpy(s.ptr, s.bytes, s.size, hipMemcpyHostToDevice));
+}
 
 uint64_t global_count(DType t, uint64_t ints, uint64_t longs, uint64_t floats, uint64_t doubles) {
   switch (t) {
@@ -237,7 +276,11 @@ bool run_vector(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>&
       stage(b);
       for (Op o : ops) {
         HIP_CHECK(hipMemsetAsync(const_cast<void*>(out_ptr(c, b)), 0, b.count * dtype_size(b.t), c.stream));  // bzero (reduce.c:74)
+        SavedElement saved;
+        if (c.fault.at(c.env.rank, c.fault_step++, "vector collective") && b.count)
+          saved = corrupt_any(const_cast<void*>(in_ptr(c, b)), 7 % b.count, b.t, o);  // a sampled index
         const double dt = time_iters(c, body_for(b, o));
+        restore_element(saved);  // the check compares against the clean inputs
         const double bytes = static_cast<double>(b.count) * c.env.world * dtype_size(b.t);
         const double algbw = static_cast<double>(b.count) * dtype_size(b.t) / dt / kGB;
         const bool all = c.collective == "allreduce" || c.collective == "direct";
@@ -294,7 +337,10 @@ bool run_scalar(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>&
         c.comm->synchronize(c.stream, c.timeout_s);
       }
       for (int x_ = 0; x_ < c.retries; ++x_) {
+        SavedElement saved;
+        if (c.fault.at(c.env.rank, c.fault_step++, "scalar step") && count) saved = corrupt_any(x.get(), 0, t, o);
         const double dt = time_iters(c, body);
+        restore_element(saved);
         Json j;
         j.set("n_total", n).set("count_per_rank", count).set("retry", x_);
         bool vok = true;
@@ -489,6 +535,8 @@ void usage() {
       "  --mt19937                    vector mode: reduce.c's exact per-rank MT19937 data (host-generated)\n"
       "  --units=gib|gb               GNUPlot column unit (default gib = reduce.c's 2^30)\n"
       "  --json=PATH  --noverify  --seed=N  --block= --unroll= --wg-per-cu= --policy=auto|nt|default\n"
+      "  --timeout=S                  RCCL wait deadline (s); bootstrap: MIREDUCE_BOOTSTRAP_TIMEOUT\n"
+      "  --inject-fault=KIND[@RANK][:STEP]  exit|hang|corrupt|delay=<ms> at a timed collective (tests)\n"
       "launch: torchrun --nproc-per-node=8 --master-addr 127.0.0.1 ... | mpirun -np 8 ...\n");
 }
 
@@ -569,6 +617,11 @@ int main(int argc, char** argv) {
     c.units_gb = args.str_or("units", "gib") == "gb";
     double to = 0;
     if (args.get_double("timeout", &to)) c.timeout_s = to;
+    try {
+      c.fault = FaultInjector::from_flag_or_env(args.str_or("inject-fault", ""));
+    } catch (const std::invalid_argument& e) {
+      throw CliError(e.what());
+    }
     c.kcfg.block = args.int_or<int>("block", 0);
     c.kcfg.unroll = args.int_or<int>("unroll", 0);
     c.kcfg.wg_per_cu = args.int_or<int>("wg-per-cu", 0);

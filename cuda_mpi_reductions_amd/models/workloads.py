@@ -151,15 +151,28 @@ class ScalarReduction:
     def new_slots(self, k: int) -> torch.Tensor:
         return torch.empty(k, dtype=self.acc, device=self.ctx.device)
 
+    def _local_into(self, out: torch.Tensor) -> None:
+        if self.bound is not None:
+            self.bound.launch(_current_stream_handle(self.ctx.device), out.data_ptr())
+        else:
+            self.local(out)
+
     def local(self, out: torch.Tensor) -> torch.Tensor:
         if self.reducer is not None:
             return self.reducer(self.x, self.cfg.op, self.acc, out=out)
         from ..ops import reduce as host_reduce
         return host_reduce(self.x, self.cfg.op, self.acc, out=out)
 
-    def step(self, out: torch.Tensor, async_op: bool = True):
+    def step(self, out: torch.Tensor, async_op: bool = True, corrupt: bool = False):
         """Local reduce into ``out`` (1 element) then all-reduce it across ranks. Returns the
-        collective's work handle (``None`` for a single rank)."""
+        collective's work handle (``None`` for a single rank). ``corrupt`` (fault injection)
+        perturbs the local result before the collective; verification must catch it."""
+        if corrupt:
+            self._local_into(out)
+            out.sub_(1) if self.cfg.op == "min" else out.add_(1)
+            if self.ctx.world_size == 1:
+                return None
+            return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op)
         if len(self.lanes) > 1:
             stream, reducer = self.lanes[self._next % len(self.lanes)]
             self._next += 1
@@ -168,10 +181,7 @@ class ScalarReduction:
                 if self.ctx.world_size == 1:
                     return None
                 return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op)
-        if self.bound is not None:  # prepared launch on the *current* stream (graph-capturable)
-            self.bound.launch(_current_stream_handle(self.ctx.device), out.data_ptr())
-        else:
-            self.local(out)
+        self._local_into(out)  # prepared launch on the *current* stream (graph-capturable)
         if self.ctx.world_size == 1:
             return None
         return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op)

@@ -3,10 +3,12 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "mireduce/cli.hpp"
+#include "mireduce/fault.hpp"
 #include "mireduce/mt19937.hpp"
 #include "mireduce/report.hpp"
 #include "mireduce/timer.hpp"
@@ -106,8 +108,37 @@ static void test_report() {
   CHECK(w.sessions() == 2 && w.laps_ms().size() == 2 && w.average_ms() >= 0);
 }
 
+static void test_fault_spec() {
+  FaultSpec f = parse_fault_spec("");
+  CHECK(f.kind == FaultSpec::Kind::None);
+  f = parse_fault_spec("exit");
+  CHECK(f.kind == FaultSpec::Kind::Exit && f.rank == 1 && f.step == 0);
+  f = parse_fault_spec("hang@3:17");
+  CHECK(f.kind == FaultSpec::Kind::Hang && f.rank == 3 && f.step == 17);
+  f = parse_fault_spec("delay=250@0:2");
+  CHECK(f.kind == FaultSpec::Kind::Delay && f.delay_ms == 250 && f.rank == 0 && f.step == 2);
+  f = parse_fault_spec("corrupt:5");
+  CHECK(f.kind == FaultSpec::Kind::Corrupt && f.rank == 1 && f.step == 5);
+  for (const char* bad : {"boom", "exit@", "exit@x", "hang:-1", "delay=", "corrupt@1:2x"}) {
+    bool threw = false;
+    try {
+      parse_fault_spec(bad);
+    } catch (const std::invalid_argument&) {
+      threw = true;
+    }
+    CHECK(threw);
+  }
+  FaultInjector inj(parse_fault_spec("corrupt@2:4"));
+  CHECK(!inj.at(1, 4, "unit") && !inj.at(2, 3, "unit"));
+  CHECK(inj.at(2, 4, "unit"));
+  CHECK(!inj.at(2, 4, "unit"));  // fires once
+  FaultInjector d(parse_fault_spec("delay=1@0:0"));
+  CHECK(!d.at(0, 0, "unit"));
+}
+
 int main() {
   test_cli();
+  test_fault_spec();
   test_types();
   test_mt();
   test_report();

@@ -147,3 +147,38 @@ def test_reduce_xgmi_single_process(collective):
     assert "verification PASSED" in r.stderr
     rows = [ln for ln in r.stdout.splitlines() if re.match(r"^(INT|DOUBLE) (MAX|MIN|SUM) \d+ +[0-9.]+$", ln)]
     assert len(rows) == 12 and r.stdout.splitlines()[0] == "# DATATYPE OP NODES GB/sec"
+
+
+# ---------------------------------------------------------------- failure detection
+
+def test_reduce_xgmi_scalar_corrupt_detected():
+    r = run([os.path.join(BIN, "reduce_xgmi"), "--mode=scalar", "--n=10000019", "--dtypes=DOUBLE", "--ops=SUM",
+             "--retries=2", "--iters=3", "--inject-fault=corrupt@0:0"], timeout=300)
+    assert r.returncode != 0
+    assert "[fault] rank 0 corrupts" in r.stderr and "verification FAILED" in r.stderr
+
+
+@pytest.mark.parametrize("collective", ["direct", "direct-reduce"])
+def test_reduce_xgmi_direct_corrupt_detected(collective):
+    r = torchrun(2, ["--no-python", os.path.join(BIN, "reduce_xgmi"), "--mode=vector", f"--collective={collective}",
+                     "--ints=1000003", "--doubles=999999", "--retries=1", "--iters=2", "--inject-fault=corrupt@1:4"],
+                 timeout=300)
+    assert r.returncode != 0
+    assert "verification FAILED" in r.stderr
+
+
+@pytest.mark.parametrize("kind", ["exit", "hang"])
+def test_reduce_xgmi_direct_lost_peer_fails_fast(kind, monkeypatch):
+    # A crashed or hung peer: the survivor's host-barrier phase hits the bootstrap deadline (or a
+    # closed socket) and exits with an error; no kernel ever waits on another GPU, so nothing hangs
+    # on the device; torchrun then tears down the hung rank.
+    import time
+    monkeypatch.setenv("MIREDUCE_BOOTSTRAP_TIMEOUT", "5")
+    t0 = time.time()
+    r = torchrun(2, ["--no-python", os.path.join(BIN, "reduce_xgmi"), "--mode=vector", "--collective=direct",
+                     "--ints=1000003", "--doubles=999999", "--retries=2", "--iters=2",
+                     f"--inject-fault={kind}@1:2"], timeout=240)
+    assert r.returncode != 0
+    assert f"[fault] rank 1 {'exits' if kind == 'exit' else 'hangs'}" in r.stderr
+    assert "[rank 0] error: bootstrap" in r.stderr, r.stderr[-2000:]
+    assert time.time() - t0 < 180

@@ -1,0 +1,104 @@
+"""Failure detection under injected faults, on CPU ranks over gloo.
+
+The reference had none: MPI return codes ignored (mpi/reduce.c:32-106), no result check
+(B11), a stuck rank stalls until the SLURM walltime (mpi/submit_all.sh:4). Here a wrong
+contribution must fail verification, and a crashed or hung rank must end the job with an error
+within the process-group deadline — never a silent pass or an endless hang. The native twin
+(bootstrap deadlines) is covered in tests/test_native_unit.py.
+"""
+import json
+import os
+import time
+
+import pytest
+
+from helpers import ROOT, torchrun
+
+from cuda_mpi_reductions_amd.utils.fault import FaultInjector, FaultSpec, parse_fault_spec
+
+BENCH = os.path.join(ROOT, "bench.py")
+SCALAR = ["--gpus", "2", "--device", "cpu", "--elements", "200003", "--steps", "6", "--warmup", "2"]
+VECTOR = ["--gpus", "2", "--config", "mpi_1m_int32_sum_cpu2", "--steps", "4", "--warmup", "1"]
+
+
+def _json(r):
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return json.loads(lines[0]) if lines else None
+
+
+def test_parse_fault_spec():
+    assert parse_fault_spec(None) == FaultSpec()
+    assert parse_fault_spec("exit") == FaultSpec("exit", 1, 0, 0)
+    assert parse_fault_spec("hang@3:17") == FaultSpec("hang", 3, 17, 0)
+    assert parse_fault_spec("delay=250@0:2") == FaultSpec("delay", 0, 2, 250)
+    assert parse_fault_spec("corrupt:5") == FaultSpec("corrupt", 1, 5, 0)
+    for bad in ("boom", "exit@", "exit@x", "hang:-1", "delay=", "corrupt@1:2x"):
+        with pytest.raises(ValueError):
+            parse_fault_spec(bad)
+    inj = FaultInjector(parse_fault_spec("corrupt@2:4"))
+    assert not inj.at(1, 4) and not inj.at(2, 3) and inj.at(2, 4) and not inj.at(2, 4)
+
+
+@pytest.mark.parametrize("args", [SCALAR, VECTOR], ids=["scalar", "vector"])
+@pytest.mark.parametrize("step", [1, 4])
+def test_corrupt_contribution_fails_verification(tmp_path, args, step):
+    r = torchrun(2, [BENCH, *args, "--inject-fault", f"corrupt@1:{step}"], cwd=tmp_path, timeout=300)
+    assert r.returncode == 1, r.stderr[-2000:]
+    d = _json(r)
+    assert d is not None and d["verified"] is False
+    assert "[fault] rank 1 corrupt" in r.stderr
+
+
+@pytest.mark.parametrize("args", [SCALAR, VECTOR], ids=["scalar", "vector"])
+def test_straggler_delay_still_verifies(tmp_path, args):
+    r = torchrun(2, [BENCH, *args, "--inject-fault", "delay=300@0:3"], cwd=tmp_path, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json(r)
+    assert d["verified"] is True
+
+
+def test_crashed_rank_fails_job_fast(tmp_path):
+    t0 = time.time()
+    r = torchrun(2, [BENCH, *SCALAR, "--inject-fault", "exit@1:3", "--pg-timeout", "20"], cwd=tmp_path, timeout=300)
+    assert r.returncode != 0
+    assert _json(r) is None
+    assert time.time() - t0 < 120
+
+
+def test_hung_rank_hits_deadline(tmp_path):
+    # rank 1 stops making progress inside the timed loop; rank 0's all-reduce times out after
+    # --pg-timeout and the launcher tears the job down.
+    t0 = time.time()
+    r = torchrun(2, [BENCH, *SCALAR, "--inject-fault", "hang@1:4", "--pg-timeout", "8"], cwd=tmp_path, timeout=300)
+    assert r.returncode != 0
+    assert _json(r) is None
+    assert "[fault] rank 1 hang" in r.stderr
+    assert time.time() - t0 < 150
+
+
+# ---------------------------------------------------------------- native apps on CPU ranks (MPICH)
+
+from helpers import BIN, MPIRUN, ensure_built, run  # noqa: E402
+
+needs_mpi = pytest.mark.skipif(not os.path.exists(MPIRUN), reason="MPICH not available")
+
+
+@needs_mpi
+@pytest.mark.parametrize("op", ["SUM", "MIN", "MAX"])
+@pytest.mark.parametrize("dtypes", ["INT", "LONG", "FLOAT", "DOUBLE"])
+def test_reduce_mpi_corrupt_detected(op, dtypes):
+    ensure_built()
+    r = run([MPIRUN, "-np", "3", os.path.join(BIN, "reduce_mpi"), "--ints=30001", "--doubles=30001", f"--dtypes={dtypes}",
+             f"--ops={op}", "--retries=1", "--verify", "--inject-fault=corrupt@2:0"], timeout=120)
+    assert r.returncode != 0
+    assert "[fault] rank 2 corrupts" in r.stderr and "verification FAILED" in r.stderr
+
+
+@needs_mpi
+def test_reduce_mpi_crashed_rank_ends_job():
+    ensure_built()
+    t0 = time.time()
+    r = run([MPIRUN, "-np", "2", os.path.join(BIN, "reduce_mpi"), "--ints=30001", "--doubles=30001", "--retries=3",
+             "--inject-fault=exit@1:2"], timeout=120)
+    assert r.returncode != 0
+    assert time.time() - t0 < 60

@@ -81,3 +81,51 @@ def test_bootstrap_missing_peer_fails_fast(rank):
     assert r.returncode == 2, (r.returncode, r.stderr)
     assert ("timed out" in r.stderr) or ("cannot connect" in r.stderr)
     assert time.time() - t0 < 30
+
+
+def _spawn_bootstrap_ranks(world, fault, timeout_s="3"):
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for rank in range(world):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                   MASTER_ADDR="127.0.0.1", MIREDUCE_BOOTSTRAP_PORT=port, MIREDUCE_BOOTSTRAP_TIMEOUT=timeout_s,
+                   MIREDUCE_INJECT_FAULT=fault)
+        procs.append(subprocess.Popen([os.path.join(BIN, "bootstrap_test")], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    return procs
+
+
+@pytest.mark.parametrize("step", [0, 2, 4])
+def test_bootstrap_peer_crash_detected(step):
+    # Injected crash of rank 1 mid-exchange: every other rank fails with a bootstrap error quickly
+    # (the reference's MPI job would hang or die with MPI_ERRORS_ARE_FATAL, mpi/reduce.c:32-106).
+    import time
+    t0 = time.time()
+    procs = _spawn_bootstrap_ranks(3, f"exit@1:{step}")
+    outs = [p.communicate(timeout=60) for p in procs]
+    codes = [p.returncode for p in procs]
+    assert codes[1] == 3, outs[1]
+    assert "[fault] rank 1 exits" in outs[1][1]
+    for r in (0, 2):
+        assert codes[r] == 2, (r, codes, outs[r])
+        assert "bootstrap" in outs[r][1]
+    assert time.time() - t0 < 30
+
+
+def test_bootstrap_peer_hang_detected():
+    # Injected hang of rank 2: the others hit the bootstrap deadline (3 s) and exit with an error;
+    # the hung rank is then killed, as a launcher would.
+    import time
+    t0 = time.time()
+    procs = _spawn_bootstrap_ranks(3, "hang@2:3", timeout_s="3")
+    try:
+        for r in (0, 1):
+            out, err = procs[r].communicate(timeout=60)
+            assert procs[r].returncode == 2, (r, err)
+            assert "timed out" in err or "peer closed" in err, err
+        assert time.time() - t0 < 30
+        assert procs[2].poll() is None  # still hung
+    finally:
+        procs[2].kill()
+        procs[2].communicate()

@@ -61,6 +61,7 @@ struct Options {
   int cputhresh = 1;        // reduction.cpp:670
   int iterations = 100;     // reduction.cpp:731
   bool batch_timing = false;  // one event pair around all iterations (throughput) vs per iteration
+  bool cold = false;          // flush L2 + Infinity Cache before every timed iteration
   int unroll = 0;
   int wg_per_cu = 0;
   int policy = -1;
@@ -76,7 +77,7 @@ const std::set<std::string> kKnown = {
     "method", "type", "n", "threads", "kernel", "maxblocks", "cpufinal", "cputhresh", "shmoo",
     "device", "qatest", "noprompt", "prompt", "help", "quiet", "iterations", "acc", "unroll",
     "wg-per-cu", "policy", "pattern", "seed", "fill", "noverify", "json", "log", "master-log",
-    "countdown", "shmoo-max", "trace", "timing"};
+    "countdown", "shmoo-max", "trace", "timing", "cold"};
 
 void usage() {
   std::printf(
@@ -90,6 +91,8 @@ void usage() {
       "  --cputhresh=N    fold on the host when <= N partials remain\n"
       "  --shmoo          sweep n = 1..32M (powers of two, --shmoo-max=N) over kernels, print CSV\n"
       "  --timing=per-iter|batch  event pair per iteration (reference, default) or around all (shmoo default)\n"
+      "  --cold           overwrite a 1 GiB scratch buffer before every timed iteration (evicts the\n"
+      "                   256 MB Infinity Cache and the L2s): HBM numbers for small arrays; per-iter timing\n"
       "  --iterations=100 --acc=TYPE --unroll=2|4|8 --wg-per-cu=N --policy=auto|nt|default\n"
       "  --pattern=smallint|uniform|fullrange|iotamod --seed=N --fill=host|device --noverify\n"
       "  --device=N --json=PATH --log=FILE|none --master-log=FILE|none (default SdkMasterLog.csv) --qatest\n"
@@ -118,8 +121,11 @@ void parallel_fill_host(void* p, uint64_t n, DType t, const FillSpec& s) {
   for (auto& x : pool) x.join();
 }
 
+constexpr size_t kFlushBytes = size_t(1) << 30;  // > 256 MB MALL + 8 x 4 MB L2, written untimed
+
 struct Buffers {
   DeviceBuffer in, out, partials, ladder;  // ladder: ping-pong scratch of kernels 0..6
+  DeviceBuffer flush;                      // --cold: cache-eviction scratch
   std::vector<unsigned char> host;  // input copy (for CPU verification)
   void* pinned = nullptr;           // --cpufinal partials landing zone
   ~Buffers() {
@@ -194,7 +200,8 @@ Timing time_iterations(Runner& r, uint64_t n, int iters) {
   EventTimer ev;
   HIP_CHECK(hipDeviceSynchronize());
   const bool host_path = r.o.kernel >= 7 && (r.o.cpufinal || r.o.cputhresh > 1);
-  if (r.o.batch_timing && !host_path) {  // back-to-back launches, one event pair: throughput
+  if (r.o.cold && r.b.flush.bytes() < kFlushBytes) r.b.flush.allocate(kFlushBytes);
+  if (r.o.batch_timing && !host_path && !r.o.cold) {  // back-to-back launches, one event pair: throughput
     ev.start(r.s);
     for (int i = 0; i < iters; ++i) r.run_once(n, t.result);
     ev.stop(r.s);
@@ -205,6 +212,10 @@ Timing time_iterations(Runner& r, uint64_t n, int iters) {
     return t;
   }
   for (int i = 0; i < iters; ++i) {
+    if (r.o.cold) {  // evict the array from L2 / MALL outside the event pair
+      HIP_CHECK(hipMemsetAsync(r.b.flush.get(), i & 0xFF, kFlushBytes, r.s));
+      HIP_CHECK(hipStreamSynchronize(r.s));
+    }
     const double h0 = StopWatch::now_s();
     ev.start(r.s);
     const bool host = r.run_once(n, t.result);
@@ -312,7 +323,7 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
         .set("acc", dtype_cli_name(o.acc)).set("n", o.n).set("bytes", static_cast<uint64_t>(bytes))
         .set("kernel", o.kernel).set("block", r.plan.block).set("grid", r.plan.grid).set("unroll", r.plan.unroll)
         .set("groups", r.plan.groups).set("nontemporal", r.plan.nontemporal).set("cpufinal", o.cpufinal)
-        .set("iterations", o.iterations).set("avg_ms", t.avg_ms).set("median_ms", st.median).set("min_ms", st.min)
+        .set("iterations", o.iterations).set("cold", o.cold).set("timing", o.batch_timing && !o.cold ? "batch" : "per-iter").set("avg_ms", t.avg_ms).set("median_ms", st.median).set("min_ms", st.min)
         .set("max_ms", st.max).set("std_ms", st.stddev).set("gb_per_s", secs > 0 ? bytes / secs / kGB : 0.0)
         .set("gib_per_s", secs > 0 ? bytes / secs / kGiB : 0.0).set("bytes_per_GB", kGB)
         .set("gpu_result", acc_as_double(t.result, o.acc)).set("verified", checked ? ok : true)
@@ -437,6 +448,7 @@ int main(int argc, char** argv) {
       const std::string tm = args.str_or("timing", args.has("shmoo") ? "batch" : "per-iter");
       if (tm != "batch" && tm != "per-iter") throw CliError("--timing must be per-iter|batch");
       o.batch_timing = tm == "batch";
+      o.cold = args.has("cold");
     }
     if (o.kernel < 0 || o.kernel > 8) throw CliError("--kernel must be 0..8");
     if (o.kernel >= 7 && o.threads != 0 && o.threads != 256 && o.threads != 512 && o.threads != 1024)

@@ -182,3 +182,13 @@ def test_reduce_xgmi_direct_lost_peer_fails_fast(kind, monkeypatch):
     assert f"[fault] rank 1 {'exits' if kind == 'exit' else 'hangs'}" in r.stderr
     assert "[rank 0] error: bootstrap" in r.stderr, r.stderr[-2000:]
     assert time.time() - t0 < 180
+
+
+def test_reduction_cold_cache_mode(tmp_path):
+    # --cold evicts the array from L2 / Infinity Cache before each timed iteration (per-iter timing).
+    js = tmp_path / "cold.jsonl"
+    r = reduction(tmp_path, "--method=SUM", "--type=double", "--n=16777216", "--iterations=5", "--cold",
+                  f"--json={js}")
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(js.read_text().splitlines()[-1])
+    assert d["cold"] is True and d["timing"] == "per-iter" and d["verified"] is True

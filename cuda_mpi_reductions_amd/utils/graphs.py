@@ -40,7 +40,9 @@ class StepGraph:
 
     def _capture_one(self, count: int) -> "torch.cuda.CUDAGraph":
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: HIP calls made by other threads meanwhile (ProcessGroupNCCL's watchdog
+        # querying events of earlier eager collectives) must not invalidate this capture.
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             works = [self.step_fn(j) for j in range(count)]
             for w in works:
                 if w is not None:

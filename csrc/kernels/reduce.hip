@@ -355,7 +355,10 @@ const Table& table() {
 //   8 GB i64 max        256 x  2, 3 WG/CU, nt   7.30 TB/s (best; 512 x 16 x 1 is not in the top 8)
 //   8 GB f32 sum / max  256 x  2, 3 WG/CU, nt   7.20 / 7.25 TB/s (best 7.21 / 7.25)
 //   8 GB i32 sum        256 x  2, 3 WG/CU, nt   7.20 TB/s (best 7.25)
-//   256 MB              512 x 16, 1 WG/CU, default policy (Infinity-Cache re-reads) 6.72 TB/s
+//   192-384 MB          256 x  2, 3 WG/CU, nt   256 MB: 6.33 TB/s warm, 5.93 cold (--cold). The
+//                       earlier warm-only pick (512 x 16 x 1, default policy: 6.25 warm) fell to
+//                       2.69 TB/s when the array was not already in the Infinity Cache
+//                       (profiles/r1_bench/plan_256mb.csv): non-nt loads are never the safe choice.
 //   128 MB              256 x  4, 3 WG/CU, nt   6.10 TB/s (best; launch + tail dominate)
 // Fewer, fatter workgroups beat the "fill every wave slot" grid (8 WG/CU: 6.91 TB/s at 8 GB).
 struct Defaults {
@@ -364,8 +367,7 @@ struct Defaults {
 Defaults tuned_defaults(size_t bytes, DType t) {
   constexpr size_t MB = 1ull << 20;
   if (t == DType::Float64 && bytes >= 3072 * MB) return {512, 16, 1, 1, 0};
-  if (bytes > 384 * MB) return {256, 2, 3, 1, 0};
-  if (bytes > 192 * MB) return {512, 16, 1, 0, 0};
+  if (bytes > 192 * MB) return {256, 2, 3, 1, 0};
   return {256, 4, 3, 1, 0};
 }
 constexpr int kDefaultGroups = 8;

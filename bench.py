@@ -263,6 +263,9 @@ def main(argv=None) -> int:
             "native_ext": os.path.basename(native_path()),
         }
         print(json.dumps(line), flush=True)
+    if sg is not None:
+        sg.reset()  # captured RCCL work must not outlive the communicator
+    _sync(dev)
     pdist.shutdown(ctx)
     return 0 if verified in (None, True) else 1
 

@@ -90,3 +90,10 @@ class StepGraph:
             g.replay()
         if self.rem:
             self.graphs[1].replay()
+
+    def reset(self) -> None:
+        """Free the captured graphs. Call before destroying the process group: graphs that captured
+        RCCL kernels must not outlive the communicator they reference."""
+        for g in self.graphs:
+            g.reset()
+        self.graphs = []

@@ -129,3 +129,18 @@ def test_bootstrap_peer_hang_detected():
     finally:
         procs[2].kill()
         procs[2].communicate()
+
+
+def test_slurm_scripts_dry_run():
+    # tools/slurm/ plays the role of mpi/submit_all.sh + mpi/ccni_vn.sh (SLURM job orchestration).
+    env = dict(os.environ, DRY_RUN="1", PARTITION="mi355x", EXTRA="--dtypes=INT,DOUBLE --retries=2")
+    r = run(["bash", os.path.join(ROOT, "tools", "slurm", "submit_all.sh"), "1", "8"], env=env, timeout=60)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 2 and lines[1].startswith("sbatch -p mi355x --nodes 1 --ntasks-per-node 8 --gpus-per-node 8")
+    env.update(SLURM_NTASKS="8", SLURM_JOB_ID="42", MODE="scalar")
+    r = run(["bash", os.path.join(ROOT, "tools", "slurm", "mi355x_sweep.sbatch")], env=env, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines()[-1].endswith("reduce_xgmi --mode=scalar --dtypes=INT,DOUBLE --retries=2")
+    bad = run(["bash", os.path.join(ROOT, "tools", "slurm", "submit_all.sh"), "16"], env=env, timeout=60)
+    assert bad.returncode == 2

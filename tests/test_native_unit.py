@@ -144,3 +144,11 @@ def test_slurm_scripts_dry_run():
     assert r.stdout.strip().splitlines()[-1].endswith("reduce_xgmi --mode=scalar --dtypes=INT,DOUBLE --retries=2")
     bad = run(["bash", os.path.join(ROOT, "tools", "slurm", "submit_all.sh"), "16"], env=env, timeout=60)
     assert bad.returncode == 2
+
+
+def test_plot_shmoo_tool(tmp_path):
+    csv = os.path.join(ROOT, "profiles", "r1_bench", "shmoo_double_sum_r1.csv")
+    out = tmp_path / "shmoo.png"
+    r = run(["python", os.path.join(ROOT, "tools", "plot_shmoo.py"), csv, "-o", str(out), "--title", "t"], timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert out.exists() and out.stat().st_size > 1000

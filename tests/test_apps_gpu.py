@@ -125,6 +125,18 @@ def test_bench_rehearsal_two_ranks_one_gpu(tmp_path):
     assert d["verified"] is True and d["n_gpus"] == 2 and d["config"]["backend"] == "gloo"
 
 
+def test_bench_graph_capture_failure_falls_back_on_all_ranks(tmp_path, monkeypatch):
+    # gloo collectives on GPU tensors cannot be captured: every rank must agree on the failure
+    # and fall back to eager issue (never some ranks replaying graphs and others not).
+    monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    r = torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "6",
+                     "--warmup", "2", "--elements", "20000003", "--launch", "graph"], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["verified"] is True
+    assert d["config"]["launch"].startswith("eager (graph capture failed"), d["config"]["launch"]
+
+
 @pytest.mark.parametrize("launch", ["graph", "eager"])
 def test_bench_launch_modes(tmp_path, launch):
     # Default launch on a GPU is graph replay of the timed steps; both modes verify every slot.

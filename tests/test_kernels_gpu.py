@@ -304,3 +304,35 @@ def test_step_graph_failed_capture_falls_back():
     assert not sg.capture() and not sg.captured and sg.error
     # the device is still usable afterwards
     assert torch.ones(3, device=DEV).sum().item() == 3.0
+
+
+@pytest.mark.parametrize("dt", [torch.int32, torch.int64, torch.float32, torch.float64])
+@pytest.mark.parametrize("where", ["first", "last", "random", "tile_edge"])
+def test_planted_extremes_large(dt, where):
+    # a planted min and max in a large array (no CPU oracle needed) — at the
+    # unaligned head, the sub-vector tail, a random index, and the last full-tile boundary.
+    import random
+    n = 150_000_007
+    base = torch.empty(n + 3, dtype=dt, device=DEV)
+    x = base[3:]  # misaligned: exercises the scalar head
+    fill_(x, "uniform" if dt.is_floating_point else "smallint", seed=77)
+    rng = random.Random(hash((str(dt), where)) & 0xFFFF)
+    if where == "first":
+        i_min, i_max = 0, 1
+    elif where == "last":
+        i_min, i_max = n - 1, n - 2
+    elif where == "tile_edge":
+        vec = 16 // x.element_size()
+        i_min = (n // (256 * 2 * vec)) * (256 * 2 * vec) - 1
+        i_max = i_min + 1
+    else:
+        i_min, i_max = rng.randrange(n), rng.randrange(n)
+        if i_max == i_min:
+            i_max = (i_min + 1) % n
+    lo, hi = (-1.5, 2.5) if dt.is_floating_point else (-7, 1 << 20)
+    x[i_min] = lo
+    x[i_max] = hi
+    assert reduce(x, "min").item() == lo
+    assert reduce(x, "max").item() == hi
+    del base, x
+    torch.cuda.empty_cache()

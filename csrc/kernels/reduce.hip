@@ -11,14 +11,17 @@
 //     (reduction_kernel.cu:110-122 assumes warp lockstep — wrong on CDNA), then one LDS slot per
 //     wave;
 //   * single launch: each workgroup publishes its partial write-through (sc1), drains, and takes
-//     an agent-scope ticket; the last arriver of each of G ticket groups folds its group, and the
-//     last group folds the G group partials (threadFenceReduction_kernel.cu:116-171 idea, but
-//     with the gfx950 release/acquire forms and a sharded fan-in: one counter for 2048
-//     arrivals costs ~25 us, eight counters ~3 us).
+//     an agent-scope ticket on one of G sharded counters; the last arriver of each group takes a
+//     ticket on the top counter and the last of those folds every partial in one parallel sc1
+//     load round (threadFenceReduction_kernel.cu:116-171 idea, but with the gfx950
+//     release/acquire forms and a sharded fan-in: one counter for 2048 arrivals costs ~25 us,
+//     eight counters ~3 us). MIREDUCE_FANIN=tree selects the older two-level fold (each group's
+//     last arriver folds and republishes its group first).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -91,6 +94,7 @@ struct Args {
   unsigned* tickets;     // [(groups + 1) * kTicketStride]
   void* out;             // AccT[1]
   int groups;            // 0: two-pass mode (write partials only)
+  int flat;              // 1: group last-arrivers only count; the final arriver folds every partial
 };
 
 template <class V, int BLOCK, int UNROLL, bool NT>
@@ -185,6 +189,28 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   }
   __syncthreads();
   if (!is_last) return;
+
+  if (a.flat) {
+    // Flat fan-in: the group's last arriver only takes a ticket on the top counter; the last of
+    // those folds all gridDim.x partials at once (one parallel sc1 load round instead of a
+    // group fold + group-partial publish + second fold: two memory round trips shorter).
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(&a.tickets[g * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned prev = __hip_atomic_fetch_add(&a.tickets[G * kTicketStride], 1u,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      is_last = (prev == G - 1);
+    }
+    __syncthreads();
+    if (!is_last) return;
+    AccT t = OpT::template identity<AccT>();
+    for (unsigned i = threadIdx.x; i < gridDim.x; i += BLOCK) t = OpT::apply(t, load_sc1(&partials[i]));
+    t = block_reduce<OpT, AccT, BLOCK>(t, lds);
+    if (threadIdx.x == 0) {
+      *static_cast<AccT*>(a.out) = t;
+      __hip_atomic_store(&a.tickets[G * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
 
   // Last arriver of group g: fold partials g, g+G, g+2G, ... (sc1 loads: L1 never holds them).
   AccT s = OpT::template identity<AccT>();
@@ -372,6 +398,17 @@ Defaults tuned_defaults(size_t bytes, DType t) {
 }
 constexpr int kDefaultGroups = 8;
 
+// Fan-in shape of the single-pass finalisation; MIREDUCE_FANIN=flat|tree overrides (A/B runs).
+bool fanin_flat() {
+  static const int v = [] {
+    const char* e = std::getenv("MIREDUCE_FANIN");
+    if (e && std::strcmp(e, "tree") == 0) return 0;
+    if (e && std::strcmp(e, "flat") == 0) return 1;
+    return 1;  // flat: 1 GB 139.8 vs 140.1 us, 8 MB 6.24 vs 6.80 us (profiles/r1_bench/fanin_ab.txt)
+  }();
+  return v == 1;
+}
+
 template <class OpT, class AccT>
 void launch_finalize(const void* partials, uint64_t count, void* out, hipStream_t s) {
   hipLaunchKernelGGL((kern::finalize<OpT, AccT>), dim3(1), dim3(256), 0, s,
@@ -478,6 +515,7 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   if (groups > kMaxGroups) groups = kMaxGroups;
   if (groups > p.grid) groups = p.grid;
   p.groups = p.single_pass ? groups : 0;
+  p.flat = p.single_pass && fanin_flat();
   return p;
 }
 
@@ -503,6 +541,7 @@ LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out
   a.tickets = ws.tickets();
   a.out = out;
   a.groups = p.groups;
+  a.flat = p.flat ? 1 : 0;
   const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0];
   fn(a, p.grid, stream);
   MIREDUCE_HIP_THROW(hipGetLastError());
@@ -531,6 +570,7 @@ BoundReduce::BoundReduce(const void* in, size_t n, DType t, Op op, DType acc, vo
   a.tickets = ws.tickets();
   a.out = out;
   a.groups = p.groups;
+  a.flat = p.flat ? 1 : 0;
   impl_ = new Impl{a, table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0],
                    p, op, acc};
 }

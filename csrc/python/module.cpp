@@ -40,6 +40,7 @@ py::dict plan_dict(const LaunchPlan& p) {
   d["nontemporal"] = p.nontemporal;
   d["pipelined"] = p.pipelined;
   d["single_pass"] = p.single_pass;
+  d["flat"] = p.flat;
   d["head"] = p.head;
   d["nvec"] = p.nvec;
   d["tail"] = p.tail;

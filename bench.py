@@ -13,8 +13,8 @@ MAX elapsed time over ranks defines the measurement. Value = total bytes reduced
 elapsed / 1e9 (GB = 1e9 B, the CUDA sample's unit, reduction.cpp:744-745). Steps are
 independent reductions, so by default step i+1's local reduce overlaps step i's all-reduce
 (RCCL runs on its own stream); ``--serial`` makes each step wait for its all-reduce.
-By default the K timed steps are replayed from captured hipGraphs (``--launch``; chunks of 32 steps,
-captured after the W eager warm-up steps and replayed once untimed): eager Python issue of the
+By default the K timed steps are replayed from captured hipGraphs (``--launch``; chunks of up to 128
+steps, captured after the W eager warm-up steps and replayed once untimed): eager Python issue of the
 RCCL all-reduce leaves ~22 us GPU gaps per step, which at N=8 (0.14 ms per step) would cost ~15 %.
 Every step's result is checked after timing against torch's own fp64 reduction of the shards.
 
@@ -59,7 +59,9 @@ def parse_args(argv=None):
     p.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
                    help="graph: replay the timed steps as captured hipGraphs (chunks of --graph-chunk steps); "
                         "eager: issue every step from Python; auto: graph on GPUs when capturable")
-    p.add_argument("--graph-chunk", type=int, default=32, help="steps per captured graph")
+    p.add_argument("--graph-chunk", type=int, default=128,
+                   help="steps per captured graph (each graph ends by joining its last all-reduce, so fewer, "
+                        "longer graphs leave fewer all-reduce-latency bubbles at N>1)")
     p.add_argument("--inject-fault", default=None,
                    help="failure-detection test: KIND[@RANK][:STEP], KIND = exit|hang|corrupt|delay=<ms> "
                         "(steps count warm-up first; forces --launch eager)")

@@ -44,8 +44,8 @@ COMMLIB     := $(BUILD)/lib/libmireduce_comm.a
 APPS := $(BUILD)/bin/reduction $(BUILD)/bin/reduce_xgmi $(BUILD)/bin/bandwidth_test
 MPI_APP := $(BUILD)/bin/reduce_mpi
 
-.PHONY: all python apps mpi clean asan unit
-all: python apps mpi unit
+.PHONY: all python apps mpi clean asan unit diag
+all: python apps mpi unit diag
 
 python: $(PYEXT)
 apps: $(APPS)
@@ -91,6 +91,12 @@ $(MPI_APP): $(MPI_SRCS) $(HEADERS)
 	@mkdir -p $(dir $@)
 	g++ $(CXXSTD) -O3 -Wall -Icsrc/include -DMIREDUCE_NO_HIP -I$(MPI_HOME)/include \
 	    $(MPI_SRCS) -static-libstdc++ -static-libgcc $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,$(MPI_HOME)/lib -o $@
+
+# Diagnostic: per-workgroup timeline of streaming-body variants (docs/TUNING.md).
+diag: $(BUILD)/bin/wg_timeline
+$(BUILD)/bin/wg_timeline: tools/wg_timeline.hip
+	@mkdir -p $(dir $@)
+	$(HIPCC) -std=c++17 -O3 --offload-arch=$(ARCH) $< -o $@
 
 # Native unit tests (host code only) and the bootstrap multi-process test.
 UNIT := $(BUILD)/bin/host_unit $(BUILD)/bin/bootstrap_test

@@ -62,6 +62,7 @@ MPI_Datatype mpi_type(DType t) {
     case DType::Int64: return MPI_LONG_LONG;
     case DType::Float32: return MPI_FLOAT;
     case DType::Float64: return MPI_DOUBLE;
+    default: break;
   }
   return MPI_DATATYPE_NULL;
 }
@@ -82,6 +83,7 @@ void generate(Mt19937& g, DType t, void* buf, uint64_t n) {
     case DType::Int64: { auto* p = static_cast<int64_t*>(buf); for (uint64_t i = 0; i < n; ++i) { uint64_t hi = g.genrand_int32(); p[i] = static_cast<int64_t>((hi << 32) | g.genrand_int32()); } break; }
     case DType::Float32: { auto* p = static_cast<float*>(buf); for (uint64_t i = 0; i < n; ++i) p[i] = static_cast<float>(g.genrand_res53()); break; }
     case DType::Float64: { auto* p = static_cast<double*>(buf); for (uint64_t i = 0; i < n; ++i) p[i] = g.genrand_res53(); break; }
+    default: break;
   }
 }
 
@@ -132,6 +134,7 @@ bool verify(DType t, Op o, const void* send, const void* recv, uint64_t count, i
     case DType::Int64: return verify_samples(o, static_cast<const int64_t*>(send), static_cast<const int64_t*>(recv), count, rank, size, root, MPI_LONG_LONG);
     case DType::Float32: return verify_samples(o, static_cast<const float*>(send), static_cast<const float*>(recv), count, rank, size, root, MPI_FLOAT);
     case DType::Float64: return verify_samples(o, static_cast<const double*>(send), static_cast<const double*>(recv), count, rank, size, root, MPI_DOUBLE);
+    default: break;
   }
   return false;
 }
@@ -158,6 +161,7 @@ void corrupt_first(DType t, Op o, void* p) {
     }
     case DType::Float32: corrupt_first_t(o, static_cast<float*>(p)); break;
     case DType::Float64: corrupt_first_t(o, static_cast<double*>(p)); break;
+    default: break;
   }
 }
 
@@ -219,6 +223,7 @@ int main(int argc, char** argv) {
       for (auto& s : list) {
         DType t;
         if (!parse_dtype(s, &t)) throw CliError("unknown dtype " + s);
+        if (dtype_is_half(t)) throw CliError("--dtypes=" + s + ": MPI has no 16-bit float datatype (reduce.c types: INT, DOUBLE; plus LONG, FLOAT)");
         dtypes.push_back(t);
       }
     }
@@ -254,6 +259,7 @@ int main(int argc, char** argv) {
         case DType::Int64: return n_longs;
         case DType::Float32: return n_floats;
         case DType::Float64: return n_doubles;
+        default: break;
       }
       return 0;
     };

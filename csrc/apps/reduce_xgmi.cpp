@@ -99,6 +99,7 @@ SavedElement corrupt_any(void* d, uint64_t i, DType t, Op o) {
     case DType::Int64: { const int64_t v = corrupt_element<int64_t>(d, i, o); std::memcpy(s.bytes, &v, 8); break; }
     case DType::Float32: { const float v = corrupt_element<float>(d, i, o); std::memcpy(s.bytes, &v, 4); break; }
     case DType::Float64: { const double v = corrupt_element<double>(d, i, o); std::memcpy(s.bytes, &v, 8); break; }
+    default: break;
   }
   return s;
 }
@@ -113,6 +114,7 @@ uint64_t global_count(DType t, uint64_t ints, uint64_t longs, uint64_t floats, u
     case DType::Int64: return longs;
     case DType::Float32: return floats;
     case DType::Float64: return doubles;
+    default: break;
   }
   return 0;
 }
@@ -292,6 +294,7 @@ bool run_vector(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>&
             case DType::Int64: vok = check_samples<int64_t>(c, o, in_ptr(c, b), out_ptr(c, b), b.count); break;
             case DType::Float32: vok = check_samples<float>(c, o, in_ptr(c, b), out_ptr(c, b), b.count); break;
             case DType::Float64: vok = check_samples<double>(c, o, in_ptr(c, b), out_ptr(c, b), b.count); break;
+            default: break;
           }
           ok = ok && vok;
         }
@@ -584,6 +587,7 @@ int main(int argc, char** argv) {
       for (auto& s : list) {
         DType t;
         if (!parse_dtype(s, &t)) throw CliError("unknown dtype " + s);
+        if (dtype_is_half(t)) throw CliError("--dtypes=" + s + ": bf16/half are reduced by the single-GPU reduction app and the Python API; the cross-rank apps keep the reduce.c types (INT, LONG, FLOAT, DOUBLE)");
         dtypes.push_back(t);
       }
     }

@@ -351,6 +351,7 @@ void run_shmoo(Options o, Workspace& ws, hipStream_t s, uint64_t max_n) {
   const int kernels[] = {0, 1, 2, 3, 4, 5, 6, 8, 7};
   for (uint64_t n = 1; n <= max_n; n *= 2) {
     for (int k : kernels) {
+      if (k <= 6 && dtype_is_half(o.dtype)) continue;  // ladder kernels: reference element types only
       o.kernel = k;
       o.cpufinal = false;
       o.cputhresh = 1;
@@ -451,6 +452,8 @@ int main(int argc, char** argv) {
       o.cold = args.has("cold");
     }
     if (o.kernel < 0 || o.kernel > 8) throw CliError("--kernel must be 0..8");
+    if (o.kernel <= 6 && dtype_is_half(o.dtype))
+      throw CliError("--kernel 0..6 (the reference's ladder) covers int/int64/float/double; bf16/half use kernels 7/8");
     if (o.kernel >= 7 && o.threads != 0 && o.threads != 256 && o.threads != 512 && o.threads != 1024)
       throw CliError("--threads must be 256, 512 or 1024 for kernels 7/8");
     if (o.kernel <= 6 && o.threads == 0) o.threads = 256;

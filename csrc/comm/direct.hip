@@ -113,6 +113,7 @@ void rs_by_type(DType t, const kern::PeerPtrs& ins, int world, void* out, uint64
     case DType::Int64: launch_rs<OpT, int64_t>(ins, world, out, b, e, s); break;
     case DType::Float32: launch_rs<OpT, float>(ins, world, out, b, e, s); break;
     case DType::Float64: launch_rs<OpT, double>(ins, world, out, b, e, s); break;
+    default: MIREDUCE_REQUIRE(false, "direct: int32, int64, float32 or float64 only");
   }
 }
 }  // namespace

@@ -32,6 +32,8 @@ ncclDataType_t nccl_type(DType t) {
     case DType::Int64: return ncclInt64;
     case DType::Float32: return ncclFloat32;
     case DType::Float64: return ncclFloat64;
+    case DType::BFloat16: return ncclBfloat16;
+    case DType::Float16: return ncclFloat16;
   }
   return ncclFloat64;
 }

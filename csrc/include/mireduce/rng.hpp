@@ -10,6 +10,7 @@
 
 #include <cstdint>
 
+#include "mireduce/half.hpp"
 #include "mireduce/ops.hpp"
 #include "mireduce/types.hpp"
 
@@ -54,6 +55,26 @@ MIREDUCE_HD T pattern_value(Pattern p, uint64_t seed, uint64_t i, double value) 
     if constexpr (sizeof(T) == 8) return static_cast<T>(h);
     else return static_cast<T>(static_cast<uint32_t>(h >> 32));
   }
+}
+
+// 16-bit floats (half.hpp): the value is produced in fp32 and rounded to nearest even; the uniform
+// patterns draw exactly as many random bits as the type's significand holds, so U[0,1) values are
+// exact and never round up to 1.0.
+template <class H>
+MIREDUCE_HD uint16_t pattern_half_bits(Pattern p, uint64_t seed, uint64_t i, double value) {
+  float f;
+  switch (p) {
+    case Pattern::Constant: f = static_cast<float>(value); break;
+    case Pattern::IotaMod: f = static_cast<float>(i & 1023u); break;
+    default: {
+      const uint64_t h = element_bits(seed, i);
+      constexpr int P = half_precision<H>::value;
+      if (p == Pattern::SmallInt) f = static_cast<float>(static_cast<double>(h & 0xFFu) / kRandMax);
+      else f = static_cast<float>(h >> (64 - P)) * (1.0f / static_cast<float>(1u << P));
+      break;
+    }
+  }
+  return H::from_float(f).bits;
 }
 
 struct FillSpec {

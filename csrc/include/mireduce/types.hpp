@@ -6,7 +6,8 @@
 // (cuda/C/src/reduction/reduction_kernel.cu:527-564) and {MPI_INT, MPI_DOUBLE} x
 // {MPI_MAX, MPI_MIN, MPI_SUM} across ranks (mpi/reduce.c:21-28). We add int64 (BASELINE config 3)
 // and make the accumulator type explicit so that int32 SUM does not silently wrap
-// (SURVEY.md §8 B7/B11).
+// (SURVEY.md §8 B7/B11). bfloat16 / half (half.hpp) are MI355X additions: read at 16 bytes per
+// lane like every other type, accumulated in fp32.
 #pragma once
 
 #include <cstddef>
@@ -15,10 +16,10 @@
 
 namespace mireduce {
 
-enum class DType : int { Int32 = 0, Int64 = 1, Float32 = 2, Float64 = 3 };
+enum class DType : int { Int32 = 0, Int64 = 1, Float32 = 2, Float64 = 3, BFloat16 = 4, Float16 = 5 };
 enum class Op : int { Sum = 0, Min = 1, Max = 2 };
 
-constexpr int kNumDTypes = 4;
+constexpr int kNumDTypes = 6;
 constexpr int kNumOps = 3;
 
 inline size_t dtype_size(DType t) {
@@ -27,11 +28,14 @@ inline size_t dtype_size(DType t) {
     case DType::Int64: return 8;
     case DType::Float32: return 4;
     case DType::Float64: return 8;
+    case DType::BFloat16: return 2;
+    case DType::Float16: return 2;
   }
   return 0;
 }
 
-inline bool dtype_is_float(DType t) { return t == DType::Float32 || t == DType::Float64; }
+inline bool dtype_is_half(DType t) { return t == DType::BFloat16 || t == DType::Float16; }
+inline bool dtype_is_float(DType t) { return t == DType::Float32 || t == DType::Float64 || dtype_is_half(t); }
 
 // Names as they appear in the reference's GNUPlot lines ("INT", "DOUBLE"; mpi/reduce.c:81,95)
 // plus the two new element types.
@@ -41,6 +45,8 @@ inline const char* dtype_gnuplot_name(DType t) {
     case DType::Int64: return "LONG";
     case DType::Float32: return "FLOAT";
     case DType::Float64: return "DOUBLE";
+    case DType::BFloat16: return "BF16";
+    case DType::Float16: return "HALF";
   }
   return "?";
 }
@@ -52,6 +58,8 @@ inline const char* dtype_cli_name(DType t) {
     case DType::Int64: return "int64";
     case DType::Float32: return "float";
     case DType::Float64: return "double";
+    case DType::BFloat16: return "bf16";
+    case DType::Float16: return "half";
   }
   return "?";
 }
@@ -74,8 +82,10 @@ bool parse_op_strict(const std::string& s, Op* out);
 bool parse_op(const std::string& s, Op* out);
 
 // Default accumulator: widen int32 SUM to int64 and fp32 SUM to fp64; MIN/MAX keep the
-// element type (they cannot overflow or lose precision).
+// element type (they cannot overflow or lose precision). The 16-bit float types always
+// accumulate (and return) fp32: every 16-bit value is exact in fp32.
 inline DType default_acc(DType t, Op o) {
+  if (dtype_is_half(t)) return DType::Float32;
   if (o != Op::Sum) return t;
   if (t == DType::Int32) return DType::Int64;
   if (t == DType::Float32) return DType::Float64;
@@ -84,6 +94,7 @@ inline DType default_acc(DType t, Op o) {
 
 // Accumulator types we instantiate: same as input, or the widened type for SUM.
 inline bool acc_supported(DType t, Op o, DType acc) {
+  if (dtype_is_half(t)) return acc == DType::Float32;
   if (acc == t) return true;
   if (o != Op::Sum) return false;
   return (t == DType::Int32 && acc == DType::Int64) || (t == DType::Float32 && acc == DType::Float64);

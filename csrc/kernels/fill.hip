@@ -40,6 +40,23 @@ __global__ __launch_bounds__(256) void fill_kernel_scalar(T* __restrict__ out, u
     out[i] = pattern_value<T>(s.pattern, s.seed, s.offset + i, s.value);
 }
 
+// 16-bit floats: eight 2-byte patterns per 16-byte store.
+template <class H>
+__global__ __launch_bounds__(256) void fill_kernel_half(uint16_t* __restrict__ out, uint64_t n, FillSpec s) {
+  using V = uint16_t __attribute__((ext_vector_type(8)));
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const uint64_t nvec = reinterpret_cast<uintptr_t>(out) % 16 == 0 ? n / 8 : 0;
+  V* vout = reinterpret_cast<V*>(out);
+  for (uint64_t i = tid; i < nvec; i += stride) {
+    V v;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = pattern_half_bits<H>(s.pattern, s.seed, s.offset + i * 8 + k, s.value);
+    __builtin_nontemporal_store(v, vout + i);
+  }
+  for (uint64_t i = nvec * 8 + tid; i < n; i += stride) out[i] = pattern_half_bits<H>(s.pattern, s.seed, s.offset + i, s.value);
+}
+
 }  // namespace kern
 
 namespace {
@@ -57,6 +74,22 @@ void launch_fill(void* ptr, size_t n, const FillSpec& s, hipStream_t st) {
                        st, static_cast<T*>(ptr), static_cast<uint64_t>(n), s);
 }
 
+template <class H>
+void launch_fill_half(void* ptr, size_t n, const FillSpec& s, hipStream_t st) {
+  if (n == 0) return;
+  uint64_t blocks = (n / 8 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(kern::fill_kernel_half<H>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st,
+                     static_cast<uint16_t*>(ptr), static_cast<uint64_t>(n), s);
+}
+
+template <class H>
+void host_fill_half(void* ptr, size_t n, const FillSpec& s) {
+  uint16_t* p = static_cast<uint16_t*>(ptr);
+  for (size_t i = 0; i < n; ++i) p[i] = pattern_half_bits<H>(s.pattern, s.seed, s.offset + i, s.value);
+}
+
 template <class T>
 void host_fill(void* ptr, size_t n, const FillSpec& s) {
   T* p = static_cast<T*>(ptr);
@@ -70,6 +103,8 @@ void fill_device(void* ptr, size_t n, DType t, const FillSpec& spec, hipStream_t
     case DType::Int64: launch_fill<int64_t>(ptr, n, spec, stream); break;
     case DType::Float32: launch_fill<float>(ptr, n, spec, stream); break;
     case DType::Float64: launch_fill<double>(ptr, n, spec, stream); break;
+    case DType::BFloat16: launch_fill_half<bf16_t>(ptr, n, spec, stream); break;
+    case DType::Float16: launch_fill_half<f16_t>(ptr, n, spec, stream); break;
   }
   MIREDUCE_HIP_THROW(hipGetLastError());
 }
@@ -80,6 +115,8 @@ void fill_host(void* ptr, size_t n, DType t, const FillSpec& spec) {
     case DType::Int64: host_fill<int64_t>(ptr, n, spec); break;
     case DType::Float32: host_fill<float>(ptr, n, spec); break;
     case DType::Float64: host_fill<double>(ptr, n, spec); break;
+    case DType::BFloat16: host_fill_half<bf16_t>(ptr, n, spec); break;
+    case DType::Float16: host_fill_half<f16_t>(ptr, n, spec); break;
   }
 }
 

@@ -226,6 +226,8 @@ int ladder_reduce(int kernel, const void* in, uint64_t n, DType t, Op op, DType 
                   int max_threads, int max_blocks, hipStream_t s) {
   MIREDUCE_REQUIRE(kernel >= 0 && kernel <= 6, "ladder kernel must be 0..6");
   MIREDUCE_REQUIRE(acc_supported(t, op, acc), "unsupported (dtype, op, accumulator) combination");
+  MIREDUCE_REQUIRE(!dtype_is_half(t), "ladder kernels 0..6 cover the reference's element types (int, float, double, "
+                                      "int64); bf16/half use the streaming kernel (7/8)");
   using namespace ladder;
 #define MIREDUCE_LADDER_CASE(OPT, T, A) return run<OPT, T, A>(kernel, in, n, out, scratch, max_threads, max_blocks, s)
   switch (op) {
@@ -235,6 +237,7 @@ int ladder_reduce(int kernel, const void* in, uint64_t n, DType t, Op op, DType 
         case DType::Int64: MIREDUCE_LADDER_CASE(SumOp, int64_t, int64_t);
         case DType::Float32: if (acc == DType::Float64) MIREDUCE_LADDER_CASE(SumOp, float, double); MIREDUCE_LADDER_CASE(SumOp, float, float);
         case DType::Float64: MIREDUCE_LADDER_CASE(SumOp, double, double);
+        default: break;
       }
       break;
     case Op::Min:
@@ -243,6 +246,7 @@ int ladder_reduce(int kernel, const void* in, uint64_t n, DType t, Op op, DType 
         case DType::Int64: MIREDUCE_LADDER_CASE(MinOp, int64_t, int64_t);
         case DType::Float32: MIREDUCE_LADDER_CASE(MinOp, float, float);
         case DType::Float64: MIREDUCE_LADDER_CASE(MinOp, double, double);
+        default: break;
       }
       break;
     case Op::Max:
@@ -251,6 +255,7 @@ int ladder_reduce(int kernel, const void* in, uint64_t n, DType t, Op op, DType 
         case DType::Int64: MIREDUCE_LADDER_CASE(MaxOp, int64_t, int64_t);
         case DType::Float32: MIREDUCE_LADDER_CASE(MaxOp, float, float);
         case DType::Float64: MIREDUCE_LADDER_CASE(MaxOp, double, double);
+        default: break;
       }
       break;
   }

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "mireduce/check.hpp"
+#include "mireduce/half.hpp"
 #include "mireduce/ops.hpp"
 #include "mireduce/reduce.hpp"
 
@@ -38,6 +39,25 @@ template <> struct Vec16<int32_t> { using type = int32_t __attribute__((ext_vect
 template <> struct Vec16<int64_t> { using type = int64_t __attribute__((ext_vector_type(2))); static constexpr int N = 2; };
 template <> struct Vec16<float>   { using type = float __attribute__((ext_vector_type(4)));   static constexpr int N = 4; };
 template <> struct Vec16<double>  { using type = double __attribute__((ext_vector_type(2)));  static constexpr int N = 2; };
+// 16-bit floats: 8 elements per 16-byte load, carried as four 32-bit words (half.hpp)
+template <> struct Vec16<bf16_t>  { using type = uint32_t __attribute__((ext_vector_type(4))); static constexpr int N = 8; };
+template <> struct Vec16<f16_t>   { using type = uint32_t __attribute__((ext_vector_type(4))); static constexpr int N = 8; };
+
+// Element k of a loaded 16-byte vector, converted to the accumulator type. bf16 -> fp32 is a
+// shift or a mask of the containing word; fp16 -> fp32 is one v_cvt_f32_f16.
+template <class T, class AccT, class V>
+__device__ __forceinline__ AccT elem(const V& v, int k) {
+  if constexpr (std::is_same_v<T, bf16_t>) {
+    const uint32_t w = v[k >> 1];
+    return bits_to_float((k & 1) ? (w & 0xffff0000u) : (w << 16));
+  } else if constexpr (std::is_same_v<T, f16_t>) {
+    const uint32_t w = v[k >> 1];
+    const uint16_t h = static_cast<uint16_t>((k & 1) ? (w >> 16) : (w & 0xffffu));
+    return static_cast<float>(__builtin_bit_cast(_Float16, h));
+  } else {
+    return static_cast<AccT>(v[k]);
+  }
+}
 
 template <class T> struct Bits { using type = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>; };
 
@@ -106,12 +126,12 @@ __device__ __forceinline__ void load_tile(V (&v)[UNROLL], const V* p) {
   }
 }
 
-template <class OpT, class AccT, class V, int N, int UNROLL>
+template <class OpT, class T, class AccT, class V, int N, int UNROLL>
 __device__ __forceinline__ void consume_tile(AccT (&acc)[UNROLL], const V (&v)[UNROLL]) {
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
 #pragma unroll
-    for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], static_cast<AccT>(v[u][k]));
+    for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], elem<T, AccT>(v[u], k));
   }
 }
 
@@ -139,17 +159,17 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       for (uint64_t tn = blockIdx.x + static_cast<uint64_t>(gridDim.x); tn < ntiles; tn += gridDim.x) {
         V nxt[UNROLL];
         load_tile<V, BLOCK, UNROLL, NT>(nxt, vin + tn * kTile + threadIdx.x);
-        consume_tile<OpT, AccT, V, N, UNROLL>(acc, cur);
+        consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, cur);
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) cur[u] = nxt[u];
       }
-      consume_tile<OpT, AccT, V, N, UNROLL>(acc, cur);
+      consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, cur);
     }
   } else {
     for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
       V v[UNROLL];
       load_tile<V, BLOCK, UNROLL, NT>(v, vin + t * kTile + threadIdx.x);
-      consume_tile<OpT, AccT, V, N, UNROLL>(acc, v);
+      consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, v);
     }
   }
   // Vectors past the last full tile, grid-strided.
@@ -157,7 +177,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
        i < a.nvec; i += static_cast<uint64_t>(gridDim.x) * BLOCK) {
     const V v = vin[i];
 #pragma unroll
-    for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], static_cast<AccT>(v[k]));
+    for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], elem<T, AccT>(v, k));
   }
   // Unaligned head and sub-vector tail (< N elements each), folded by the last workgroup.
   if (blockIdx.x == gridDim.x - 1) {
@@ -313,10 +333,14 @@ int combo_index(Op op, DType t, DType acc) {
       return acc == DType::Float32 ? 8 + o : -1;  // 9 (min), 10 (max)
     case DType::Float64:
       return acc == DType::Float64 ? 11 + o : -1;  // 11..13
+    case DType::BFloat16:
+      return acc == DType::Float32 ? 14 + o : -1;  // 14..16
+    case DType::Float16:
+      return acc == DType::Float32 ? 17 + o : -1;  // 17..19
   }
   return -1;
 }
-constexpr int kCombos = 14;
+constexpr int kCombos = 20;
 
 struct Table {
   LaunchFn fn[kCombos][kNumBlocks][kNumUnrolls][2][2];  // [..][policy nt][pipelined]
@@ -369,6 +393,12 @@ const Table& table() {
     fill_combo<SumOp, double, double>(t, 11);
     fill_combo<MinOp, double, double>(t, 12);
     fill_combo<MaxOp, double, double>(t, 13);
+    fill_combo<SumOp, bf16_t, float>(t, 14);
+    fill_combo<MinOp, bf16_t, float>(t, 15);
+    fill_combo<MaxOp, bf16_t, float>(t, 16);
+    fill_combo<SumOp, f16_t, float>(t, 17);
+    fill_combo<MinOp, f16_t, float>(t, 18);
+    fill_combo<MaxOp, f16_t, float>(t, 19);
     return t;
   }();
   return tb;
@@ -386,6 +416,8 @@ const Table& table() {
 //                       2.69 TB/s when the array was not already in the Infinity Cache
 //                       (profiles/r1_bench/plan_256mb.csv): non-nt loads are never the safe choice.
 //   128 MB              256 x  4, 3 WG/CU, nt   6.10 TB/s (best; launch + tail dominate)
+//   8 GB / 1 GB bf16 sum 256 x  4, 2 WG/CU, nt   7.18 / 7.01 TB/s (best at both; 256 x 2 x 3: 7.10 / 6.97);
+//   8 GB f16 max        512 x 4 x 1 7.18, 256 x 4 x 2 7.14 (profiles/r1_session3/tune_half.txt)
 // Fewer, fatter workgroups beat the "fill every wave slot" grid (8 WG/CU: 6.91 TB/s at 8 GB).
 struct Defaults {
   int block, unroll, wg_per_cu, policy, pipeline;
@@ -393,6 +425,7 @@ struct Defaults {
 Defaults tuned_defaults(size_t bytes, DType t) {
   constexpr size_t MB = 1ull << 20;
   if (t == DType::Float64 && bytes >= 3072 * MB) return {512, 16, 1, 1, 0};
+  if (dtype_is_half(t) && bytes > 192 * MB) return {256, 4, 2, 1, 0};
   if (bytes > 192 * MB) return {256, 2, 3, 1, 0};
   return {256, 4, 3, 1, 0};
 }
@@ -422,6 +455,7 @@ void finalize_by_acc(DType acc, const void* partials, uint64_t count, void* out,
     case DType::Int64: launch_finalize<OpT, int64_t>(partials, count, out, s); break;
     case DType::Float32: launch_finalize<OpT, float>(partials, count, out, s); break;
     case DType::Float64: launch_finalize<OpT, double>(partials, count, out, s); break;
+    default: MIREDUCE_REQUIRE(false, "finalize: accumulator must be int32, int64, float32 or float64");
   }
 }
 
@@ -442,6 +476,7 @@ void combine_by_type(DType t, void* inout, const void* other, uint64_t n, hipStr
     case DType::Int64: launch_combine<OpT, int64_t>(inout, other, n, s); break;
     case DType::Float32: launch_combine<OpT, float>(inout, other, n, s); break;
     case DType::Float64: launch_combine<OpT, double>(inout, other, n, s); break;
+    default: MIREDUCE_REQUIRE(false, "combine_elementwise: int32, int64, float32 or float64 only");
   }
 }
 

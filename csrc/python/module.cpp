@@ -81,6 +81,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("DTYPE_INT64") = static_cast<int>(DType::Int64);
   m.attr("DTYPE_FLOAT32") = static_cast<int>(DType::Float32);
   m.attr("DTYPE_FLOAT64") = static_cast<int>(DType::Float64);
+  m.attr("DTYPE_BFLOAT16") = static_cast<int>(DType::BFloat16);
+  m.attr("DTYPE_FLOAT16") = static_cast<int>(DType::Float16);
   m.attr("OP_SUM") = static_cast<int>(Op::Sum);
   m.attr("OP_MIN") = static_cast<int>(Op::Min);
   m.attr("OP_MAX") = static_cast<int>(Op::Max);

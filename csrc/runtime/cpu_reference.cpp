@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "mireduce/check.hpp"
+#include "mireduce/half.hpp"
 #include "mireduce/ops.hpp"
 
 namespace mireduce {
@@ -68,11 +69,17 @@ A reduce_parallel(const T* p, size_t n, int threads) {
 template <class OpT, class T>
 void dispatch_acc(const void* in, size_t n, DType acc, void* out, int threads) {
   const T* p = static_cast<const T*>(in);
-  switch (acc) {
-    case DType::Int32: { int32_t r = reduce_parallel<OpT, T, int32_t>(p, n, threads); std::memcpy(out, &r, 4); break; }
-    case DType::Int64: { int64_t r = reduce_parallel<OpT, T, int64_t>(p, n, threads); std::memcpy(out, &r, 8); break; }
-    case DType::Float32: { float r = reduce_parallel<OpT, T, float>(p, n, threads); std::memcpy(out, &r, 4); break; }
-    case DType::Float64: { double r = reduce_parallel<OpT, T, double>(p, n, threads); std::memcpy(out, &r, 8); break; }
+  if constexpr (is_half16_v<T>) {  // 16-bit floats accumulate in fp32 only (acc_supported)
+    float r = reduce_parallel<OpT, T, float>(p, n, threads);
+    std::memcpy(out, &r, 4);
+  } else {
+    switch (acc) {
+      case DType::Int32: { int32_t r = reduce_parallel<OpT, T, int32_t>(p, n, threads); std::memcpy(out, &r, 4); break; }
+      case DType::Int64: { int64_t r = reduce_parallel<OpT, T, int64_t>(p, n, threads); std::memcpy(out, &r, 8); break; }
+      case DType::Float32: { float r = reduce_parallel<OpT, T, float>(p, n, threads); std::memcpy(out, &r, 4); break; }
+      case DType::Float64: { double r = reduce_parallel<OpT, T, double>(p, n, threads); std::memcpy(out, &r, 8); break; }
+      default: MIREDUCE_REQUIRE(false, "accumulator must be int32, int64, float32 or float64");
+    }
   }
 }
 
@@ -83,6 +90,8 @@ void dispatch_t(const void* in, size_t n, DType t, DType acc, void* out, int thr
     case DType::Int64: dispatch_acc<OpT, int64_t>(in, n, acc, out, threads); break;
     case DType::Float32: dispatch_acc<OpT, float>(in, n, acc, out, threads); break;
     case DType::Float64: dispatch_acc<OpT, double>(in, n, acc, out, threads); break;
+    case DType::BFloat16: dispatch_acc<OpT, bf16_t>(in, n, acc, out, threads); break;
+    case DType::Float16: dispatch_acc<OpT, f16_t>(in, n, acc, out, threads); break;
   }
 }
 
@@ -128,6 +137,8 @@ double cpu_abs_sum(const void* in, size_t n, DType t, int threads) {
     case DType::Int64: return abs_sum_t<int64_t>(in, n, threads);
     case DType::Float32: return abs_sum_t<float>(in, n, threads);
     case DType::Float64: return abs_sum_t<double>(in, n, threads);
+    case DType::BFloat16: return abs_sum_t<bf16_t>(in, n, threads);
+    case DType::Float16: return abs_sum_t<f16_t>(in, n, threads);
   }
   return 0.0;
 }
@@ -154,6 +165,8 @@ double acc_as_double(const void* p, DType acc) {
     case DType::Int64: { int64_t v; std::memcpy(&v, p, 8); return static_cast<double>(v); }
     case DType::Float32: { float v; std::memcpy(&v, p, 4); return v; }
     case DType::Float64: { double v; std::memcpy(&v, p, 8); return v; }
+    case DType::BFloat16: { bf16_t v; std::memcpy(&v, p, 2); return static_cast<float>(v); }
+    case DType::Float16: { f16_t v; std::memcpy(&v, p, 2); return static_cast<float>(v); }
   }
   return 0.0;
 }
@@ -164,6 +177,8 @@ int64_t acc_as_int64(const void* p, DType acc) {
     case DType::Int64: { int64_t v; std::memcpy(&v, p, 8); return v; }
     case DType::Float32: { float v; std::memcpy(&v, p, 4); return static_cast<int64_t>(v); }
     case DType::Float64: { double v; std::memcpy(&v, p, 8); return static_cast<int64_t>(v); }
+    case DType::BFloat16:
+    case DType::Float16: return static_cast<int64_t>(acc_as_double(p, acc));
   }
   return 0;
 }

@@ -14,6 +14,8 @@ bool parse_dtype(const std::string& s, DType* out) {
   if (!strcasecmp(c, "int64") || !strcasecmp(c, "long") || !strcasecmp(c, "i64")) { *out = DType::Int64; return true; }
   if (!strcasecmp(c, "float") || !strcasecmp(c, "float32") || !strcasecmp(c, "fp32") || !strcasecmp(c, "f32")) { *out = DType::Float32; return true; }
   if (!strcasecmp(c, "double") || !strcasecmp(c, "float64") || !strcasecmp(c, "fp64") || !strcasecmp(c, "f64")) { *out = DType::Float64; return true; }
+  if (!strcasecmp(c, "bf16") || !strcasecmp(c, "bfloat16")) { *out = DType::BFloat16; return true; }
+  if (!strcasecmp(c, "half") || !strcasecmp(c, "float16") || !strcasecmp(c, "fp16") || !strcasecmp(c, "f16")) { *out = DType::Float16; return true; }
   return false;
 }
 

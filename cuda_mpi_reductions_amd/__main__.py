@@ -19,7 +19,8 @@ from .utils import cli
 from .utils.formats import throughput_line
 
 _TYPES = {"int": "int32", "int32": "int32", "int64": "int64", "long": "int64", "float": "float32",
-          "float32": "float32", "double": "float64", "float64": "float64"}
+          "float32": "float32", "double": "float64", "float64": "float64", "bf16": "bfloat16",
+          "bfloat16": "bfloat16", "half": "float16", "fp16": "float16", "float16": "float16"}
 
 
 def _qa(argv, status=None):
@@ -53,7 +54,7 @@ def main(argv=None) -> int:
     import torch
 
     from .ops import KernelConfig, Reducer, fill_
-    from .ops.reduce import default_acc_dtype
+    from .ops.reduce import default_acc_dtype, sum_tolerance
     tname = (cli.get_str(args, "type") or "int").lower()
     dt = getattr(torch, _TYPES.get(tname, "int32"))
     op = method.lower()
@@ -93,7 +94,8 @@ def main(argv=None) -> int:
         ref = x.sum(dtype=torch.float64 if acc.is_floating_point else torch.int64).item()
         if acc == torch.int32:
             ref = (int(ref) + 2 ** 31) % 2 ** 32 - 2 ** 31
-        ok = abs(got - ref) <= (1e-9 * max(1.0, abs(ref)) if acc.is_floating_point else 0)
+        tol = sum_tolerance(dt, acc, n, x.abs().sum(dtype=torch.float64).item()) if acc.is_floating_point else 0
+        ok = abs(got - ref) <= tol
     else:
         ref = (x.min() if op == "min" else x.max()).item()
         ok = got == ref

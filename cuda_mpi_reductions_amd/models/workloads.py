@@ -68,6 +68,10 @@ CONFIGS: dict[str, WorkloadConfig] = {
         baseline=92.7729, baseline_source="mpi/CUdata.txt:2 (CUDA DOUBLE SUM, best reference GB/s)",
         description="1B double sum across N MI355X: local HIP reduce + RCCL all-reduce over xGMI",
     ),
+    "gpu_4g_bf16_sum": WorkloadConfig(
+        name="gpu_4g_bf16_sum", dtype=torch.bfloat16, op="sum", n_total=4_000_000_000,
+        description="4e9 bfloat16 (8 GB) sum, fp32 accumulation (MI355X addition; not a reference config)",
+    ),
     "hbm_fill_fp32_sum": WorkloadConfig(
         name="hbm_fill_fp32_sum", dtype=torch.float32, op="sum", n_total=None,
         description="fp32 sum with each GPU's shard sized to fill its 288 GB HBM (HBM saturation)",

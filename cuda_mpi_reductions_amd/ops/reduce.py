@@ -32,7 +32,8 @@ __all__ = [
     "ladder_reduce",
 ]
 
-DTYPE_CODES = {torch.int32: 0, torch.int64: 1, torch.float32: 2, torch.float64: 3}
+DTYPE_CODES = {torch.int32: 0, torch.int64: 1, torch.float32: 2, torch.float64: 3,
+               torch.bfloat16: 4, torch.float16: 5}
 CODE_DTYPES = {v: k for k, v in DTYPE_CODES.items()}
 OP_CODES = {"sum": 0, "min": 1, "max": 2}
 
@@ -41,7 +42,8 @@ def dtype_code(dt: torch.dtype) -> int:
     try:
         return DTYPE_CODES[dt]
     except KeyError:
-        raise TypeError(f"unsupported dtype {dt}; supported: int32, int64, float32, float64") from None
+        raise TypeError(f"unsupported dtype {dt}; supported: int32, int64, float32, float64, "
+                        "bfloat16, float16") from None
 
 
 def op_code(op: str) -> int:
@@ -52,7 +54,8 @@ def op_code(op: str) -> int:
 
 
 def default_acc_dtype(dt: torch.dtype, op: str) -> torch.dtype:
-    """int32 SUM -> int64, float32 SUM -> float64, everything else keeps its dtype."""
+    """int32 SUM -> int64, float32 SUM -> float64, bfloat16/float16 -> float32 (every op), everything
+    else keeps its dtype."""
     return CODE_DTYPES[native().default_acc(dtype_code(dt), op_code(op))]
 
 

@@ -1,24 +1,33 @@
-# gnuplot twin of tools/plot.py (the reference's mpi/makePlots.gp:1-40 layout): results/*.txt
-# from tools/getAvgs.sh, x = column 3 (ranks), y = column 4 (GB/sec). Reference CUDA constants
-# from mpi/CUdata.txt are drawn as dashed lines.
-set term postscript eps enhanced color
-set style line 1 lt 1 lw 3 lc rgb "red" pt 2
-set style line 2 lt 1 lw 3 lc rgb "blue" pt 2
-set style line 3 lt 1 lw 3 lc rgb "green" pt 2
-set style line 4 lt 2 lw 5 lc rgb "red"
-set style line 5 lt 2 lw 5 lc rgb "blue"
-set style line 6 lt 2 lw 5 lc rgb "green"
-set xlabel "Number of ranks (GPUs)"
-set ylabel "Bandwidth (GB/sec)"
-set key bottom right
-set logscale y
-set output "int.eps"
-plot "results/INT_MAX.txt" using 3:4 ls 1 title "MI355X Max" with linespoints, \
-     "results/INT_MIN.txt" using 3:4 ls 2 title "MI355X Min" with linespoints, \
-     "results/INT_SUM.txt" using 3:4 ls 3 title "MI355X Sum" with linespoints, \
-     90.8413 ls 4 title "ref CUDA Sum", 90.7905 ls 5 title "ref CUDA Min", 90.7969 ls 6 title "ref CUDA Max"
-set output "double.eps"
-plot "results/DOUBLE_MAX.txt" using 3:4 ls 1 title "MI355X Max" with linespoints, \
-     "results/DOUBLE_MIN.txt" using 3:4 ls 2 title "MI355X Min" with linespoints, \
-     "results/DOUBLE_SUM.txt" using 3:4 ls 3 title "MI355X Sum" with linespoints, \
-     92.7729 ls 4 title "ref CUDA Sum", 92.6014 ls 5 title "ref CUDA Min", 92.7552 ls 6 title "ref CUDA Max"
+# Scaling plots from tools/getAvgs.sh output (gnuplot >= 5; tools/plot.py is the matplotlib
+# equivalent and the one the tests run — gnuplot is not installed in the build image).
+#
+# Data contract (same columns the reference's mpi/makePlots.gp:21-23 reads): results/<DT>_<OP>.txt,
+# column 3 = ranks (GPUs), column 4 = GB/sec. The reference's single-GPU CUDA numbers
+# (mpi/CUdata.txt:2-8) are drawn as horizontal reference levels.
+#
+#   gnuplot tools/makePlots.gp            -> int.eps, double.eps in the current directory
+
+set terminal postscript eps enhanced color font "Helvetica,14" size 6in,4in
+set grid ytics lc rgb "#dddddd"
+set logscale xy 2
+set format y "%g"
+set xlabel "GPUs (one rank each)"
+set ylabel "GB/s (whole job)"
+set key outside right top box
+
+ops = "MAX MIN SUM"
+colours = "#d62728 #1f77b4 #2ca02c"
+
+# reference CUDA levels per dtype, in op order SUM MIN MAX (mpi/CUdata.txt)
+ref_INT = "90.8413 90.7905 90.7969"
+ref_DOUBLE = "92.7729 92.6014 92.7552"
+
+do for [dt in "INT DOUBLE"] {
+    set output sprintf("%s.eps", dt eq "INT" ? "int" : "double")
+    set title sprintf("%s reductions on MI355X vs the reference's CUDA GPU", dt)
+    levels = dt eq "INT" ? ref_INT : ref_DOUBLE
+    plot for [i=1:3] sprintf("results/%s_%s.txt", dt, word(ops, i)) using 3:4 \
+             with linespoints lw 2 pt 7 lc rgb word(colours, i) title sprintf("MI355X %s", word(ops, i)), \
+         for [j=1:3] (real(word(levels, j))) with lines dt 3 lw 2 lc rgb "#555555" \
+             title sprintf("reference CUDA %s", word("SUM MIN MAX", j))
+}

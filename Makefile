@@ -44,8 +44,8 @@ COMMLIB     := $(BUILD)/lib/libmireduce_comm.a
 APPS := $(BUILD)/bin/reduction $(BUILD)/bin/reduce_xgmi $(BUILD)/bin/bandwidth_test
 MPI_APP := $(BUILD)/bin/reduce_mpi
 
-.PHONY: all python apps mpi clean asan unit diag
-all: python apps mpi unit diag
+.PHONY: all python apps mpi clean asan unit diag examples
+all: python apps mpi unit diag examples
 
 python: $(PYEXT)
 apps: $(APPS)
@@ -97,6 +97,12 @@ diag: $(BUILD)/bin/wg_timeline
 $(BUILD)/bin/wg_timeline: tools/wg_timeline.hip
 	@mkdir -p $(dir $@)
 	$(HIPCC) -std=c++17 -O3 --offload-arch=$(ARCH) $< -o $@
+
+# C++ library consumer example (examples/cpp_consumer; the CMake build links it via find_package).
+examples: $(BUILD)/bin/cpp_consumer
+$(BUILD)/bin/cpp_consumer: examples/cpp_consumer/main.cpp $(LIB) $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HOSTCXX) $(HOSTFLAGS) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive $(LDLIBS) -o $@
 
 # Native unit tests (host code only) and the bootstrap multi-process test.
 UNIT := $(BUILD)/bin/host_unit $(BUILD)/bin/bootstrap_test

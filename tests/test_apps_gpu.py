@@ -90,6 +90,13 @@ def test_bandwidth_test_app():
     assert "Device to Device copy" in r.stdout and "Read stream" in r.stdout
 
 
+def test_cpp_consumer_example():
+    """examples/cpp_consumer: a plain C++ program linked against libmireduce (closed-form sum)."""
+    r = run([os.path.join(BIN, "cpp_consumer")], timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "expected" in r.stdout
+
+
 # ---------------------------------------------------------------------------------------------
 # Multi-rank paths rehearsed on the 1-GPU box (every rank on GPU 0).
 from helpers import ROOT, torchrun  # noqa: E402

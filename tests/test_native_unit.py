@@ -152,3 +152,18 @@ def test_plot_shmoo_tool(tmp_path):
     r = run(["python", os.path.join(ROOT, "tools", "plot_shmoo.py"), csv, "-o", str(out), "--title", "t"], timeout=300)
     assert r.returncode == 0, r.stderr
     assert out.exists() and out.stat().st_size > 1000
+
+
+def test_cmake_build_and_ctest(tmp_path):
+    """The CMake build configures, builds the CPU-only targets and passes
+    their ctest entries (the HIP targets are the Makefile's, built by ensure_built)."""
+    b = tmp_path / "cmake"
+    r = run(["cmake", "-S", ROOT, "-B", str(b), "-G", "Ninja", "-DMIREDUCE_ASAN=ON"], timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    targets = ["host_unit"] + (["reduce_mpi"] if os.path.exists(MPIRUN) else [])
+    r = run(["cmake", "--build", str(b), "-j4", "--target"] + targets, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    r = run(["ctest", "--test-dir", str(b), "-R", "host_unit|reduce_mpi", "--output-on-failure"], timeout=300,
+            env={"ASAN_OPTIONS": "detect_leaks=1"})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert "tests passed" in r.stdout

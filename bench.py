@@ -231,7 +231,7 @@ def main(argv=None) -> int:
     ms = elapsed / K * 1e3
     if ctx.is_root:
         line = {
-            "metric": METRIC,
+            "metric": METRIC if cfg.name == NORTH_STAR else f"reduction bandwidth (GB/s), {cfg.name}",
             "value": round(gbps, 3),
             "unit": "GB/s",
             "n_gpus": ctx.world_size,

@@ -12,8 +12,10 @@
 #include <cstdint>
 
 #include "mireduce/check.hpp"
+#include "mireduce/half.hpp"
 #include "mireduce/moments.hpp"
 #include "mireduce/ops.hpp"
+#include "mireduce/vec16.hpp"
 
 namespace mireduce {
 namespace kern {
@@ -46,10 +48,15 @@ __device__ __forceinline__ Mom block_mom(Mom v, Mom* lds) {
   return v;
 }
 
+template <class T>
+__device__ __forceinline__ double first_value(const void* p) {
+  return static_cast<double>(*static_cast<const T*>(p));
+}
+
 template <class T, int BLOCK, int UNROLL>
 __global__ __launch_bounds__(BLOCK) void moments_stream(const T* __restrict__ in, uint64_t n, Mom* __restrict__ partials) {
-  constexpr int N = 16 / sizeof(T);
-  using V = T __attribute__((ext_vector_type(N)));
+  using V = typename Vec16<T>::type;
+  constexpr int N = Vec16<T>::N;
   __shared__ Mom lds[BLOCK / 64];
   const double K = n ? static_cast<double>(in[0]) : 0.0;
   double s[UNROLL], q[UNROLL], mn[UNROLL], mx[UNROLL];
@@ -73,7 +80,7 @@ __global__ __launch_bounds__(BLOCK) void moments_stream(const T* __restrict__ in
     for (int u = 0; u < UNROLL; ++u) {
 #pragma unroll
       for (int k = 0; k < N; ++k) {
-        const double x = static_cast<double>(v[u][k]);
+        const double x = elem<T, double>(v[u], k);
         const double d = x - K;
         s[u] += d;
         q[u] = __builtin_fma(d, d, q[u]);
@@ -88,7 +95,7 @@ __global__ __launch_bounds__(BLOCK) void moments_stream(const T* __restrict__ in
     const V v = vin[i];
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-      const double x = static_cast<double>(v[k]);
+      const double x = elem<T, double>(v, k);
       const double d = x - K;
       s[0] += d;
       q[0] = __builtin_fma(d, d, q[0]);
@@ -111,8 +118,9 @@ __global__ __launch_bounds__(BLOCK) void moments_stream(const T* __restrict__ in
   if (threadIdx.x == 0) partials[blockIdx.x] = m;
 }
 
+template <class T>
 __global__ __launch_bounds__(256) void moments_finalize(const Mom* __restrict__ partials, int count,
-                                                        const void* __restrict__ first, int is_f64, uint64_t n,
+                                                        const void* __restrict__ first, uint64_t n,
                                                         double* __restrict__ out) {
   __shared__ Mom lds[4];
   Mom m{0.0, 0.0, MinOp::identity<double>(), MaxOp::identity<double>()};
@@ -120,7 +128,7 @@ __global__ __launch_bounds__(256) void moments_finalize(const Mom* __restrict__ 
   m = block_mom<256>(m, lds);
   if (threadIdx.x == 0) {
     double K = 0.0;
-    if (n) K = is_f64 ? *static_cast<const double*>(first) : static_cast<double>(*static_cast<const float*>(first));
+    if (n) K = first_value<T>(first);
     out[0] = K;
     out[1] = m.s;
     out[2] = m.q;
@@ -131,26 +139,34 @@ __global__ __launch_bounds__(256) void moments_finalize(const Mom* __restrict__ 
 
 }  // namespace kern
 
-void moments_device(const void* in, size_t n, DType t, double* out5, void* partials, int max_grid, int num_cus,
-                    hipStream_t stream) {
-  MIREDUCE_REQUIRE(t == DType::Float32 || t == DType::Float64, "moments: float32 or float64 input");
-  MIREDUCE_REQUIRE(reinterpret_cast<uintptr_t>(in) % 16 == 0, "moments: input must be 16-byte aligned");
+namespace {
+template <class T>
+void launch_moments(const void* in, size_t n, double* out5, kern::Mom* p, int max_grid, int num_cus, hipStream_t stream) {
   constexpr int kBlock = 256, kUnroll = 4;
-  const size_t vec = 16 / dtype_size(t);
+  constexpr size_t vec = kern::Vec16<T>::N;
   const uint64_t tiles = (n / vec + kBlock * kUnroll - 1) / (kBlock * kUnroll);
   int grid = static_cast<int>(std::min<uint64_t>(std::max<uint64_t>(tiles, 1), static_cast<uint64_t>(num_cus) * 3));
   grid = std::min(grid, max_grid);
+  hipLaunchKernelGGL((kern::moments_stream<T, kBlock, kUnroll>), dim3(grid), dim3(kBlock), 0, stream,
+                     static_cast<const T*>(in), static_cast<uint64_t>(n), p);
+  MIREDUCE_HIP_THROW(hipGetLastError());
+  hipLaunchKernelGGL(kern::moments_finalize<T>, dim3(1), dim3(256), 0, stream, p, grid, in, static_cast<uint64_t>(n), out5);
+  MIREDUCE_HIP_THROW(hipGetLastError());
+}
+}  // namespace
+
+void moments_device(const void* in, size_t n, DType t, double* out5, void* partials, int max_grid, int num_cus,
+                    hipStream_t stream) {
+  MIREDUCE_REQUIRE(dtype_is_float(t), "moments: float32, float64, bfloat16 or float16 input");
+  MIREDUCE_REQUIRE(reinterpret_cast<uintptr_t>(in) % 16 == 0, "moments: input must be 16-byte aligned");
   auto* p = static_cast<kern::Mom*>(partials);
-  if (t == DType::Float64)
-    hipLaunchKernelGGL((kern::moments_stream<double, kBlock, kUnroll>), dim3(grid), dim3(kBlock), 0, stream,
-                       static_cast<const double*>(in), static_cast<uint64_t>(n), p);
-  else
-    hipLaunchKernelGGL((kern::moments_stream<float, kBlock, kUnroll>), dim3(grid), dim3(kBlock), 0, stream,
-                       static_cast<const float*>(in), static_cast<uint64_t>(n), p);
-  MIREDUCE_HIP_THROW(hipGetLastError());
-  hipLaunchKernelGGL(kern::moments_finalize, dim3(1), dim3(256), 0, stream, p, grid, in, t == DType::Float64 ? 1 : 0,
-                     static_cast<uint64_t>(n), out5);
-  MIREDUCE_HIP_THROW(hipGetLastError());
+  switch (t) {
+    case DType::Float64: launch_moments<double>(in, n, out5, p, max_grid, num_cus, stream); break;
+    case DType::Float32: launch_moments<float>(in, n, out5, p, max_grid, num_cus, stream); break;
+    case DType::BFloat16: launch_moments<bf16_t>(in, n, out5, p, max_grid, num_cus, stream); break;
+    case DType::Float16: launch_moments<f16_t>(in, n, out5, p, max_grid, num_cus, stream); break;
+    default: break;
+  }
 }
 
 size_t moments_partials_bytes(int max_grid) { return static_cast<size_t>(max_grid) * sizeof(kern::Mom); }

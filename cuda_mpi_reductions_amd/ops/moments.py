@@ -1,4 +1,5 @@
-"""Fused one-pass statistics: count, sum, mean, variance, std, min, max of a float tensor.
+"""Fused one-pass statistics: count, sum, mean, variance, std, min, max of a float tensor
+(fp32 / fp64 / bf16 / fp16 storage; all statistics are computed in fp64).
 
 Device tensors: one streaming HIP pass (csrc/kernels/moments.hip) computing Σ(x-K), Σ(x-K)²,
 min and max with K = x[0] (shifted-data variance), then a one-workgroup fold. Pattern reference:
@@ -60,8 +61,8 @@ def combine_moments(a, b):
 
 
 def moments(x: torch.Tensor, group=None, ddof: int = 0) -> dict:
-    if x.dtype not in (torch.float32, torch.float64):
-        raise TypeError("moments: float32 or float64 input")
+    if x.dtype not in (torch.float32, torch.float64, torch.bfloat16, torch.float16):
+        raise TypeError("moments: float32, float64, bfloat16 or float16 input")
     x = x.contiguous().reshape(-1)
     r = _raw(x)
     if group is not None or (torch.distributed.is_initialized() and torch.distributed.get_world_size() > 1):

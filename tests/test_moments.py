@@ -45,7 +45,7 @@ def test_rejects_ints():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("n", [1, 3, 63, 65, 4097, 1_000_003, (1 << 24) + 5])
 def test_device_moments(dt, n):
     x = torch.empty(n, dtype=dt, device="cuda")

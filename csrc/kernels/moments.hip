@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <type_traits>
 
 #include "mireduce/check.hpp"
 #include "mireduce/half.hpp"
@@ -53,19 +54,33 @@ __device__ __forceinline__ double first_value(const void* p) {
   return static_cast<double>(*static_cast<const T*>(p));
 }
 
+// One element: shifted Σ and Σ² in fp64; MIN/MAX in the narrowest exact type E (fp32 for fp32 /
+// bf16 / f16 storage, which halves the fp64 VALU work per element: 6.4-6.7 TB/s -> see
+// profiles/r1_session3/moments_bw.jsonl), widened to fp64 only when the partials are combined.
+template <class E>
+__device__ __forceinline__ void mom_step(E x, double K, double& s, double& q, E& mn, E& mx) {
+  const double d = static_cast<double>(x) - K;
+  s += d;
+  q = __builtin_fma(d, d, q);
+  mn = MinOp::apply(mn, x);
+  mx = MaxOp::apply(mx, x);
+}
+
 template <class T, int BLOCK, int UNROLL>
 __global__ __launch_bounds__(BLOCK) void moments_stream(const T* __restrict__ in, uint64_t n, Mom* __restrict__ partials) {
   using V = typename Vec16<T>::type;
+  using E = std::conditional_t<std::is_same_v<T, double>, double, float>;
   constexpr int N = Vec16<T>::N;
   __shared__ Mom lds[BLOCK / 64];
   const double K = n ? static_cast<double>(in[0]) : 0.0;
-  double s[UNROLL], q[UNROLL], mn[UNROLL], mx[UNROLL];
+  double s[UNROLL], q[UNROLL];
+  E mn[UNROLL], mx[UNROLL];
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
     s[u] = 0.0;
     q[u] = 0.0;
-    mn[u] = MinOp::identity<double>();
-    mx[u] = MaxOp::identity<double>();
+    mn[u] = MinOp::identity<E>();
+    mx[u] = MaxOp::identity<E>();
   }
   const uint64_t nvec = n / N;
   const V* vin = reinterpret_cast<const V*>(in);
@@ -79,14 +94,7 @@ __global__ __launch_bounds__(BLOCK) void moments_stream(const T* __restrict__ in
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
 #pragma unroll
-      for (int k = 0; k < N; ++k) {
-        const double x = elem<T, double>(v[u], k);
-        const double d = x - K;
-        s[u] += d;
-        q[u] = __builtin_fma(d, d, q[u]);
-        mn[u] = MinOp::apply(mn[u], x);
-        mx[u] = MaxOp::apply(mx[u], x);
-      }
+      for (int k = 0; k < N; ++k) mom_step<E>(elem<T, E>(v[u], k), K, s[u], q[u], mn[u], mx[u]);
     }
   }
   // remaining vectors, then the < N scalar tail (input is 16-byte aligned: checked on the host)
@@ -94,26 +102,14 @@ __global__ __launch_bounds__(BLOCK) void moments_stream(const T* __restrict__ in
   for (uint64_t i = ntiles * kTile + static_cast<uint64_t>(blockIdx.x) * BLOCK + threadIdx.x; i < nvec; i += stride) {
     const V v = vin[i];
 #pragma unroll
-    for (int k = 0; k < N; ++k) {
-      const double x = elem<T, double>(v, k);
-      const double d = x - K;
-      s[0] += d;
-      q[0] = __builtin_fma(d, d, q[0]);
-      mn[0] = MinOp::apply(mn[0], x);
-      mx[0] = MaxOp::apply(mx[0], x);
-    }
+    for (int k = 0; k < N; ++k) mom_step<E>(elem<T, E>(v, k), K, s[0], q[0], mn[0], mx[0]);
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x < n - nvec * N) {
-    const double x = static_cast<double>(in[nvec * N + threadIdx.x]);
-    const double d = x - K;
-    s[0] += d;
-    q[0] = __builtin_fma(d, d, q[0]);
-    mn[0] = MinOp::apply(mn[0], x);
-    mx[0] = MaxOp::apply(mx[0], x);
-  }
-  Mom m{s[0], q[0], mn[0], mx[0]};
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x < n - nvec * N)
+    mom_step<E>(static_cast<E>(in[nvec * N + threadIdx.x]), K, s[0], q[0], mn[0], mx[0]);
+  Mom m{s[0], q[0], static_cast<double>(mn[0]), static_cast<double>(mx[0])};
 #pragma unroll
-  for (int u = 1; u < UNROLL; ++u) m = mom_combine(m, Mom{s[u], q[u], mn[u], mx[u]});
+  for (int u = 1; u < UNROLL; ++u)
+    m = mom_combine(m, Mom{s[u], q[u], static_cast<double>(mn[u]), static_cast<double>(mx[u])});
   m = block_mom<BLOCK>(m, lds);
   if (threadIdx.x == 0) partials[blockIdx.x] = m;
 }

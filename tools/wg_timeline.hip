@@ -48,6 +48,7 @@ struct TArgs {
   uint64_t chunk;            // dynamic: tiles per big chunk
   uint64_t nchunks;          // dynamic: big chunks + single-tile chunks
   uint64_t* stamps;          // [grid * 4] start, end, xcc, tiles (nullptr: no stamps)
+  unsigned long long* qctr;  // tail-steal: 8 queue counters, 16 words apart (zeroed by fold)
 };
 
 __device__ __forceinline__ uint64_t now_rt() {
@@ -130,6 +131,33 @@ __global__ __launch_bounds__(BLOCK) void body(TArgs a) {
       consume<UNROLL>(acc, cur);
       ++done;
     }
+  } else if constexpr (!DYN && MODE == 4) {
+    // static grid-stride over the first a.nbig tiles, then the tail [a.nbig, ntiles) as 8 queues
+    // of a.nchunks granules (a.chunk tiles each); a workgroup drains its own XCD's queue first,
+    // then the others. A plain sc1 read skips exhausted queues without an atomic.
+    __shared__ unsigned long long grab[2];
+    for (uint64_t t = blockIdx.x; t < a.nbig; t += gridDim.x, ++done) tile<BLOCK, UNROLL, 0>(acc, a.v + t * kTile + threadIdx.x);
+    const unsigned x = xcc_id();
+    int slot = 0;
+    for (unsigned j = 0; j < 8; ++j) {
+      const unsigned q = (x + j) & 7u;
+      unsigned long long* c = a.qctr + 16 * q;
+      while (true) {
+        if (threadIdx.x == 0) {
+          unsigned long long g = a.nchunks;
+          if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.nchunks)
+            g = __hip_atomic_fetch_add(c, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          grab[slot] = g;
+        }
+        __syncthreads();
+        const unsigned long long g = grab[slot];
+        slot ^= 1;
+        if (g >= a.nchunks) break;
+        const uint64_t first = a.nbig + (q * a.nchunks + g) * a.chunk;
+        const uint64_t last = first + a.chunk < ntiles ? first + a.chunk : ntiles;
+        for (uint64_t t = first; t < last; ++t, ++done) tile<BLOCK, UNROLL, 0>(acc, a.v + t * kTile + threadIdx.x);
+      }
+    }
   } else if constexpr (!DYN && MODE == 3) {
     // static, but in runs of a.chunk consecutive tiles (the dynamic variant's access window)
     const uint64_t runs = ntiles / a.chunk;
@@ -184,7 +212,8 @@ __global__ __launch_bounds__(BLOCK) void body(TArgs a) {
   if (threadIdx.x == 0) a.partials[blockIdx.x] = s;
 }
 
-__global__ void fold(const double* p, int n, double* out) {
+__global__ void fold(const double* p, int n, double* out, unsigned long long* qctr) {
+  if (threadIdx.x < 8) qctr[16 * threadIdx.x] = 0;  // tail-steal queues: ready for the next launch
   __shared__ double lds[4];
   double s = 0.0;
   for (int i = threadIdx.x; i < n; i += 256) s += p[i];
@@ -237,12 +266,14 @@ int main(int argc, char** argv) {
   const uint64_t nvec = n / 2;
   V* v;
   double *partials, *out;
-  unsigned long long* ctr;
+  unsigned long long *ctr, *qctr;
   uint64_t* stamps;
   CK(hipMalloc(&v, nvec * sizeof(V)));
   CK(hipMalloc(&partials, 8192 * sizeof(double)));
   CK(hipMalloc(&out, sizeof(double)));
   CK(hipMalloc(&ctr, sizeof(unsigned long long)));
+  CK(hipMalloc(&qctr, 8 * 16 * sizeof(unsigned long long)));
+  CK(hipMemset(qctr, 0, 8 * 16 * sizeof(unsigned long long)));
   CK(hipMalloc(&stamps, 8192 * 4 * sizeof(uint64_t)));
   CK(hipMemset(ctr, 0, sizeof(unsigned long long)));
   fill<<<4096, 256>>>(v, nvec);
@@ -252,7 +283,19 @@ int main(int argc, char** argv) {
   // --set=mlp: how many loads the scheduler keeps in flight; --set=sched: static-chunked and
   // dynamic assignment (profiles/r1_session3/wg_timeline/).
   std::vector<Variant> vars;
-  if (set == "mlp") {
+  if (set == "steal") {
+    vars = {
+        mk<256, 2, false, 0>("s 256x2x3", 3),
+        mk<256, 2, false, 4>("steal 256x2x3 g4 t8", 3, 4, 8),
+        mk<256, 2, false, 4>("steal 256x2x3 g8 t8", 3, 8, 8),
+        mk<256, 2, false, 4>("steal 256x2x3 g2 t5", 3, 2, 5),
+        mk<256, 2, false, 4>("steal 256x2x3 g8 t15", 3, 8, 15),
+        mk<512, 16, false, 0>("s 512x16x1", 1),
+        mk<512, 16, false, 4>("steal 512x16x1 g1 t8", 1, 1, 8),
+        mk<256, 4, false, 0>("s 256x4x2", 2),
+        mk<256, 4, false, 4>("steal 256x4x2 g4 t8", 2, 4, 8),
+    };
+  } else if (set == "mlp") {
     vars = {
         mk<256, 2, false, 0>("s 256x2x3 compiler", 3),
         mk<512, 16, false, 0>("s 512x16x1 compiler", 1),
@@ -288,7 +331,14 @@ int main(int argc, char** argv) {
     const uint64_t tile = static_cast<uint64_t>(x.block) * x.unroll;
     const uint64_t ntiles = nvec / tile;
     uint64_t grid = std::min<uint64_t>(static_cast<uint64_t>(cus) * x.wpc, std::max<uint64_t>(ntiles, 1));
-    TArgs a{v, nvec, partials, ctr, counter, 0, 0, 0, st};
+    TArgs a{v, nvec, partials, ctr, counter, 0, 0, 0, st, qctr};
+    if (!x.dyn && x.tailpct > 0) {  // tail-steal: chunk = granule tiles, tail = tailpct % of tiles
+      const uint64_t tail = static_cast<uint64_t>(std::ceil(ntiles * x.tailpct / 100.0));
+      a.nbig = ntiles - std::min(tail, ntiles);
+      a.chunk = x.chunk;
+      const uint64_t granules = (ntiles - a.nbig + x.chunk - 1) / x.chunk;
+      a.nchunks = (granules + 7) / 8;
+    }
     if (!x.dyn && x.chunk) a.chunk = x.chunk;
     if (x.dyn) {
       const uint64_t tail = static_cast<uint64_t>(std::ceil(ntiles * x.tailpct / 100.0));
@@ -298,7 +348,7 @@ int main(int argc, char** argv) {
       counter += a.nchunks + grid;  // every workgroup draws exactly one index past the end
     }
     hipLaunchKernelGGL(x.kern, dim3(static_cast<unsigned>(grid)), dim3(x.block), 0, 0, a);
-    fold<<<1, 256>>>(partials, static_cast<int>(grid), out);
+    fold<<<1, 256>>>(partials, static_cast<int>(grid), out, qctr);
     return grid;
   };
   hipEvent_t e0, e1;

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstring>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "mireduce/check.hpp"
@@ -28,11 +29,18 @@ struct Compensated {
   A value() const { return sum + c; }
 };
 
+// Floating sums are compensated in fp64 whatever the accumulator type (per-thread partials stay
+// fp64 too) and rounded to it once at the end: a float-typed Neumaier sum saturates once its
+// compensation term stops absorbing the addends (4e9 bf16 values of ~6e-8 summed to 64.0 instead
+// of 237.5). W is the working type of a range: fp64 for floating sums, the accumulator otherwise.
+template <class OpT, class A>
+using Work = std::conditional_t<std::is_same_v<OpT, SumOp> && std::is_floating_point_v<A>, double, A>;
+
 template <class OpT, class T, class A>
-A reduce_range(const T* p, size_t n) {
+Work<OpT, A> reduce_range(const T* p, size_t n) {
   if constexpr (std::is_same_v<OpT, SumOp> && std::is_floating_point_v<A>) {
-    Compensated<A> k;
-    for (size_t i = 0; i < n; ++i) k.add(static_cast<A>(p[i]));
+    Compensated<double> k;
+    for (size_t i = 0; i < n; ++i) k.add(static_cast<double>(static_cast<A>(p[i])));
     return k.value();
   } else {
     A a = OpT::template identity<A>();
@@ -51,9 +59,10 @@ int pick_threads(size_t n, int threads) {
 
 template <class OpT, class T, class A>
 A reduce_parallel(const T* p, size_t n, int threads) {
+  using W = Work<OpT, A>;
   threads = pick_threads(n, threads);
-  if (threads <= 1) return reduce_range<OpT, T, A>(p, n);
-  std::vector<A> part(threads);
+  if (threads <= 1) return static_cast<A>(reduce_range<OpT, T, A>(p, n));
+  std::vector<W> part(threads);
   std::vector<std::thread> pool;
   const size_t chunk = (n + threads - 1) / threads;
   for (int t = 0; t < threads; ++t) {
@@ -63,7 +72,7 @@ A reduce_parallel(const T* p, size_t n, int threads) {
     });
   }
   for (auto& th : pool) th.join();
-  return reduce_range<OpT, A, A>(part.data(), part.size());
+  return static_cast<A>(reduce_range<OpT, W, W>(part.data(), part.size()));
 }
 
 template <class OpT, class T>

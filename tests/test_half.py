@@ -175,3 +175,13 @@ def test_gpu_reduction_app_half(ty):
         assert r.returncode == 0, r.stdout + r.stderr
         assert "&&&& PASSED" in r.stdout + r.stderr
         assert "GPU result" in r.stdout
+
+
+def test_host_reducer_does_not_saturate():
+    """fp32-accumulated host sums are compensated in fp64: a float-typed Neumaier sum of 40M ones
+    saturates (sum and compensation both stall at 2^24) — the bug that made a 4e9-element bf16 check
+    report 64.0 for a true 237.5."""
+    x = torch.ones(40_000_000, dtype=torch.bfloat16)
+    assert cpu_reduce(x, "sum", threads=1) == 40_000_000.0
+    y = torch.full((40_000_000,), 1.0, dtype=torch.float32)
+    assert cpu_reduce(y, "sum", torch.float32, threads=1) == 40_000_000.0

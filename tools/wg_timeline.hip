@@ -131,6 +131,20 @@ __global__ __launch_bounds__(BLOCK) void body(TArgs a) {
       consume<UNROLL>(acc, cur);
       ++done;
     }
+  } else if constexpr (!DYN && MODE == 5) {
+    // rotated grid-stride: in round k workgroup b takes tile k*grid + (b + k*a.chunk) % grid, so
+    // the tiles an XCD reads (b % 8 under round-robin dispatch) cycle through every address
+    // residue instead of always sitting at offset (b % 8) * tile within each 8-tile stripe.
+    const uint64_t g = gridDim.x;
+    for (uint64_t k = 0;; ++k) {
+      const uint64_t t = k * g + (blockIdx.x + k * a.chunk) % g;
+      if (t >= ntiles) {
+        if (k * g >= ntiles) break;
+        continue;
+      }
+      tile<BLOCK, UNROLL, 0>(acc, a.v + t * kTile + threadIdx.x);
+      ++done;
+    }
   } else if constexpr (!DYN && MODE == 4) {
     // static grid-stride over the first a.nbig tiles, then the tail [a.nbig, ntiles) as 8 queues
     // of a.nchunks granules (a.chunk tiles each); a workgroup drains its own XCD's queue first,
@@ -283,7 +297,18 @@ int main(int argc, char** argv) {
   // --set=mlp: how many loads the scheduler keeps in flight; --set=sched: static-chunked and
   // dynamic assignment (profiles/r1_session3/wg_timeline/).
   std::vector<Variant> vars;
-  if (set == "steal") {
+  if (set == "rotate") {
+    vars = {
+        mk<256, 2, false, 0>("s 256x2x3", 3),
+        mk<256, 2, false, 5>("rot1 256x2x3", 3, 1),
+        mk<256, 2, false, 5>("rot3 256x2x3", 3, 3),
+        mk<256, 2, false, 5>("rot8 256x2x3", 3, 8),
+        mk<512, 16, false, 0>("s 512x16x1", 1),
+        mk<512, 16, false, 5>("rot1 512x16x1", 1, 1),
+        mk<256, 4, false, 0>("s 256x4x2", 2),
+        mk<256, 4, false, 5>("rot1 256x4x2", 2, 1),
+    };
+  } else if (set == "steal") {
     vars = {
         mk<256, 2, false, 0>("s 256x2x3", 3),
         mk<256, 2, false, 4>("steal 256x2x3 g4 t8", 3, 4, 8),
@@ -339,7 +364,7 @@ int main(int argc, char** argv) {
       const uint64_t granules = (ntiles - a.nbig + x.chunk - 1) / x.chunk;
       a.nchunks = (granules + 7) / 8;
     }
-    if (!x.dyn && x.chunk) a.chunk = x.chunk;
+    if (!x.dyn && x.chunk) a.chunk = x.chunk;  // MODE 3: run length; MODE 5: rotation step
     if (x.dyn) {
       const uint64_t tail = static_cast<uint64_t>(std::ceil(ntiles * x.tailpct / 100.0));
       a.chunk = x.chunk;

@@ -67,6 +67,9 @@ def parse_args(argv=None):
                         "(steps count warm-up first; forces --launch eager)")
     p.add_argument("--pg-timeout", type=float, default=600.0, help="process-group collective timeout (s)")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--compare-torch", action="store_true",
+                   help="after the measurement, time torch's own reduction of the same shard (reported as "
+                        "torch_gbps; not part of the metric)")
     p.add_argument("--trace", action="store_true", help="roctx range per step (rocprofv3 --marker-trace)")
     p.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
                    help="auto: nccl (RCCL) on GPUs, gloo on CPU; gloo + MIREDUCE_FORCE_DEVICE=0 rehearses "
@@ -79,6 +82,35 @@ def parse_args(argv=None):
 def _sync(dev: torch.device) -> None:
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
+
+
+def _time_torch_reduction(wl, K: int, W: int, ctx) -> float:
+    """Whole-job GB/s of the same step done with PyTorch's reduction (x.sum / amin / amax on each
+    shard, then the same scalar all-reduce) — a vendor-library reference point for the native
+    kernel, measured the same way (W warm-up steps, K timed, MAX over ranks)."""
+    x, op = wl.x, wl.cfg.op
+    acc = wl.acc
+
+    def step():
+        if op == "sum":
+            r = x.sum(dtype=acc).reshape(1)
+        else:
+            r = (x.amin() if op == "min" else x.amax()).to(acc).reshape(1)
+        if ctx.world_size > 1:
+            pdist.scalar_allreduce(r, op)
+        return r
+
+    for _ in range(W):
+        step()
+    _sync(ctx.device)
+    pdist.barrier(ctx)
+    _sync(ctx.device)
+    t0 = time.perf_counter()
+    for _ in range(K):
+        step()
+    _sync(ctx.device)
+    el = pdist.max_over_ranks(time.perf_counter() - t0, ctx)
+    return wl.bytes_total * K / el / 1e9
 
 
 def run_vector(args, ctx, cfg, fault) -> int:
@@ -226,6 +258,9 @@ def main(argv=None) -> int:
         if not ok and ctx.is_root:
             print(f"[bench] VERIFICATION FAILED: {ref}", file=sys.stderr)
 
+    torch_gbps = None
+    if args.compare_torch and dev.type == "cuda":
+        torch_gbps = _time_torch_reduction(wl, K, W, ctx)
     bytes_step = wl.bytes_total
     gbps = bytes_step * K / elapsed / 1e9
     ms = elapsed / K * 1e3
@@ -264,6 +299,8 @@ def main(argv=None) -> int:
             "verified": verified,
             "native_ext": os.path.basename(native_path()),
         }
+        if torch_gbps is not None:
+            line["torch_gbps"] = round(torch_gbps, 3)  # same data, torch's own reduction kernels
         print(json.dumps(line), flush=True)
     if sg is not None:
         sg.reset()  # captured RCCL work must not outlive the communicator

@@ -2,7 +2,8 @@
 //
 // Every element type is read 16 bytes per lane — one global_load_dwordx4 — whatever its width:
 // int32x4, int64x2, float4, double2, or eight bf16/f16 carried as four 32-bit words. elem() returns
-// element k of such a vector in the accumulator type.
+// element k of such a vector in the accumulator type. store_sc1 / load_sc1 are the write-through /
+// L1-bypassing accesses the single-pass finalisations publish and read partials with.
 #pragma once
 
 #include <cstdint>
@@ -36,6 +37,28 @@ __device__ __forceinline__ AccT elem(const V& v, int k) {
   } else {
     return static_cast<AccT>(v[k]);
   }
+}
+
+
+template <class T> struct Bits { using type = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>; };
+
+// Write-through (sc1) store / L1-bypassing (sc1) load of one accumulator value: the
+// agent-scope relaxed atomic forms lower to global_store/load ... sc1 on gfx950.
+template <class T>
+__device__ __forceinline__ void store_sc1(T* p, T v) {
+  using B = typename Bits<T>::type;
+  B b;
+  __builtin_memcpy(&b, &v, sizeof(T));
+  __hip_atomic_store(reinterpret_cast<B*>(p), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <class T>
+__device__ __forceinline__ T load_sc1(const T* p) {
+  using B = typename Bits<T>::type;
+  B b = __hip_atomic_load(reinterpret_cast<const B*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  T v;
+  __builtin_memcpy(&v, &b, sizeof(T));
+  return v;
 }
 
 }  // namespace kern

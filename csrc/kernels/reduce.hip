@@ -35,27 +35,6 @@
 namespace mireduce {
 namespace kern {
 
-template <class T> struct Bits { using type = std::conditional_t<sizeof(T) == 8, uint64_t, uint32_t>; };
-
-// Write-through (sc1) store / L1-bypassing (sc1) load of one accumulator value: the
-// agent-scope relaxed atomic forms lower to global_store/load ... sc1 on gfx950.
-template <class T>
-__device__ __forceinline__ void store_sc1(T* p, T v) {
-  using B = typename Bits<T>::type;
-  B b;
-  __builtin_memcpy(&b, &v, sizeof(T));
-  __hip_atomic_store(reinterpret_cast<B*>(p), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <class T>
-__device__ __forceinline__ T load_sc1(const T* p) {
-  using B = typename Bits<T>::type;
-  B b = __hip_atomic_load(reinterpret_cast<const B*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  T v;
-  __builtin_memcpy(&v, &b, sizeof(T));
-  return v;
-}
-
 template <class OpT, class AccT>
 __device__ __forceinline__ AccT wave_reduce(AccT v) {
 #pragma unroll

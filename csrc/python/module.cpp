@@ -18,6 +18,7 @@
 #include "mireduce/moments.hpp"
 #include "mireduce/mt19937.hpp"
 #include "mireduce/reduce.hpp"
+#include "mireduce/reduce_dim.hpp"
 #include "mireduce/trace.hpp"
 #include "mireduce/types.hpp"
 
@@ -323,6 +324,42 @@ PYBIND11_MODULE(_C, m) {
   });
 
   m.def("compiled_variants", &compiled_variants);
+
+  // Reductions along one axis of a row-major [rows, cols] matrix (csrc/kernels/reduce_dim.hip).
+  auto dim_dict = [](const DimPlan& p) {
+    py::dict d;
+    d["grid"] = p.grid;
+    d["block"] = p.block;
+    d["lanes_per_row"] = p.lanes_per_row;
+    d["splits"] = p.splits;
+    return d;
+  };
+  m.def(
+      "reduce_rows",
+      [dim_dict](uintptr_t in, uint64_t rows, uint64_t cols, int dtype, int op, int acc, uintptr_t out,
+                 uintptr_t scratch, int num_cus, uintptr_t stream) {
+        return dim_dict(reduce_rows(as_ptr<const void>(in), rows, cols, static_cast<DType>(dtype), static_cast<Op>(op),
+                                    static_cast<DType>(acc), as_ptr<void>(out), as_ptr<void>(scratch), num_cus,
+                                    as_stream(stream)));
+      },
+      py::arg("in_ptr"), py::arg("rows"), py::arg("cols"), py::arg("dtype"), py::arg("op"), py::arg("acc"),
+      py::arg("out_ptr"), py::arg("scratch_ptr"), py::arg("num_cus"), py::arg("stream") = 0);
+  m.def(
+      "reduce_cols",
+      [dim_dict](uintptr_t in, uint64_t outer, uint64_t rows, uint64_t cols, int dtype, int op, int acc, uintptr_t out,
+                 uintptr_t scratch, int num_cus, uintptr_t stream) {
+        return dim_dict(reduce_cols(as_ptr<const void>(in), outer, rows, cols, static_cast<DType>(dtype), static_cast<Op>(op),
+                                    static_cast<DType>(acc), as_ptr<void>(out), as_ptr<void>(scratch), num_cus,
+                                    as_stream(stream)));
+      },
+      py::arg("in_ptr"), py::arg("outer"), py::arg("rows"), py::arg("cols"), py::arg("dtype"), py::arg("op"),
+      py::arg("acc"), py::arg("out_ptr"), py::arg("scratch_ptr"), py::arg("num_cus"), py::arg("stream") = 0);
+  m.def("reduce_rows_scratch_bytes", [](uint64_t rows, uint64_t cols, int dtype, int num_cus) {
+    return reduce_rows_scratch_bytes(rows, cols, static_cast<DType>(dtype), num_cus);
+  });
+  m.def("reduce_cols_scratch_bytes", [](uint64_t outer, uint64_t rows, uint64_t cols, int dtype, int acc, int num_cus) {
+    return reduce_cols_scratch_bytes(outer, rows, cols, static_cast<DType>(dtype), static_cast<DType>(acc), num_cus);
+  });
 
   m.def(
       "moments",

@@ -72,6 +72,7 @@ MPI_Op mpi_op(Op o) {
     case Op::Sum: return MPI_SUM;
     case Op::Min: return MPI_MIN;
     case Op::Max: return MPI_MAX;
+    default: break;
   }
   return MPI_OP_NULL;
 }
@@ -232,6 +233,7 @@ int main(int argc, char** argv) {
       for (auto& s : list) {
         Op o;
         if (!parse_op(s, &o)) throw CliError("unknown op " + s);
+        if (op_is_fused(o)) throw CliError("--ops=" + s + ": the element-wise cross-rank benchmark keeps reduce.c's MAX/MIN/SUM");
         ops.push_back(o);
       }
     }

@@ -596,6 +596,7 @@ int main(int argc, char** argv) {
       for (auto& s : list) {
         Op o;
         if (!parse_op(s, &o)) throw CliError("unknown op " + s);
+        if (op_is_fused(o)) throw CliError("--ops=" + s + ": the element-wise cross-rank benchmark keeps reduce.c's MAX/MIN/SUM");
         ops.push_back(o);
       }
     }

@@ -288,8 +288,11 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
     checked = true;
     if (dtype_is_float(o.acc)) {
       const double g = acc_as_double(t.result, o.acc), c = acc_as_double(cpu, o.acc);
-      tol = (o.op == Op::Sum) ? sum_tolerance(o.dtype, o.acc, o.n, cpu_abs_sum(b.host.data(), o.n, o.dtype)) : 0.0;
-      ok = (o.op == Op::Sum) ? std::fabs(g - c) <= tol : g == c;
+      // SUMSQ is a sum too; its terms are non-negative, so its Σ|.| is the result itself
+      const bool summed = o.op == Op::Sum || o.op == Op::SumSq;
+      const double abs_sum = o.op == Op::SumSq ? std::fabs(c) : (summed ? cpu_abs_sum(b.host.data(), o.n, o.dtype) : 0.0);
+      tol = summed ? sum_tolerance(o.dtype, o.acc, o.n, abs_sum) : 0.0;
+      ok = summed ? std::fabs(g - c) <= tol : g == c;
     } else {
       ok = acc_as_int64(t.result, o.acc) == acc_as_int64(cpu, o.acc);
     }
@@ -304,7 +307,7 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
     r2.run_once(o.n, scratch);
     HIP_CHECK(hipMemcpy(cpu, b.out.get(), dtype_size(o.acc), hipMemcpyDeviceToHost));
     checked = true;
-    if (dtype_is_float(o.acc) && o.op == Op::Sum) {
+    if (dtype_is_float(o.acc) && (o.op == Op::Sum || o.op == Op::SumSq)) {
       const double g = acc_as_double(t.result, o.acc), c = acc_as_double(cpu, o.acc);
       tol = 1e-9 * std::fabs(c) + 1e-12;
       ok = std::fabs(g - c) <= tol;
@@ -351,7 +354,7 @@ void run_shmoo(Options o, Workspace& ws, hipStream_t s, uint64_t max_n) {
   const int kernels[] = {0, 1, 2, 3, 4, 5, 6, 8, 7};
   for (uint64_t n = 1; n <= max_n; n *= 2) {
     for (int k : kernels) {
-      if (k <= 6 && dtype_is_half(o.dtype)) continue;  // ladder kernels: reference element types only
+      if (k <= 6 && (dtype_is_half(o.dtype) || op_is_fused(o.op))) continue;  // ladder: reference types/ops only
       o.kernel = k;
       o.cpufinal = false;
       o.cputhresh = 1;
@@ -452,6 +455,10 @@ int main(int argc, char** argv) {
       o.cold = args.has("cold");
     }
     if (o.kernel < 0 || o.kernel > 8) throw CliError("--kernel must be 0..8");
+    if (op_is_fused(o.op) && !dtype_is_float(o.dtype))
+      throw CliError(std::string("--method=") + op_name(o.op) + " needs --type=float|double|bf16|half");
+    if (o.kernel <= 6 && op_is_fused(o.op))
+      throw CliError("--kernel 0..6 (the reference's ladder) implement SUM/MIN/MAX; SUMSQ/AMAX use kernels 7/8");
     if (o.kernel <= 6 && dtype_is_half(o.dtype))
       throw CliError("--kernel 0..6 (the reference's ladder) covers int/int64/float/double; bf16/half use kernels 7/8");
     if (o.kernel >= 7 && o.threads != 0 && o.threads != 256 && o.threads != 512 && o.threads != 1024)

@@ -169,6 +169,7 @@ void DirectPeers::reduce_scatter(size_t count, DType t, Op op, hipStream_t s) {
       case Op::Sum: rs_by_type<SumOp>(t, ins, world_, out_, b, e, s); break;
       case Op::Min: rs_by_type<MinOp>(t, ins, world_, out_, b, e, s); break;
       case Op::Max: rs_by_type<MaxOp>(t, ins, world_, out_, b, e, s); break;
+      default: MIREDUCE_REQUIRE(false, "direct: SUM, MIN or MAX");
     }
     MIREDUCE_HIP_THROW(hipGetLastError());
   }

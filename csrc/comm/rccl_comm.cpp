@@ -43,6 +43,9 @@ ncclRedOp_t nccl_op(Op o) {
     case Op::Sum: return ncclSum;
     case Op::Min: return ncclMin;
     case Op::Max: return ncclMax;
+    // fused ops: ranks exchange already-transformed partials (sum of x^2, max |x|), combined like SUM / MAX
+    case Op::SumSq: return ncclSum;
+    case Op::AbsMax: return ncclMax;
   }
   return ncclSum;
 }

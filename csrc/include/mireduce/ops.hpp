@@ -30,9 +30,22 @@ MIREDUCE_HD T wrap_add(T a, T b) {
   }
 }
 
+// Every functor has `identity`, `apply` (the associative combine of two accumulators) and `pre`
+// (the per-element transform applied once when an input element enters an accumulator: the
+// identity for SUM/MIN/MAX, x*x for SUMSQ, |x| for AMAX). Partials are combined with `apply`
+// only, so a fused transform never runs twice.
 struct SumOp {
   template <class T> MIREDUCE_HD static T identity() { return T(0); }
   template <class T> MIREDUCE_HD static T apply(T a, T b) { return wrap_add(a, b); }
+  template <class T> MIREDUCE_HD static T pre(T x) { return x; }
+};
+
+// Σ x² (squared L2 norm) — fused: the square is taken in the accumulator type as the element is
+// loaded, no intermediate array. Floating types only.
+struct SumSqOp {
+  template <class T> MIREDUCE_HD static T identity() { return T(0); }
+  template <class T> MIREDUCE_HD static T apply(T a, T b) { return a + b; }
+  template <class T> MIREDUCE_HD static T pre(T x) { return x * x; }
 };
 
 // MIN/MAX on floats follow IEEE-754 minNum/maxNum (a NaN operand is ignored), which is what
@@ -78,6 +91,7 @@ struct MinOp {
 #endif
     else return b < a ? b : a;
   }
+  template <class T> MIREDUCE_HD static T pre(T x) { return x; }
 };
 
 struct MaxOp {
@@ -93,6 +107,19 @@ struct MaxOp {
 #endif
     else return a < b ? b : a;
   }
+  template <class T> MIREDUCE_HD static T pre(T x) { return x; }
+};
+
+// max |x| (the amax of FP8 scaling, the inf-norm): |x| on load, MAX to combine (identity 0 since
+// every transformed value is >= 0; a NaN input is ignored like in MaxOp). Floating types only.
+struct AbsMaxOp {
+  template <class T> MIREDUCE_HD static T identity() { return T(0); }
+  template <class T> MIREDUCE_HD static T apply(T a, T b) { return MaxOp::apply(a, b); }
+#if defined(__HIP_DEVICE_COMPILE__)
+  template <class T> MIREDUCE_HD static T pre(T x) { return __builtin_fabs(x); }
+#else
+  template <class T> MIREDUCE_HD static T pre(T x) { return std::fabs(x); }
+#endif
 };
 
 }  // namespace mireduce

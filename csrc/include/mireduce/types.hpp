@@ -17,10 +17,10 @@
 namespace mireduce {
 
 enum class DType : int { Int32 = 0, Int64 = 1, Float32 = 2, Float64 = 3, BFloat16 = 4, Float16 = 5 };
-enum class Op : int { Sum = 0, Min = 1, Max = 2 };
+enum class Op : int { Sum = 0, Min = 1, Max = 2, SumSq = 3, AbsMax = 4 };
 
 constexpr int kNumDTypes = 6;
-constexpr int kNumOps = 3;
+constexpr int kNumOps = 5;
 
 inline size_t dtype_size(DType t) {
   switch (t) {
@@ -69,6 +69,8 @@ inline const char* op_name(Op o) {
     case Op::Sum: return "SUM";
     case Op::Min: return "MIN";
     case Op::Max: return "MAX";
+    case Op::SumSq: return "SUMSQ";
+    case Op::AbsMax: return "AMAX";
   }
   return "?";
 }
@@ -76,7 +78,8 @@ inline const char* op_name(Op o) {
 // Case-insensitive dtype parser. Accepts the reference spellings and common aliases.
 // Returns false when the string is not recognised.
 bool parse_dtype(const std::string& s, DType* out);
-// Case-SENSITIVE op parser ("SUM" | "MIN" | "MAX"), mirroring reduction.cpp:165-199's strcmp.
+// Case-SENSITIVE op parser ("SUM" | "MIN" | "MAX", plus the fused "SUMSQ" | "AMAX"), mirroring
+// reduction.cpp:165-199's strcmp.
 bool parse_op_strict(const std::string& s, Op* out);
 // Case-insensitive op parser used by the new apps' list flags (`--ops=max,min,sum`).
 bool parse_op(const std::string& s, Op* out);
@@ -84,8 +87,12 @@ bool parse_op(const std::string& s, Op* out);
 // Default accumulator: widen int32 SUM to int64 and fp32 SUM to fp64; MIN/MAX keep the
 // element type (they cannot overflow or lose precision). The 16-bit float types always
 // accumulate (and return) fp32: every 16-bit value is exact in fp32.
+// The fused ops (SUMSQ, AMAX) are for floating types; SUMSQ accumulates like SUM.
+inline bool op_is_fused(Op o) { return o == Op::SumSq || o == Op::AbsMax; }
+
 inline DType default_acc(DType t, Op o) {
   if (dtype_is_half(t)) return DType::Float32;
+  if (o == Op::SumSq) o = Op::Sum;
   if (o != Op::Sum) return t;
   if (t == DType::Int32) return DType::Int64;
   if (t == DType::Float32) return DType::Float64;
@@ -94,6 +101,8 @@ inline DType default_acc(DType t, Op o) {
 
 // Accumulator types we instantiate: same as input, or the widened type for SUM.
 inline bool acc_supported(DType t, Op o, DType acc) {
+  if (op_is_fused(o) && !dtype_is_float(t)) return false;
+  if (o == Op::SumSq) o = Op::Sum;
   if (dtype_is_half(t)) return acc == DType::Float32;
   if (acc == t) return true;
   if (o != Op::Sum) return false;

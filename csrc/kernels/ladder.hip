@@ -226,6 +226,7 @@ int ladder_reduce(int kernel, const void* in, uint64_t n, DType t, Op op, DType 
                   int max_threads, int max_blocks, hipStream_t s) {
   MIREDUCE_REQUIRE(kernel >= 0 && kernel <= 6, "ladder kernel must be 0..6");
   MIREDUCE_REQUIRE(acc_supported(t, op, acc), "unsupported (dtype, op, accumulator) combination");
+  MIREDUCE_REQUIRE(!op_is_fused(op), "ladder kernels 0..6 implement the reference's SUM/MIN/MAX");
   MIREDUCE_REQUIRE(!dtype_is_half(t), "ladder kernels 0..6 cover the reference's element types (int, float, double, "
                                       "int64); bf16/half use the streaming kernel (7/8)");
   using namespace ladder;
@@ -248,6 +249,8 @@ int ladder_reduce(int kernel, const void* in, uint64_t n, DType t, Op op, DType 
         case DType::Float64: MIREDUCE_LADDER_CASE(MinOp, double, double);
         default: break;
       }
+      break;
+    default:
       break;
     case Op::Max:
       switch (t) {

@@ -86,7 +86,7 @@ __device__ __forceinline__ void consume_tile(AccT (&acc)[UNROLL], const V (&v)[U
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
 #pragma unroll
-    for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], elem<T, AccT>(v[u], k));
+    for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(v[u], k)));
   }
 }
 
@@ -132,14 +132,14 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
        i < a.nvec; i += static_cast<uint64_t>(gridDim.x) * BLOCK) {
     const V v = vin[i];
 #pragma unroll
-    for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], elem<T, AccT>(v, k));
+    for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], OpT::pre(elem<T, AccT>(v, k)));
   }
   // Unaligned head and sub-vector tail (< N elements each), folded by the last workgroup.
   if (blockIdx.x == gridDim.x - 1) {
     const T* hp = static_cast<const T*>(a.head_ptr);
-    if (threadIdx.x < a.head) acc[0] = OpT::apply(acc[0], static_cast<AccT>(hp[threadIdx.x]));
+    if (threadIdx.x < a.head) acc[0] = OpT::apply(acc[0], OpT::pre(static_cast<AccT>(hp[threadIdx.x])));
     const T* tp = static_cast<const T*>(a.body) + a.nvec * N;
-    if (threadIdx.x < a.tail) acc[0] = OpT::apply(acc[0], static_cast<AccT>(tp[threadIdx.x]));
+    if (threadIdx.x < a.tail) acc[0] = OpT::apply(acc[0], OpT::pre(static_cast<AccT>(tp[threadIdx.x])));
   }
 #pragma unroll
   for (int u = 1; u < UNROLL; ++u) acc[0] = OpT::apply(acc[0], acc[u]);
@@ -274,8 +274,26 @@ constexpr int kNumUnrolls = 4;
 int block_index(int b) { return b == 256 ? 0 : (b == 512 ? 1 : (b == 1024 ? 2 : -1)); }
 int unroll_index(int u) { return u == 2 ? 0 : (u == 4 ? 1 : (u == 8 ? 2 : (u == 16 ? 3 : -1))); }
 
-// combo index: (op, dtype, acc) → 0..13
+// combo index: (op, dtype, acc) → 0..28
 int combo_index(Op op, DType t, DType acc) {
+  if (op == Op::SumSq) {  // 20..24
+    switch (t) {
+      case DType::Float32: return acc == DType::Float64 ? 20 : (acc == DType::Float32 ? 21 : -1);
+      case DType::Float64: return acc == DType::Float64 ? 22 : -1;
+      case DType::BFloat16: return acc == DType::Float32 ? 23 : -1;
+      case DType::Float16: return acc == DType::Float32 ? 24 : -1;
+      default: return -1;
+    }
+  }
+  if (op == Op::AbsMax) {  // 25..28
+    switch (t) {
+      case DType::Float32: return acc == DType::Float32 ? 25 : -1;
+      case DType::Float64: return acc == DType::Float64 ? 26 : -1;
+      case DType::BFloat16: return acc == DType::Float32 ? 27 : -1;
+      case DType::Float16: return acc == DType::Float32 ? 28 : -1;
+      default: return -1;
+    }
+  }
   const int o = static_cast<int>(op);
   switch (t) {
     case DType::Int32:
@@ -295,7 +313,7 @@ int combo_index(Op op, DType t, DType acc) {
   }
   return -1;
 }
-constexpr int kCombos = 20;
+constexpr int kCombos = 29;
 
 struct Table {
   LaunchFn fn[kCombos][kNumBlocks][kNumUnrolls][2][2];  // [..][policy nt][pipelined]
@@ -354,6 +372,15 @@ const Table& table() {
     fill_combo<SumOp, f16_t, float>(t, 17);
     fill_combo<MinOp, f16_t, float>(t, 18);
     fill_combo<MaxOp, f16_t, float>(t, 19);
+    fill_combo<SumSqOp, float, double>(t, 20);
+    fill_combo<SumSqOp, float, float>(t, 21);
+    fill_combo<SumSqOp, double, double>(t, 22);
+    fill_combo<SumSqOp, bf16_t, float>(t, 23);
+    fill_combo<SumSqOp, f16_t, float>(t, 24);
+    fill_combo<AbsMaxOp, float, float>(t, 25);
+    fill_combo<AbsMaxOp, double, double>(t, 26);
+    fill_combo<AbsMaxOp, bf16_t, float>(t, 27);
+    fill_combo<AbsMaxOp, f16_t, float>(t, 28);
     return t;
   }();
   return tb;
@@ -595,10 +622,12 @@ LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, 
 
 void reduce_finalize(const void* partials, size_t count, DType acc, Op op, void* out,
                      hipStream_t stream) {
-  switch (op) {
-    case Op::Sum: finalize_by_acc<SumOp>(acc, partials, count, out, stream); break;
+  switch (op) {  // partials are already transformed: SUMSQ folds like SUM, AMAX like MAX
+    case Op::Sum:
+    case Op::SumSq: finalize_by_acc<SumOp>(acc, partials, count, out, stream); break;
     case Op::Min: finalize_by_acc<MinOp>(acc, partials, count, out, stream); break;
-    case Op::Max: finalize_by_acc<MaxOp>(acc, partials, count, out, stream); break;
+    case Op::Max:
+    case Op::AbsMax: finalize_by_acc<MaxOp>(acc, partials, count, out, stream); break;
   }
   MIREDUCE_HIP_THROW(hipGetLastError());
 }
@@ -613,6 +642,7 @@ void combine_elementwise(void* inout, const void* other, size_t n, DType t, Op o
     case Op::Sum: combine_by_type<SumOp>(t, inout, other, n, stream); break;
     case Op::Min: combine_by_type<MinOp>(t, inout, other, n, stream); break;
     case Op::Max: combine_by_type<MaxOp>(t, inout, other, n, stream); break;
+    default: MIREDUCE_REQUIRE(false, "combine_elementwise: SUM, MIN or MAX");
   }
   MIREDUCE_HIP_THROW(hipGetLastError());
 }

@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kDimBlock) void rows_kernel(RowArgs a) {
         uint64_t head = addr % 16 ? (16 - addr % 16) / sizeof(T) : 0;
         if (head > e - b) head = e - b;
         // head and tail hold up to N-1 scalars each; a group may have fewer lanes (lpr < N)
-        for (uint64_t h = sl; h < head; h += lpr) acc[0] = OpT::apply(acc[0], static_cast<AccT>(p[b + h]));
+        for (uint64_t h = sl; h < head; h += lpr) acc[0] = OpT::apply(acc[0], OpT::pre(static_cast<AccT>(p[b + h])));
         const uint64_t vb = b + head;
         const uint64_t nvec = (e - vb) / N;
         const V* vp = reinterpret_cast<const V*>(p + vb);
@@ -90,16 +90,16 @@ __global__ __launch_bounds__(kDimBlock) void rows_kernel(RowArgs a) {
 #pragma unroll
           for (int u = 0; u < kRowUnroll; ++u) {
 #pragma unroll
-            for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], elem<T, AccT>(v[u], k));
+            for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(v[u], k)));
           }
         }
         for (; i < nvec; i += lpr) {
           const V v = __builtin_nontemporal_load(vp + i);
 #pragma unroll
-          for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], elem<T, AccT>(v, k));
+          for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], OpT::pre(elem<T, AccT>(v, k)));
         }
         const uint64_t tb = vb + nvec * N;
-        for (uint64_t h = tb + sl; h < e; h += lpr) acc[1] = OpT::apply(acc[1], static_cast<AccT>(p[h]));
+        for (uint64_t h = tb + sl; h < e; h += lpr) acc[1] = OpT::apply(acc[1], OpT::pre(static_cast<AccT>(p[h])));
       }
     }
 #pragma unroll
@@ -166,16 +166,16 @@ __global__ __launch_bounds__(kDimBlock) void short_rows_kernel(RowArgs a) {
       AccT acc = OpT::template identity<AccT>();
       if (has[j]) {
 #pragma unroll
-        for (int k = 0; k < N; ++k) acc = OpT::apply(acc, elem<T, AccT>(v[j], k));
+        for (int k = 0; k < N; ++k) acc = OpT::apply(acc, OpT::pre(elem<T, AccT>(v[j], k)));
       }
       if (r < a.rows) {  // scalar head / tail (rows not 16-byte aligned, or lengths not a multiple of N)
         const T* p = base + r * a.cols;
         const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
         uint64_t h = addr % 16 ? (16 - addr % 16) / sizeof(T) : 0;
         if (h > a.cols) h = a.cols;
-        for (uint64_t i = sl; i < h; i += lpr) acc = OpT::apply(acc, static_cast<AccT>(p[i]));
+        for (uint64_t i = sl; i < h; i += lpr) acc = OpT::apply(acc, OpT::pre(static_cast<AccT>(p[i])));
         const uint64_t tb = h + (a.cols - h) / N * N;
-        for (uint64_t i = tb + sl; i < a.cols; i += lpr) acc = OpT::apply(acc, static_cast<AccT>(p[i]));
+        for (uint64_t i = tb + sl; i < a.cols; i += lpr) acc = OpT::apply(acc, OpT::pre(static_cast<AccT>(p[i])));
       }
       for (int off = lpr >> 1; off > 0; off >>= 1) acc = OpT::apply(acc, __shfl_xor(acc, off, 64));
       if (sl == 0 && r < a.rows) out[r] = acc;
@@ -227,13 +227,13 @@ __global__ __launch_bounds__(kDimBlock) void cols_kernel(ColArgs a) {
 #pragma unroll
         for (int u = 0; u < kColUnroll; ++u) {
 #pragma unroll
-          for (int k = 0; k < N; ++k) acc[k] = OpT::apply(acc[k], elem<T, AccT>(v[u], k));
+          for (int k = 0; k < N; ++k) acc[k] = OpT::apply(acc[k], OpT::pre(elem<T, AccT>(v[u], k)));
         }
       }
       for (; r < r1; r += step) {
         const V v = __builtin_nontemporal_load(reinterpret_cast<const V*>(base + r * a.cols + c0));
 #pragma unroll
-        for (int k = 0; k < N; ++k) acc[k] = OpT::apply(acc[k], elem<T, AccT>(v, k));
+        for (int k = 0; k < N; ++k) acc[k] = OpT::apply(acc[k], OpT::pre(elem<T, AccT>(v, k)));
       }
     } else {
       for (; r + (kColUnroll - 1) * step < r1; r += kColUnroll * step) {
@@ -242,9 +242,9 @@ __global__ __launch_bounds__(kDimBlock) void cols_kernel(ColArgs a) {
         for (int u = 0; u < kColUnroll; ++u) v[u] = base[(r + u * step) * a.cols + c0];
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int u = 0; u < kColUnroll; ++u) acc[0] = OpT::apply(acc[0], static_cast<AccT>(v[u]));
+        for (int u = 0; u < kColUnroll; ++u) acc[0] = OpT::apply(acc[0], OpT::pre(static_cast<AccT>(v[u])));
       }
-      for (; r < r1; r += step) acc[0] = OpT::apply(acc[0], static_cast<AccT>(base[r * a.cols + c0]));
+      for (; r < r1; r += step) acc[0] = OpT::apply(acc[0], OpT::pre(static_cast<AccT>(base[r * a.cols + c0])));
     }
   }
   if (G > 1) {  // fold the G row groups of each column: a fixed pairwise tree through LDS
@@ -451,6 +451,25 @@ DimEntry lookup(Op op, DType t, DType acc) {
   MIREDUCE_DIM(Op::Min, MinOp)
   MIREDUCE_DIM(Op::Max, MaxOp)
 #undef MIREDUCE_DIM
+  // fused ops: floating types only (acc_supported)
+  if (op == Op::SumSq) {
+    switch (t) {
+      case DType::Float32: return acc == DType::Float64 ? entry<SumSqOp, float, double>() : entry<SumSqOp, float, float>();
+      case DType::Float64: return entry<SumSqOp, double, double>();
+      case DType::BFloat16: return entry<SumSqOp, bf16_t, float>();
+      case DType::Float16: return entry<SumSqOp, f16_t, float>();
+      default: break;
+    }
+  }
+  if (op == Op::AbsMax) {
+    switch (t) {
+      case DType::Float32: return entry<AbsMaxOp, float, float>();
+      case DType::Float64: return entry<AbsMaxOp, double, double>();
+      case DType::BFloat16: return entry<AbsMaxOp, bf16_t, float>();
+      case DType::Float16: return entry<AbsMaxOp, f16_t, float>();
+      default: break;
+    }
+  }
   throw Error("reduce_dim: unsupported combination");
 }
 

@@ -87,6 +87,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("OP_SUM") = static_cast<int>(Op::Sum);
   m.attr("OP_MIN") = static_cast<int>(Op::Min);
   m.attr("OP_MAX") = static_cast<int>(Op::Max);
+  m.attr("OP_SUMSQ") = static_cast<int>(Op::SumSq);
+  m.attr("OP_AMAX") = static_cast<int>(Op::AbsMax);
   m.attr("TICKET_STRIDE") = kTicketStride;
 
   // Read and clear the calling thread's sticky HIP error (e.g. left behind by an aborted

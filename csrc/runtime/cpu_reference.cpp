@@ -33,18 +33,27 @@ struct Compensated {
 // fp64 too) and rounded to it once at the end: a float-typed Neumaier sum saturates once its
 // compensation term stops absorbing the addends (4e9 bf16 values of ~6e-8 summed to 64.0 instead
 // of 237.5). W is the working type of a range: fp64 for floating sums, the accumulator otherwise.
+// The fused ops transform each element once (OpT::pre) and combine like SUM (SUMSQ) or MAX (AMAX);
+// partial results are folded with the combining op only.
+template <class OpT>
+using Combine = std::conditional_t<std::is_same_v<OpT, SumSqOp>, SumOp,
+                                   std::conditional_t<std::is_same_v<OpT, AbsMaxOp>, MaxOp, OpT>>;
+
+template <class OpT>
+inline constexpr bool kIsSum = std::is_same_v<Combine<OpT>, SumOp>;
+
 template <class OpT, class A>
-using Work = std::conditional_t<std::is_same_v<OpT, SumOp> && std::is_floating_point_v<A>, double, A>;
+using Work = std::conditional_t<kIsSum<OpT> && std::is_floating_point_v<A>, double, A>;
 
 template <class OpT, class T, class A>
 Work<OpT, A> reduce_range(const T* p, size_t n) {
-  if constexpr (std::is_same_v<OpT, SumOp> && std::is_floating_point_v<A>) {
-    Compensated<double> k;
-    for (size_t i = 0; i < n; ++i) k.add(static_cast<double>(static_cast<A>(p[i])));
+  if constexpr (kIsSum<OpT> && std::is_floating_point_v<A>) {
+    Compensated<double> k;  // squares (SUMSQ) are taken in fp64 here: the exact reference
+    for (size_t i = 0; i < n; ++i) k.add(OpT::pre(static_cast<double>(static_cast<A>(p[i]))));
     return k.value();
   } else {
     A a = OpT::template identity<A>();
-    for (size_t i = 0; i < n; ++i) a = OpT::apply(a, static_cast<A>(p[i]));
+    for (size_t i = 0; i < n; ++i) a = OpT::apply(a, OpT::pre(static_cast<A>(p[i])));
     return a;
   }
 }
@@ -72,7 +81,7 @@ A reduce_parallel(const T* p, size_t n, int threads) {
     });
   }
   for (auto& th : pool) th.join();
-  return static_cast<A>(reduce_range<OpT, W, W>(part.data(), part.size()));
+  return static_cast<A>(reduce_range<Combine<OpT>, W, W>(part.data(), part.size()));
 }
 
 template <class OpT, class T>
@@ -112,6 +121,8 @@ void cpu_reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out, 
     case Op::Sum: dispatch_t<SumOp>(in, n, t, acc, out, threads); break;
     case Op::Min: dispatch_t<MinOp>(in, n, t, acc, out, threads); break;
     case Op::Max: dispatch_t<MaxOp>(in, n, t, acc, out, threads); break;
+    case Op::SumSq: dispatch_t<SumSqOp>(in, n, t, acc, out, threads); break;
+    case Op::AbsMax: dispatch_t<AbsMaxOp>(in, n, t, acc, out, threads); break;
   }
 }
 
@@ -153,7 +164,9 @@ double cpu_abs_sum(const void* in, size_t n, DType t, int threads) {
 }
 
 void cpu_fold(const void* partials, size_t count, DType acc, Op op, void* out) {
-  cpu_reduce(partials, count, acc, op, acc, out, 1);
+  // partials of the fused ops are already transformed: fold them with the combining op
+  const Op combine = op == Op::SumSq ? Op::Sum : (op == Op::AbsMax ? Op::Max : op);
+  cpu_reduce(partials, count, acc, combine, acc, out, 1);
 }
 
 double sum_tolerance(DType t, DType acc, size_t n, double abs_sum) {

@@ -23,6 +23,8 @@ bool parse_op_strict(const std::string& s, Op* out) {
   if (s == "SUM") { *out = Op::Sum; return true; }
   if (s == "MIN") { *out = Op::Min; return true; }
   if (s == "MAX") { *out = Op::Max; return true; }
+  if (s == "SUMSQ") { *out = Op::SumSq; return true; }
+  if (s == "AMAX") { *out = Op::AbsMax; return true; }
   return false;
 }
 
@@ -31,6 +33,8 @@ bool parse_op(const std::string& s, Op* out) {
   if (!strcasecmp(c, "sum")) { *out = Op::Sum; return true; }
   if (!strcasecmp(c, "min")) { *out = Op::Min; return true; }
   if (!strcasecmp(c, "max")) { *out = Op::Max; return true; }
+  if (!strcasecmp(c, "sumsq")) { *out = Op::SumSq; return true; }
+  if (!strcasecmp(c, "amax") || !strcasecmp(c, "absmax")) { *out = Op::AbsMax; return true; }
   return false;
 }
 

@@ -48,7 +48,7 @@ def main(argv=None) -> int:
     if not cli.has(args, "method"):
         print("MISSING --method FLAG.\nYou must provide --method={ SUM | MIN | MAX }.", file=sys.stderr)
         return 1
-    if method not in ("SUM", "MIN", "MAX"):
+    if method not in ("SUM", "MIN", "MAX", "SUMSQ", "AMAX"):
         print("No --method specified!", file=sys.stderr)
         return 1
     import torch
@@ -90,7 +90,14 @@ def main(argv=None) -> int:
     print(f"{plan.get('grid', 0)} blocks\n")
     print(throughput_line(1e-9 * nbytes / secs if secs else 0.0, secs, n, 1, plan.get("block", 0)))
     got = out.item()
-    if op == "sum":
+    if op == "sumsq":
+        xd = x.double()
+        ref = (xd * xd).sum().item()
+        ok = abs(got - ref) <= sum_tolerance(dt, acc, n, ref)
+    elif op == "amax":
+        ref = x.abs().max().item()
+        ok = got == ref
+    elif op == "sum":
         ref = x.sum(dtype=torch.float64 if acc.is_floating_point else torch.int64).item()
         if acc == torch.int32:
             ref = (int(ref) + 2 ** 31) % 2 ** 32 - 2 ** 31

@@ -68,6 +68,11 @@ CONFIGS: dict[str, WorkloadConfig] = {
         baseline=92.7729, baseline_source="mpi/CUdata.txt:2 (CUDA DOUBLE SUM, best reference GB/s)",
         description="1B double sum across N MI355X: local HIP reduce + RCCL all-reduce over xGMI",
     ),
+    "xgmi_1b_double_norm2": WorkloadConfig(
+        name="xgmi_1b_double_norm2", dtype=torch.float64, op="sumsq", n_total=1_000_000_000,
+        description="sum of squares (squared L2 norm) of 1e9 doubles across N GPUs, square fused into the "
+                    "load (MI355X addition; not a reference config)",
+    ),
     "gpu_4g_bf16_sum": WorkloadConfig(
         name="gpu_4g_bf16_sum", dtype=torch.bfloat16, op="sum", n_total=4_000_000_000,
         description="4e9 bfloat16 (8 GB) sum, fp32 accumulation (MI355X addition; not a reference config)",
@@ -206,6 +211,16 @@ class ScalarReduction:
                 loc += c.sum(dtype=acc_dt)
                 absl += c.abs().sum(dtype=torch.float64) if c.dtype.is_floating_point else \
                     c.abs().to(torch.float64).sum()
+        elif self.cfg.op == "sumsq":  # Σ x² in fp64; every term is non-negative, so Σ|.| is the sum
+            loc = torch.zeros(1, dtype=torch.float64, device=dev)
+            for i in range(0, x.numel(), chunk):
+                c = x[i:i + chunk].double()
+                loc += (c * c).sum()
+            absl = loc.clone()
+        elif self.cfg.op == "amax":
+            parts = [x[i:i + chunk].abs().max().reshape(1) for i in range(0, x.numel(), chunk)]
+            loc = torch.cat(parts).max().reshape(1).to(self.acc)
+            absl = torch.zeros(1, dtype=torch.float64, device=dev)
         else:
             parts = [(x[i:i + chunk].min() if self.cfg.op == "min" else x[i:i + chunk].max()).reshape(1)
                      for i in range(0, x.numel(), chunk)]
@@ -220,7 +235,7 @@ class ScalarReduction:
     def verify(self, result: torch.Tensor) -> dict:
         got = result.reshape(-1)[0].item()
         exp, abs_sum = self.reference()
-        if self.cfg.op == "sum" and self.acc.is_floating_point:
+        if self.cfg.op in ("sum", "sumsq") and self.acc.is_floating_point:
             tol = sum_tolerance(self.cfg.dtype, self.acc, self.n_total, abs_sum)
             ok = math.isfinite(got) and abs(got - exp) <= tol
         else:

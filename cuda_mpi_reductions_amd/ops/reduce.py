@@ -35,7 +35,10 @@ __all__ = [
 DTYPE_CODES = {torch.int32: 0, torch.int64: 1, torch.float32: 2, torch.float64: 3,
                torch.bfloat16: 4, torch.float16: 5}
 CODE_DTYPES = {v: k for k, v in DTYPE_CODES.items()}
-OP_CODES = {"sum": 0, "min": 1, "max": 2}
+# sum / min / max are the reference's operators; sumsq (fused sum of squares) and amax (fused
+# max |x|) transform each element once as it is loaded (floating dtypes only).
+OP_CODES = {"sum": 0, "min": 1, "max": 2, "sumsq": 3, "amax": 4}
+FUSED_OPS = ("sumsq", "amax")
 
 
 def dtype_code(dt: torch.dtype) -> int:
@@ -50,12 +53,14 @@ def op_code(op: str) -> int:
     try:
         return OP_CODES[op.lower()]
     except KeyError:
-        raise ValueError(f"unsupported op {op!r}; supported: sum, min, max") from None
+        raise ValueError(f"unsupported op {op!r}; supported: {', '.join(OP_CODES)}") from None
 
 
 def default_acc_dtype(dt: torch.dtype, op: str) -> torch.dtype:
-    """int32 SUM -> int64, float32 SUM -> float64, bfloat16/float16 -> float32 (every op), everything
-    else keeps its dtype."""
+    """int32 SUM -> int64, float32 SUM / SUMSQ -> float64, bfloat16/float16 -> float32 (every op),
+    everything else keeps its dtype."""
+    if op.lower() in FUSED_OPS and not dt.is_floating_point:
+        raise TypeError(f"{op} needs a floating-point tensor, got {dt}")
     return CODE_DTYPES[native().default_acc(dtype_code(dt), op_code(op))]
 
 

@@ -27,7 +27,10 @@ import torch.distributed as dist
 __all__ = ["DistContext", "init", "shutdown", "shard", "reduce_op", "scalar_allreduce",
            "vector_reduce", "vector_allreduce", "barrier", "max_over_ranks"]
 
-_REDUCE_OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
+# The fused ops exchange already-transformed partials (sum of x^2, max |x|) and combine them
+# like SUM / MAX across ranks.
+_REDUCE_OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX,
+               "sumsq": dist.ReduceOp.SUM, "amax": dist.ReduceOp.MAX}
 
 
 def reduce_op(op: str):

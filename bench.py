@@ -94,6 +94,10 @@ def _time_torch_reduction(wl, K: int, W: int, ctx) -> float:
     def step():
         if op == "sum":
             r = x.sum(dtype=acc).reshape(1)
+        elif op == "sumsq":  # torch's one-pass fused form of the same quantity
+            r = torch.linalg.vector_norm(x, 2, dtype=acc).square().reshape(1)
+        elif op == "amax":
+            r = torch.linalg.vector_norm(x, float("inf")).to(acc).reshape(1)
         else:
             r = (x.amin() if op == "min" else x.amax()).to(acc).reshape(1)
         if ctx.world_size > 1:

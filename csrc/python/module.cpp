@@ -19,6 +19,7 @@
 #include "mireduce/mt19937.hpp"
 #include "mireduce/reduce.hpp"
 #include "mireduce/reduce_dim.hpp"
+#include "mireduce/reduce_many.hpp"
 #include "mireduce/trace.hpp"
 #include "mireduce/types.hpp"
 
@@ -326,6 +327,24 @@ PYBIND11_MODULE(_C, m) {
   });
 
   m.def("compiled_variants", &compiled_variants);
+
+  // One launch over a list of same-typed tensors (csrc/kernels/reduce_many.hip).
+  py::class_<BoundReduceMany>(m, "BoundReduceMany")
+      .def(py::init([](const std::vector<uintptr_t>& ptrs, const std::vector<uint64_t>& counts, int dtype, int op,
+                       int acc, uintptr_t out, int device, int num_cus, uintptr_t stream) {
+             std::vector<const void*> p;
+             p.reserve(ptrs.size());
+             for (uintptr_t v : ptrs) p.push_back(as_ptr<const void>(v));
+             return new BoundReduceMany(p, counts, static_cast<DType>(dtype), static_cast<Op>(op),
+                                        static_cast<DType>(acc), as_ptr<void>(out), device, num_cus, as_stream(stream));
+           }),
+           py::arg("ptrs"), py::arg("counts"), py::arg("dtype"), py::arg("op"), py::arg("acc"), py::arg("out_ptr"),
+           py::arg("device"), py::arg("num_cus"), py::arg("stream") = 0)
+      .def("launch", [](const BoundReduceMany& b, uintptr_t stream) { b.launch(as_stream(stream)); },
+           py::arg("stream"))
+      .def_property_readonly("tensors", &BoundReduceMany::tensors)
+      .def_property_readonly("segments", &BoundReduceMany::segments)
+      .def_property_readonly("grid", &BoundReduceMany::grid);
 
   // Reductions along one axis of a row-major [rows, cols] matrix (csrc/kernels/reduce_dim.hip).
   auto dim_dict = [](const DimPlan& p) {

@@ -7,3 +7,4 @@ from .fill import PATTERNS, fill_, mt19937_fill_, synthetic  # noqa: F401
 from .moments import combine_moments, moments  # noqa: F401
 from .reduce_dim import reduce_dim  # noqa: F401
 from .norm import norm  # noqa: F401
+from .reduce_many import ReduceMany, norm_many, reduce_many  # noqa: F401

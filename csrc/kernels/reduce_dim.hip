@@ -1,10 +1,10 @@
 // Reductions along one axis of a row-major [rows, cols] matrix; see reduce_dim.hpp.
 //
-// Rows (reduce the contiguous axis). The unit of work is a row *segment* handled by a group of
-// `lpr` lanes of one wave (lpr = 1..64): short rows pack 64/lpr rows into a wave, long rows are
-// cut into `splits` segments so that even a handful of rows keeps every CU streaming. Loads are
+// Rows (reduce the contiguous axis). Short rows (<= 32 vectors) are handled by groups of `lpr`
+// lanes of one wave, 64/lpr rows per wave; long rows by one workgroup per row *segment*, cut into
+// `splits` segments so that even a handful of rows keeps every CU streaming. Loads are
 // the full reduction's 16-byte nt vectors (vec16.hpp) with per-segment scalar head/tail, so any
-// row length and base alignment works. A wave never synchronises with its workgroup. When a row
+// row length and base alignment works. When a row
 // is split, each segment publishes its partial write-through (sc1) and takes a per-row ticket;
 // the last arriver folds the row's partials in segment order (deterministic) and resets the
 // ticket — the single-pass scheme of reduce.hip (threadFenceReduction_kernel.cu:116-171 idea).
@@ -46,82 +46,83 @@ struct RowArgs {
   unsigned* tickets; // [rows] (splits > 1)
 };
 
+// Long rows: a workgroup streams one row segment at a time (256 lanes, 4 KB contiguous per load
+// round) — fewer, wider concurrent streams than a wave per segment, as in reduce_many.hip.
 template <class OpT, class T, class AccT>
 __global__ __launch_bounds__(kDimBlock) void rows_kernel(RowArgs a) {
   using V = typename Vec16<T>::type;
   constexpr int N = Vec16<T>::N;
-  const int lane = threadIdx.x & 63;
-  const int lpr = a.lpr;
-  const int per_wave = 64 / lpr;
-  const int sub = lane / lpr, sl = lane % lpr;
+  constexpr int U = kRowUnroll;
+  constexpr int kWaves = kDimBlock / 64;
+  __shared__ AccT lds[kWaves];
+  const int tid = threadIdx.x;
   const uint64_t nseg = a.rows * a.splits;
-  const uint64_t wave = static_cast<uint64_t>(blockIdx.x) * (kDimBlock / 64) + (threadIdx.x >> 6);
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * (kDimBlock / 64) * per_wave;
   const T* base = static_cast<const T*>(a.in);
-  for (uint64_t seg0 = wave * per_wave; seg0 < nseg; seg0 += stride) {  // wave-uniform loop
-    const uint64_t seg = seg0 + sub;
-    const bool active = seg < nseg;
-    AccT acc[kRowUnroll];
+  for (uint64_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {  // workgroup-uniform
+    AccT acc[U];
 #pragma unroll
-    for (int u = 0; u < kRowUnroll; ++u) acc[u] = OpT::template identity<AccT>();
-    uint64_t r = 0;
-    if (active) {
-      r = seg / a.splits;
-      const uint64_t b = (seg % a.splits) * a.seg_len;
-      const uint64_t e = std::min<uint64_t>(a.cols, b + a.seg_len);
-      const T* p = base + r * a.cols;
-      if (b < e) {
-        const uintptr_t addr = reinterpret_cast<uintptr_t>(p + b);
-        uint64_t head = addr % 16 ? (16 - addr % 16) / sizeof(T) : 0;
-        if (head > e - b) head = e - b;
-        // head and tail hold up to N-1 scalars each; a group may have fewer lanes (lpr < N)
-        for (uint64_t h = sl; h < head; h += lpr) acc[0] = OpT::apply(acc[0], OpT::pre(static_cast<AccT>(p[b + h])));
-        const uint64_t vb = b + head;
-        const uint64_t nvec = (e - vb) / N;
-        const V* vp = reinterpret_cast<const V*>(p + vb);
-        uint64_t i = sl;
-        for (; i + static_cast<uint64_t>(kRowUnroll - 1) * lpr < nvec; i += static_cast<uint64_t>(kRowUnroll) * lpr) {
-          V v[kRowUnroll];
+    for (int u = 0; u < U; ++u) acc[u] = OpT::template identity<AccT>();
+    const uint64_t r = seg / a.splits;
+    const uint64_t b = (seg % a.splits) * a.seg_len;
+    const uint64_t e = std::min<uint64_t>(a.cols, b + a.seg_len);
+    const T* p = base + r * a.cols;
+    if (b < e) {
+      const uintptr_t addr = reinterpret_cast<uintptr_t>(p + b);
+      uint64_t head = addr % 16 ? (16 - addr % 16) / sizeof(T) : 0;
+      if (head > e - b) head = e - b;
+      if (static_cast<uint64_t>(tid) < head) acc[0] = OpT::apply(acc[0], OpT::pre(static_cast<AccT>(p[b + tid])));
+      const uint64_t vb = b + head;
+      const uint64_t nvec = (e - vb) / N;
+      const V* vp = reinterpret_cast<const V*>(p + vb);
+      uint64_t i = tid;
+      for (; i + static_cast<uint64_t>(U - 1) * kDimBlock < nvec; i += static_cast<uint64_t>(U) * kDimBlock) {
+        V v[U];
 #pragma unroll
-          for (int u = 0; u < kRowUnroll; ++u) v[u] = __builtin_nontemporal_load(vp + i + static_cast<uint64_t>(u) * lpr);
-          // all loads out before the first use: MIN/MAX's inline v_min/v_max otherwise made hipcc
-          // wait for each load in turn (one 16-byte load in flight per lane)
-          __builtin_amdgcn_sched_barrier(0);
+        for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(vp + i + static_cast<uint64_t>(u) * kDimBlock);
+        // all loads out before the first use: MIN/MAX's inline v_min/v_max otherwise made hipcc
+        // wait for each load in turn (one 16-byte load in flight per lane)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int u = 0; u < kRowUnroll; ++u) {
+        for (int u = 0; u < U; ++u) {
 #pragma unroll
-            for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(v[u], k)));
-          }
+          for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(v[u], k)));
         }
-        for (; i < nvec; i += lpr) {
-          const V v = __builtin_nontemporal_load(vp + i);
+      }
+      for (; i < nvec; i += kDimBlock) {
+        const V v = __builtin_nontemporal_load(vp + i);
 #pragma unroll
-          for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], OpT::pre(elem<T, AccT>(v, k)));
+        for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], OpT::pre(elem<T, AccT>(v, k)));
+      }
+      const uint64_t tb = vb + nvec * N;
+      if (static_cast<uint64_t>(tid) < e - tb) acc[1] = OpT::apply(acc[1], OpT::pre(static_cast<AccT>(p[tb + tid])));
+    }
+#pragma unroll
+    for (int u = 1; u < U; ++u) acc[0] = OpT::apply(acc[0], acc[u]);
+    AccT v = acc[0];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = OpT::apply(v, __shfl_xor(v, off, 64));
+    if ((tid & 63) == 0) lds[tid >> 6] = v;
+    __syncthreads();
+    if (tid == 0) {
+#pragma unroll
+      for (int w = 1; w < kWaves; ++w) v = OpT::apply(v, lds[w]);
+      AccT* out = static_cast<AccT*>(a.out);
+      if (a.splits == 1) {
+        out[r] = v;
+      } else {
+        AccT* part = static_cast<AccT*>(a.partials);
+        store_sc1(&part[seg], v);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(&a.tickets[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == a.splits - 1) {  // last segment of row r: fold in segment order
+          __hip_atomic_store(&a.tickets[r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          AccT t = OpT::template identity<AccT>();
+          for (uint64_t j = 0; j < a.splits; ++j) t = OpT::apply(t, load_sc1(&part[r * a.splits + j]));
+          out[r] = t;
         }
-        const uint64_t tb = vb + nvec * N;
-        for (uint64_t h = tb + sl; h < e; h += lpr) acc[1] = OpT::apply(acc[1], OpT::pre(static_cast<AccT>(p[h])));
       }
     }
-#pragma unroll
-    for (int u = 1; u < kRowUnroll; ++u) acc[0] = OpT::apply(acc[0], acc[u]);
-    AccT v = acc[0];
-    for (int off = lpr >> 1; off > 0; off >>= 1) v = OpT::apply(v, __shfl_xor(v, off, 64));  // within the group
-    if (!active || sl != 0) continue;
-    AccT* out = static_cast<AccT*>(a.out);
-    if (a.splits == 1) {
-      out[r] = v;
-      continue;
-    }
-    AccT* part = static_cast<AccT*>(a.partials);
-    store_sc1(&part[seg], v);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(&a.tickets[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == a.splits - 1) {  // last segment of row r: fold in segment order
-      __hip_atomic_store(&a.tickets[r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      AccT t = OpT::template identity<AccT>();
-      for (uint64_t j = 0; j < a.splits; ++j) t = OpT::apply(t, load_sc1(&part[r * a.splits + j]));
-      out[r] = t;
-    }
+    __syncthreads();  // lds is rewritten by the next segment
   }
 }
 
@@ -337,16 +338,22 @@ RowLayout row_layout(size_t rows, size_t cols, DType t, int num_cus, int residen
     L.lpr = static_cast<int>(next_pow2(std::max<uint64_t>(vecs, 1)));
     L.splits = 1;
   } else {
-    L.lpr = 64;
-    const uint64_t min_seg_vecs = 64 * kern::kRowUnroll;  // one full unrolled round per lane
+    L.lpr = 64;  // long rows: a workgroup per segment (rows_kernel)
+    const uint64_t min_seg_vecs = static_cast<uint64_t>(kern::kDimBlock) * kern::kRowUnroll;  // one full round
     const uint64_t by_len = std::max<uint64_t>(1, vecs / min_seg_vecs);
     const uint64_t want = rows ? (target_waves + rows - 1) / rows : 1;
     L.splits = std::max<uint64_t>(1, std::min({want, by_len, kMaxRowSplits}));
   }
   L.seg_len = ((cols + L.splits - 1) / L.splits + N - 1) / N * N;
-  const uint64_t per_wave = (64 / L.lpr) * (L.lpr < 64 ? kern::kRowUnroll : 1);  // segments per wave trip
-  L.waves = (rows * L.splits + per_wave - 1) / per_wave;
-  const uint64_t blocks = (L.waves + 3) / 4;
+  uint64_t blocks;
+  if (L.lpr < 64) {  // short rows: rows per wave trip = (64 / lpr) x kRowUnroll, 4 waves per workgroup
+    const uint64_t per_wave = (64 / L.lpr) * kern::kRowUnroll;
+    L.waves = (rows + per_wave - 1) / per_wave;
+    blocks = (L.waves + 3) / 4;
+  } else {  // long rows: one workgroup per segment
+    L.waves = rows * L.splits * 4;
+    blocks = rows * L.splits;
+  }
   L.grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(blocks, static_cast<uint64_t>(num_cus) * resident)));
   return L;
 }

@@ -44,3 +44,10 @@ def test_example_single_gpu():
     r = run([sys.executable, os.path.join(ROOT, "examples", "01_single_gpu.py")], cwd=ROOT, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "GB/s" in r.stdout
+
+
+@pytest.mark.gpu
+def test_example_norms_dims_many():
+    r = run([sys.executable, os.path.join(ROOT, "examples", "04_norms_dims_many.py")], timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "per-tensor sum of squares" in r.stdout and "total grad-norm-style L2" in r.stdout

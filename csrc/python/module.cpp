@@ -12,6 +12,7 @@
 #include <cstring>
 #include <memory>
 
+#include "mireduce/arg_reduce.hpp"
 #include "mireduce/check.hpp"
 #include "mireduce/cpu_reference.hpp"
 #include "mireduce/ladder.hpp"
@@ -381,6 +382,41 @@ PYBIND11_MODULE(_C, m) {
   m.def("reduce_cols_scratch_bytes", [](uint64_t outer, uint64_t rows, uint64_t cols, int dtype, int acc, int num_cus) {
     return reduce_cols_scratch_bytes(outer, rows, cols, static_cast<DType>(dtype), static_cast<DType>(acc), num_cus);
   });
+
+  m.def(
+      "arg_reduce_rows",
+      [](uintptr_t in, uint64_t rows, uint64_t cols, int dtype, int op, uintptr_t out_value, uintptr_t out_index,
+         uintptr_t scratch, int num_cus, uintptr_t stream, int unroll, int wg_per_cu) {
+        ArgTune tune;
+        tune.unroll = unroll;
+        tune.wg_per_cu = wg_per_cu;
+        const ArgPlan p = arg_reduce_rows(as_ptr<const void>(in), rows, cols, static_cast<DType>(dtype),
+                                          static_cast<Op>(op), as_ptr<void>(out_value), as_ptr<int64_t>(out_index),
+                                          as_ptr<void>(scratch), num_cus, as_stream(stream), tune);
+        py::dict d;
+        d["grid"] = p.grid;
+        d["block"] = p.block;
+        d["lanes_per_row"] = p.lanes_per_row;
+        d["splits"] = p.splits;
+        d["unroll"] = p.unroll;
+        d["wg_per_cu"] = p.wg_per_cu;
+        return d;
+      },
+      py::arg("in_ptr"), py::arg("rows"), py::arg("cols"), py::arg("dtype"), py::arg("op"), py::arg("out_value_ptr"),
+      py::arg("out_index_ptr"), py::arg("scratch_ptr"), py::arg("num_cus"), py::arg("stream") = 0,
+      py::arg("unroll") = 0, py::arg("wg_per_cu") = 0);
+  m.def("arg_reduce_scratch_bytes", [](uint64_t rows, uint64_t cols, int dtype, int num_cus) {
+    return arg_reduce_scratch_bytes(rows, cols, static_cast<DType>(dtype), num_cus);
+  });
+  m.def(
+      "cpu_arg_reduce_rows",
+      [](uintptr_t in, uint64_t rows, uint64_t cols, int dtype, int op, uintptr_t out_value, uintptr_t out_index) {
+        py::gil_scoped_release nogil;
+        cpu_arg_reduce_rows(as_ptr<const void>(in), rows, cols, static_cast<DType>(dtype), static_cast<Op>(op),
+                            as_ptr<void>(out_value), as_ptr<int64_t>(out_index));
+      },
+      py::arg("in_ptr"), py::arg("rows"), py::arg("cols"), py::arg("dtype"), py::arg("op"), py::arg("out_value_ptr"),
+      py::arg("out_index_ptr"));
 
   m.def(
       "moments",

@@ -8,3 +8,4 @@ from .moments import combine_moments, moments  # noqa: F401
 from .reduce_dim import reduce_dim  # noqa: F401
 from .norm import norm  # noqa: F401
 from .reduce_many import ReduceMany, norm_many, reduce_many  # noqa: F401
+from .arg_reduce import arg_reduce, argmax, argmin  # noqa: F401

@@ -41,6 +41,7 @@ struct RowArgs {
   uint64_t splits;   // segments per row
   uint64_t seg_len;  // elements per segment (multiple of the vector width)
   int lpr;           // lanes per segment (power of two, 1..64)
+  int aligned;       // short rows: base and row length multiples of 16 bytes
   void* out;
   void* partials;    // [rows * splits] AccT (splits > 1)
   unsigned* tickets; // [rows] (splits > 1)
@@ -129,7 +130,9 @@ __global__ __launch_bounds__(kDimBlock) void rows_kernel(RowArgs a) {
 // Short rows (every row fits in one vector per lane of its lpr-lane group, lpr < 64): a wave takes
 // kRowUnroll batches of 64/lpr consecutive rows per iteration so each lane has kRowUnroll 16-byte
 // loads in flight, instead of one load per loop trip.
-template <class OpT, class T, class AccT>
+// ALIGNED (base and row length multiples of 16 bytes): rows are whole vectors — no per-row
+// alignment arithmetic or head/tail loops (8 / 64-column bf16 rows: VALU-bound without it).
+template <class OpT, class T, class AccT, bool ALIGNED>
 __global__ __launch_bounds__(kDimBlock) void short_rows_kernel(RowArgs a) {
   using V = typename Vec16<T>::type;
   constexpr int N = Vec16<T>::N;
@@ -152,13 +155,20 @@ __global__ __launch_bounds__(kDimBlock) void short_rows_kernel(RowArgs a) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const uint64_t r = row0 + static_cast<uint64_t>(j) * per_wave + sub;
-      const T* p = base + r * a.cols;
-      const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
-      uint64_t h = addr % 16 ? (16 - addr % 16) / sizeof(T) : 0;
-      if (h > a.cols) h = a.cols;
-      has[j] = r < a.rows && static_cast<uint64_t>(sl) < (a.cols - h) / N;
-      const V* src = has[j] ? reinterpret_cast<const V*>(p + h) + sl : &g_dummy_vec<V>;
-      v[j] = __builtin_nontemporal_load(src);
+      if constexpr (ALIGNED) {
+        const uint64_t vecs = a.cols / N;
+        has[j] = r < a.rows && static_cast<uint64_t>(sl) < vecs;
+        const V* src = has[j] ? reinterpret_cast<const V*>(base) + r * vecs + sl : &g_dummy_vec<V>;
+        v[j] = __builtin_nontemporal_load(src);
+      } else {
+        const T* p = base + r * a.cols;
+        const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
+        uint64_t h = addr % 16 ? (16 - addr % 16) / sizeof(T) : 0;
+        if (h > a.cols) h = a.cols;
+        has[j] = r < a.rows && static_cast<uint64_t>(sl) < (a.cols - h) / N;
+        const V* src = has[j] ? reinterpret_cast<const V*>(p + h) + sl : &g_dummy_vec<V>;
+        v[j] = __builtin_nontemporal_load(src);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -169,7 +179,7 @@ __global__ __launch_bounds__(kDimBlock) void short_rows_kernel(RowArgs a) {
 #pragma unroll
         for (int k = 0; k < N; ++k) acc = OpT::apply(acc, OpT::pre(elem<T, AccT>(v[j], k)));
       }
-      if (r < a.rows) {  // scalar head / tail (rows not 16-byte aligned, or lengths not a multiple of N)
+      if (!ALIGNED && r < a.rows) {  // scalar head / tail (rows not 16-byte aligned, or lengths not a multiple of N)
         const T* p = base + r * a.cols;
         const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
         uint64_t h = addr % 16 ? (16 - addr % 16) / sizeof(T) : 0;
@@ -390,8 +400,10 @@ using FoldFn = void (*)(const void*, uint64_t, uint64_t, void*, hipStream_t);
 
 template <class OpT, class T, class AccT>
 void launch_rows(const kern::RowArgs& a, int grid, hipStream_t s) {
-  if (a.lpr < 64)
-    hipLaunchKernelGGL((kern::short_rows_kernel<OpT, T, AccT>), dim3(grid), dim3(kern::kDimBlock), 0, s, a);
+  if (a.lpr < 64 && a.aligned)
+    hipLaunchKernelGGL((kern::short_rows_kernel<OpT, T, AccT, true>), dim3(grid), dim3(kern::kDimBlock), 0, s, a);
+  else if (a.lpr < 64)
+    hipLaunchKernelGGL((kern::short_rows_kernel<OpT, T, AccT, false>), dim3(grid), dim3(kern::kDimBlock), 0, s, a);
   else
     hipLaunchKernelGGL((kern::rows_kernel<OpT, T, AccT>), dim3(grid), dim3(kern::kDimBlock), 0, s, a);
 }
@@ -414,7 +426,7 @@ void launch_fold(const void* partials, uint64_t splits, uint64_t cols, void* out
 
 template <class OpT, class T, class AccT>
 int rows_resident(bool short_rows) {
-  static const int s = resident_per_cu(kern::short_rows_kernel<OpT, T, AccT>);
+  static const int s = resident_per_cu(kern::short_rows_kernel<OpT, T, AccT, false>);
   static const int l = resident_per_cu(kern::rows_kernel<OpT, T, AccT>);
   return short_rows ? s : l;
 }
@@ -511,6 +523,7 @@ DimPlan reduce_rows(const void* in, size_t rows, size_t cols, DType t, Op op, DT
   a.splits = L.splits;
   a.seg_len = L.seg_len;
   a.lpr = L.lpr;
+  a.aligned = reinterpret_cast<uintptr_t>(in) % 16 == 0 && (cols * dtype_size(t)) % 16 == 0;
   a.out = out;
   if (L.splits > 1) {
     MIREDUCE_REQUIRE(scratch != nullptr, "reduce_rows: this shape needs scratch (reduce_rows_scratch_bytes)");

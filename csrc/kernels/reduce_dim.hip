@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "mireduce/check.hpp"
 #include "mireduce/half.hpp"
@@ -393,6 +394,21 @@ ColLayout col_layout(const void* in, size_t outer, size_t rows, size_t cols, DTy
   return L;
 }
 
+// Resident workgroups per CU the persistent grids are sized for. Measured (tools/dim_wg_sweep.sh,
+// profiles/r1_session3/reduce_dim/wg_sweep_bf16.txt, 4 GB bf16): column reductions stream best
+// with ONE workgroup per CU (488281 x 4096: 4.6 -> 6.8 TB/s; fewer concurrent DRAM streams, as in
+// the full reduction), long rows of >= 64 KB with two (30517 x 65536: 6.9 -> 7.2), shorter rows
+// need the occupancy limit (a workgroup per 8 KB row has little in flight).
+// MIREDUCE_DIM_WG_PER_CU=k overrides every choice (A/B runs).
+int wg_cap(int occ, int preferred) {
+  static const int env = [] {
+    const char* e = std::getenv("MIREDUCE_DIM_WG_PER_CU");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int cap = env > 0 ? env : preferred;
+  return cap > 0 ? std::min(occ, cap) : occ;
+}
+
 using RowFn = void (*)(const kern::RowArgs&, int, hipStream_t);
 using OccFn = int (*)(bool);  // resident workgroups per CU of the (short-row | vector) variant
 using ColFn = void (*)(const kern::ColArgs&, dim3, bool, hipStream_t);
@@ -515,7 +531,8 @@ DimPlan reduce_rows(const void* in, size_t rows, size_t cols, DType t, Op op, DT
   DimPlan plan;
   if (rows == 0) return plan;
   const bool short_rows = row_layout(rows, cols, t, num_cus).lpr < 64;
-  const RowLayout L = row_layout(rows, cols, t, num_cus, e.rows_occ(short_rows));
+  const bool long_rows = !short_rows && cols * dtype_size(t) >= 65536;
+  const RowLayout L = row_layout(rows, cols, t, num_cus, wg_cap(e.rows_occ(short_rows), long_rows ? 2 : 0));
   kern::RowArgs a{};
   a.in = in;
   a.rows = rows;
@@ -547,7 +564,7 @@ DimPlan reduce_cols(const void* in, size_t outer, size_t rows, size_t cols, DTyp
   if (cols == 0 || outer == 0) return plan;
   MIREDUCE_REQUIRE(rows > 0, "reduce_cols: empty reduction axis");
   const bool vec = col_layout(in, outer, rows, cols, t, num_cus).vec;
-  const ColLayout L = col_layout(in, outer, rows, cols, t, num_cus, e.cols_occ(vec));
+  const ColLayout L = col_layout(in, outer, rows, cols, t, num_cus, wg_cap(e.cols_occ(vec), 1));
   kern::ColArgs a{};
   a.in = in;
   a.rows = rows;

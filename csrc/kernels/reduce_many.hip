@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <vector>
 
 #include "mireduce/check.hpp"
@@ -53,6 +54,7 @@ __global__ __launch_bounds__(kManyBlock) void many_kernel(ManyArgs a) {
   constexpr int U = kManyUnroll;
   constexpr int kWaves = kManyBlock / 64;
   __shared__ AccT lds[kWaves];
+  __shared__ int last;
   const int tid = threadIdx.x;
   // A workgroup streams one segment at a time (its 256 lanes read 4 KB contiguous per load
   // round): fewer, wider concurrent streams than a wave per segment (13 GB bf16 parameter list:
@@ -96,24 +98,37 @@ __global__ __launch_bounds__(kManyBlock) void many_kernel(ManyArgs a) {
     for (int off = 32; off > 0; off >>= 1) v = OpT::apply(v, __shfl_xor(v, off, 64));
     if ((tid & 63) == 0) lds[tid >> 6] = v;
     __syncthreads();
+    const TensorInfo ti = a.info[g.tensor];
     if (tid == 0) {
 #pragma unroll
       for (int w = 1; w < kWaves; ++w) v = OpT::apply(v, lds[w]);
-      const TensorInfo ti = a.info[g.tensor];
       AccT* out = static_cast<AccT*>(a.out);
       if (ti.nseg == 1) {
         out[g.tensor] = v;
+        last = 0;
       } else {
         AccT* part = static_cast<AccT*>(a.partials);
         store_sc1(&part[s], v);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned prev = __hip_atomic_fetch_add(&a.tickets[g.tensor], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == ti.nseg - 1) {  // last segment of this tensor: fold in segment order
-          __hip_atomic_store(&a.tickets[g.tensor], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          AccT t = OpT::template identity<AccT>();
-          for (uint32_t j = 0; j < ti.nseg; ++j) t = OpT::apply(t, load_sc1(&part[ti.first_seg + j]));
-          out[g.tensor] = t;
-        }
+        last = prev == ti.nseg - 1;
+        if (last) __hip_atomic_store(&a.tickets[g.tensor], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+    if (last) {  // last segment of this tensor: every lane folds a strided share of its partials
+      // (a fixed order — lane j takes j, j + 256, ... — then the fixed butterfly: deterministic)
+      const AccT* part = static_cast<const AccT*>(a.partials) + ti.first_seg;
+      AccT t = OpT::template identity<AccT>();
+      for (uint32_t j = tid; j < ti.nseg; j += kManyBlock) t = OpT::apply(t, load_sc1(&part[j]));
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) t = OpT::apply(t, __shfl_xor(t, off, 64));
+      if ((tid & 63) == 0) lds[tid >> 6] = t;
+      __syncthreads();
+      if (tid == 0) {
+#pragma unroll
+        for (int w = 1; w < kWaves; ++w) t = OpT::apply(t, lds[w]);
+        static_cast<AccT*>(a.out)[g.tensor] = t;
       }
     }
     __syncthreads();  // lds is rewritten by the next segment
@@ -214,6 +229,8 @@ BoundReduceMany::BoundReduceMany(const std::vector<const void*>& ptrs, const std
   uint64_t seg = total / std::max<uint64_t>(1, wgs * 4);
   seg = std::max<uint64_t>(seg, static_cast<uint64_t>(kern::kManyBlock) * kern::kManyUnroll * N);
   seg = std::min<uint64_t>(seg, (4ull << 20) / es);
+  if (const char* e = std::getenv("MIREDUCE_MANY_SEG_KB"); e && std::atoi(e) > 0)  // A/B runs
+    seg = std::max<uint64_t>(N, static_cast<uint64_t>(std::atoi(e)) * 1024 / es);
   seg = (seg + N - 1) / N * N;
   std::vector<kern::Seg> segs;
   std::vector<kern::TensorInfo> info(ptrs.size());
@@ -247,7 +264,9 @@ BoundReduceMany::BoundReduceMany(const std::vector<const void*>& ptrs, const std
   MIREDUCE_HIP_THROW(hipMemcpyAsync(static_cast<char*>(table_) + info_off, info.data(),
                                     info.size() * sizeof(kern::TensorInfo), hipMemcpyHostToDevice, stream));
   MIREDUCE_HIP_THROW(hipStreamSynchronize(stream));  // the host vectors die with this constructor
-  const int resident = many_lookup(op, t, acc).occ();
+  int resident = many_lookup(op, t, acc).occ();
+  if (const char* e = std::getenv("MIREDUCE_MANY_WG_PER_CU"); e && std::atoi(e) > 0)  // A/B runs
+    resident = std::min(resident, std::atoi(e));
   const uint64_t blocks = segs.size();
   grid_ = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(blocks, static_cast<uint64_t>(num_cus) * resident)));
   MIREDUCE_HIP_THROW(hipSetDevice(prev));

@@ -31,6 +31,7 @@
 #include <thread>
 #include <vector>
 
+#include "mireduce/arg_reduce.hpp"
 #include "mireduce/check.hpp"
 #include "mireduce/cli.hpp"
 #include "mireduce/cpu_reference.hpp"
@@ -71,13 +72,14 @@ struct Options {
   bool verify = true;
   std::string json;
   int device = 0;
+  bool arg = false;  // --arg: the position of the MIN/MAX too (arg_reduce.hpp)
 };
 
 const std::set<std::string> kKnown = {
     "method", "type", "n", "threads", "kernel", "maxblocks", "cpufinal", "cputhresh", "shmoo",
     "device", "qatest", "noprompt", "prompt", "help", "quiet", "iterations", "acc", "unroll",
     "wg-per-cu", "policy", "pattern", "seed", "fill", "noverify", "json", "log", "master-log",
-    "countdown", "shmoo-max", "trace", "timing", "cold"};
+    "countdown", "shmoo-max", "trace", "timing", "cold", "arg"};
 
 void usage() {
   std::printf(
@@ -97,7 +99,8 @@ void usage() {
       "  --pattern=smallint|uniform|fullrange|iotamod --seed=N --fill=host|device --noverify\n"
       "  --device=N --json=PATH --log=FILE|none --master-log=FILE|none (default SdkMasterLog.csv) --qatest\n"
       "  --prompt --countdown\n"
-      "  --trace          roctx ranges per iteration (rocprofv3 --marker-trace)\n");
+      "  --trace          roctx ranges per iteration (rocprofv3 --marker-trace)\n"
+      "  --arg            with MIN/MAX: also the first index of the extreme (arg-reduction kernel)\n");
 }
 
 size_t pick_threads_for_fill() {
@@ -239,6 +242,86 @@ std::string fmt_result(const unsigned char* p, DType acc) {
   if (dtype_is_float(acc)) std::snprintf(buf, sizeof buf, "%f", acc_as_double(p, acc));
   else std::snprintf(buf, sizeof buf, "%" PRId64, acc_as_int64(p, acc));
   return buf;
+}
+
+// --arg: first index of the minimum / maximum and its value (csrc/kernels/arg_reduce.hip),
+// verified against the host reference cpu_arg_reduce_rows (same first-occurrence rule).
+bool run_arg_test(const Options& o, Workspace& ws, hipStream_t s) {
+  Logger& L = Logger::instance();
+  L.log(kLogBoth, "METHOD: ARG%s\n", op_name(o.op));
+  L.log(kLogBoth, "%" PRIu64 " elements\n", o.n);
+  const size_t es = dtype_size(o.dtype);
+  DeviceBuffer in(std::max<uint64_t>(o.n, 1) * es), val(8), idx(8);
+  const size_t need = arg_reduce_scratch_bytes(1, o.n, o.dtype, ws.num_cus());
+  DeviceBuffer scratch(std::max<size_t>(need, 256));
+  HIP_CHECK(hipMemsetAsync(scratch.get(), 0, scratch.bytes(), s));
+  FillSpec fs;
+  fs.pattern = o.pattern;
+  fs.seed = o.seed;
+  std::vector<unsigned char> host;
+  const bool host_copy = !o.device_fill || (o.verify && o.n <= (1ull << 30));
+  if (host_copy) {
+    host.resize(o.n * es);
+    parallel_fill_host(host.data(), o.n, o.dtype, fs);
+  }
+  if (o.device_fill) fill_device(in.get(), o.n, o.dtype, fs, s);
+  else HIP_CHECK(hipMemcpy(in.get(), host.data(), o.n * es, hipMemcpyHostToDevice));
+  HIP_CHECK(hipDeviceSynchronize());
+  ArgTune tune;
+  tune.wg_per_cu = o.wg_per_cu;
+  tune.unroll = o.unroll;
+  auto once = [&] {
+    return arg_reduce_rows(in.get(), 1, o.n, o.dtype, o.op, val.get(), idx.as<int64_t>(), scratch.get(), ws.num_cus(),
+                           s, tune);
+  };
+  const ArgPlan plan = once();  // warm-up
+  HIP_CHECK(hipStreamSynchronize(s));
+  L.log(kLogBoth, "%d blocks\n\n", plan.grid);
+  EventTimer ev;
+  std::vector<double> ms;
+  if (o.batch_timing) {
+    ev.start(s);
+    for (int i = 0; i < o.iterations; ++i) once();
+    ev.stop(s);
+    ms.assign(o.iterations, ev.elapsed_ms() / o.iterations);
+  } else {
+    for (int i = 0; i < o.iterations; ++i) {
+      ev.start(s);
+      once();
+      ev.stop(s);
+      ms.push_back(ev.elapsed_ms());
+    }
+  }
+  double sum = 0;
+  for (double m : ms) sum += m;
+  const double secs = sum / ms.size() * 1e-3, bytes = static_cast<double>(o.n) * es;
+  L.log(kLogBoth | kLogMaster, "%s\n", throughput_line(secs > 0 ? 1.0e-9 * bytes / secs : 0.0, secs, o.n, 1,
+                                                       static_cast<unsigned>(plan.block)).c_str());
+  int64_t gi = 0;
+  unsigned char gv[8] = {0};
+  HIP_CHECK(hipMemcpy(&gi, idx.get(), 8, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(gv, val.get(), es, hipMemcpyDeviceToHost));
+  L.log(kLogBoth, "\nGPU result = index %" PRId64 "\n", gi);
+  bool ok = true;
+  if (o.verify && host_copy) {
+    int64_t ci = 0;
+    unsigned char cv[8] = {0};
+    cpu_arg_reduce_rows(host.data(), 1, o.n, o.dtype, o.op, cv, &ci);
+    L.log(kLogBoth, "CPU result = index %" PRId64 "\n\n", ci);
+    ok = gi == ci && std::memcmp(gv, cv, es) == 0;
+  }
+  if (!o.json.empty()) {
+    Stats st = compute_stats(ms);
+    Json j;
+    j.set("app", "reduction").set("method", std::string("ARG") + op_name(o.op)).set("type", dtype_cli_name(o.dtype))
+        .set("n", o.n).set("bytes", static_cast<uint64_t>(bytes)).set("grid", plan.grid).set("splits", plan.splits)
+        .set("unroll", plan.unroll).set("wg_per_cu", plan.wg_per_cu).set("iterations", o.iterations)
+        .set("avg_ms", secs * 1e3).set("median_ms", st.median).set("min_ms", st.min)
+        .set("gb_per_s", secs > 0 ? bytes / secs / kGB : 0.0).set("index", gi).set("verified", o.verify && host_copy)
+        .set("passed", ok);
+    j.write_file(o.json);
+  }
+  return ok;
 }
 
 bool run_test(Options& o, Workspace& ws, hipStream_t s) {
@@ -467,6 +550,10 @@ int main(int argc, char** argv) {
     if (o.kernel <= 6 && (o.threads < 64 || o.threads > 1024 || (o.threads & (o.threads - 1))))
       throw CliError("--threads must be a power of two in [64, 1024] for kernels 0..6");
     if (o.iterations < 1) throw CliError("--iterations must be >= 1");
+    o.arg = args.has("arg");
+    if (o.arg && o.op != Op::Min && o.op != Op::Max) throw CliError("--arg needs --method=MIN or MAX");
+    if (o.arg && (o.kernel != 7 || o.cpufinal || o.cputhresh > 1 || args.has("shmoo")))
+      throw CliError("--arg runs the arg-reduction kernel only (no --kernel/--cpufinal/--cputhresh/--shmoo)");
   } catch (const CliError& e) {
     std::fprintf(stderr, "error: %s\n", e.what());
     return EXIT_FAILURE;
@@ -493,6 +580,8 @@ int main(int argc, char** argv) {
     Workspace ws(o.device);
     if (args.has("shmoo")) {
       run_shmoo(o, ws, s, args.int_or<uint64_t>("shmoo-max", 33554432ull));
+    } else if (o.arg) {
+      ok = run_arg_test(o, ws, s);
     } else {
       ok = run_test(o, ws, s);
     }

@@ -2,6 +2,7 @@
 
     python -m cuda_mpi_reductions_amd --method=SUM --type=double --n=268435456 [--iterations=100]
         [--qatest] [--device=0] [--acc=double] [--pattern=smallint|uniform|fullrange|iotamod] [--json=PATH]
+        [--arg]   (with MIN/MAX: the first index of the extreme too — ops.arg_reduce)
 
 Same flags and lines as the native `reduction` app (cuda/C/src/reduction/reduction.cpp:84-204):
 QA banner, "METHOD: ...", "<n> elements", the "Reduction, Throughput = ..." line (GB = 1e9 B),
@@ -74,6 +75,8 @@ def main(argv=None) -> int:
     print(f"METHOD: {method}\n{n} elements")
     x = torch.empty(n, dtype=dt, device=dev)
     fill_(x, cli.get_str(args, "pattern") or "smallint", seed=cli.get_int(args, "seed", 1))
+    if cli.has(args, "arg"):
+        return _arg_main(argv, args, x, op, iters)
     r = Reducer(dev, config=KernelConfig())
     out = torch.empty(1, dtype=acc, device=dev)
     r(x, op, acc, out=out)  # warm-up
@@ -113,6 +116,40 @@ def main(argv=None) -> int:
             f.write(json.dumps({"app": "python-reduction", "method": method, "type": tname, "n": n,
                                 "gb_per_s": 1e-9 * nbytes / secs if secs else None, "avg_s": secs,
                                 "plan": plan, "verified": bool(ok)}) + "\n")
+    _qa(argv, "PASSED" if ok else "FAILED")
+    return 0 if ok else 1
+
+
+def _arg_main(argv, args, x, op, iters) -> int:
+    """--arg: time ops.arg_reduce (first index of the MIN/MAX) and check it against torch.argmin/argmax."""
+    import torch
+
+    from .ops import arg_reduce
+    if op not in ("min", "max"):
+        print("error: --arg needs --method=MIN or MAX", file=sys.stderr)
+        _qa(argv, "FAILED")
+        return 1
+    arg_reduce(x, op)  # warm-up
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        v, i = arg_reduce(x, op)
+    e1.record()
+    e1.synchronize()
+    secs = e0.elapsed_time(e1) / iters * 1e-3
+    n, nbytes = x.numel(), x.numel() * x.element_size()
+    print(throughput_line(1e-9 * nbytes / secs if secs else 0.0, secs, n, 1, 256))
+    ref = int((x.argmax() if op == "max" else x.argmin()).item())
+    got = int(i.item())
+    ok = got == ref
+    print(f"\nGPU result = index {got}\nCPU result = index {ref}\n")
+    jpath = cli.get_str(args, "json")
+    if jpath:
+        with open(jpath, "a") as f:
+            f.write(json.dumps({"app": "python-reduction", "method": "ARG" + op.upper(), "n": n,
+                                "gb_per_s": 1e-9 * nbytes / secs if secs else None, "avg_s": secs, "index": got,
+                                "verified": bool(ok)}) + "\n")
     _qa(argv, "PASSED" if ok else "FAILED")
     return 0 if ok else 1
 

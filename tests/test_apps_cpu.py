@@ -111,3 +111,10 @@ def test_reduce_xgmi_bootstrap_env_parsing():
     assert r.returncode == 1 and "no HIP device" in r.stderr
     r = run([os.path.join(BIN, "reduce_xgmi"), "--mode=bogus"])
     assert r.returncode == 1 and "--mode must be" in r.stderr
+
+
+def test_reduction_arg_needs_min_or_max(tmp_path):
+    r = run([os.path.join(BIN, "reduction"), "--method=SUM", "--arg"], cwd=tmp_path)
+    assert r.returncode != 0 and "--arg needs --method=MIN or MAX" in r.stderr
+    r = run([os.path.join(BIN, "reduction"), "--method=MAX", "--arg", "--kernel=3"], cwd=tmp_path)
+    assert r.returncode != 0 and "arg-reduction kernel only" in r.stderr

@@ -47,6 +47,22 @@ def test_reduction_app_paths(tmp_path, flags):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("method,type_,pattern", [("MAX", "double", "uniform"), ("MIN", "int", "smallint"),
+                                                    ("MAX", "bf16", "uniform"), ("MIN", "int64", "fullrange")])
+def test_reduction_app_arg(tmp_path, method, type_, pattern):
+    out = tmp_path / "arg.json"
+    r = reduction(tmp_path, f"--method={method}", f"--type={type_}", "--arg", "--n=30000017", f"--pattern={pattern}",
+                  "--iterations=5", f"--json={out}")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert re.search(r"&&&& PASSED reduction", r.stderr)
+    gi = re.search(r"GPU result = index (\d+)", r.stdout).group(1)
+    ci = re.search(r"CPU result = index (\d+)", r.stdout).group(1)
+    assert gi == ci
+    import json
+    j = json.loads(out.read_text())
+    assert j["method"] == "ARG" + method and j["passed"] and j["verified"] and j["index"] == int(gi)
+
+
 def test_reduction_app_json_and_log(tmp_path):
     r = run([os.path.join(BIN, "reduction"), "--method=SUM", "--type=double", "--n=1M", "--iterations=4",
              "--json=out.jsonl", "--master-log=master.csv"], cwd=tmp_path, timeout=300)

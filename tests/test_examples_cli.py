@@ -40,6 +40,15 @@ def test_python_cli_gpu(method, type_):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("method,type_", [("MAX", "double"), ("MIN", "bf16")])
+def test_python_cli_gpu_arg(method, type_):
+    r = run([sys.executable, "-m", "cuda_mpi_reductions_amd", f"--method={method}", f"--type={type_}", "--arg",
+             "--n=4000037", "--iterations=5", "--pattern=uniform", "--qatest"], cwd=ROOT, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "&&&& PASSED" in r.stderr and "GPU result = index" in r.stdout
+
+
+@pytest.mark.gpu
 def test_example_single_gpu():
     r = run([sys.executable, os.path.join(ROOT, "examples", "01_single_gpu.py")], cwd=ROOT, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]

@@ -406,7 +406,11 @@ struct Defaults {
 };
 Defaults tuned_defaults(size_t bytes, DType t) {
   constexpr size_t MB = 1ull << 20;
-  if (t == DType::Float64 && bytes >= 3072 * MB) return {512, 16, 1, 1, 0};
+  // >= 3 GB: one 512-thread workgroup per CU (tools/tune_types.sh, profiles/r1_session3/tune_types.txt):
+  // 8-byte types 16 vectors in flight per lane (f64 7.30, i64 7.30 TB/s vs 7.16 at 256x2x3),
+  // 4-byte types 4 (f32 7.17, i32 7.19 vs 7.14).
+  if (dtype_size(t) == 8 && bytes >= 3072 * MB) return {512, 16, 1, 1, 0};
+  if (dtype_size(t) == 4 && bytes >= 3072 * MB) return {512, 4, 1, 1, 0};
   if (dtype_is_half(t) && bytes > 192 * MB) return {256, 4, 2, 1, 0};
   if (bytes > 192 * MB) return {256, 2, 3, 1, 0};
   return {256, 4, 3, 1, 0};

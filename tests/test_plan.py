@@ -49,8 +49,12 @@ def test_tuned_defaults_by_size():
     assert (l3["block"], l3["unroll"], l3["grid"], l3["nontemporal"]) == (256, 2, 768, True)
     # no size band picks the default (non-nt) policy: it collapses to 2.7 TB/s on a cold cache
     assert all(C.plan(0, n, F64)["nontemporal"] for n in (1, 1 << 20, 3 << 23, 1 << 25, 3 << 24, 1 << 27))
-    f32 = C.plan(0, 2 * 10**9, 2)          # 8 GB of fp32
-    assert (f32["block"], f32["unroll"]) == (256, 2)
+    f32 = C.plan(0, 2 * 10**9, 2)          # 8 GB of fp32: one 512-thread WG per CU, 4 vectors per lane
+    assert (f32["block"], f32["unroll"], f32["grid"]) == (512, 4, 256)
+    i64 = C.plan(0, 10**9, 1)              # 8 GB of int64: like fp64
+    assert (i64["block"], i64["unroll"], i64["grid"]) == (512, 16, 256)
+    f32_1g = C.plan(0, 250_000_000, 2)     # 1 GB keeps the 256x2x3 plan
+    assert (f32_1g["block"], f32_1g["unroll"]) == (256, 2)
 
 
 def test_overrides_and_caps():

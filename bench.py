@@ -31,7 +31,7 @@ import time
 import torch
 
 from cuda_mpi_reductions_amd._native import native, native_path
-from cuda_mpi_reductions_amd.models import CONFIGS, NORTH_STAR, ScalarReduction
+from cuda_mpi_reductions_amd.models import CONFIGS, LOC_OPS, NORTH_STAR, scalar_workload
 from cuda_mpi_reductions_amd.ops import KernelConfig
 from cuda_mpi_reductions_amd.parallel import dist as pdist
 from cuda_mpi_reductions_amd.utils.fault import FaultInjector
@@ -92,6 +92,13 @@ def _time_torch_reduction(wl, K: int, W: int, ctx) -> float:
     acc = wl.acc
 
     def step():
+        if op in LOC_OPS:  # torch.argmax / argmin of the shard, then the same MAXLOC/MINLOC combine
+            kind = LOC_OPS[op]
+            i = x.argmax() if kind == "max" else x.argmin()
+            r = (i + wl.offset).reshape(1)
+            if ctx.world_size > 1:
+                _, r = pdist.loc_allreduce(x[i].reshape(1), r, kind)
+            return r
         if op == "sum":
             r = x.sum(dtype=acc).reshape(1)
         elif op == "sumsq":  # torch's one-pass fused form of the same quantity
@@ -193,7 +200,7 @@ def main(argv=None) -> int:
                           groups=args.groups,
                           nontemporal=None if args.policy == "auto" else args.policy == "nt",
                           single_pass=not args.two_pass)
-    wl = ScalarReduction(cfg, ctx, kernel, streams=1 if args.serial else args.streams).setup()
+    wl = scalar_workload(cfg, ctx, kernel, streams=1 if args.serial else args.streams).setup()
     K, W = args.steps, args.warmup
     slots = wl.new_slots(W + K)
     dev = ctx.device
@@ -295,7 +302,7 @@ def main(argv=None) -> int:
                 "overlap": "serial" if args.serial else "pipelined (step i+1 local reduce || step i all-reduce)",
                 "streams": len(wl.lanes) if wl.lanes else 1,
                 "launch": launch,
-                "kernel_plan": wl.reducer.last_plan if wl.reducer else None,
+                "kernel_plan": wl.reducer.last_plan if wl.reducer else getattr(wl, "plan", None),
             },
             "per_gpu_gbps": round(gbps / ctx.world_size, 3),
             "baseline_value": cfg.baseline,

@@ -73,6 +73,11 @@ CONFIGS: dict[str, WorkloadConfig] = {
         description="sum of squares (squared L2 norm) of 1e9 doubles across N GPUs, square fused into the "
                     "load (MI355X addition; not a reference config)",
     ),
+    "xgmi_1b_double_maxloc": WorkloadConfig(
+        name="xgmi_1b_double_maxloc", dtype=torch.float64, op="maxloc", n_total=1_000_000_000,
+        description="MPI_MAXLOC of 1e9 doubles across N GPUs: local arg-reduction + all-gather of (value, "
+                    "index) pairs over RCCL (MI355X addition; not a reference config)",
+    ),
     "gpu_4g_bf16_sum": WorkloadConfig(
         name="gpu_4g_bf16_sum", dtype=torch.bfloat16, op="sum", n_total=4_000_000_000,
         description="4e9 bfloat16 (8 GB) sum, fp32 accumulation (MI355X addition; not a reference config)",

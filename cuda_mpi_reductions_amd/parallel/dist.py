@@ -25,7 +25,7 @@ import torch
 import torch.distributed as dist
 
 __all__ = ["DistContext", "init", "shutdown", "shard", "reduce_op", "scalar_allreduce",
-           "vector_reduce", "vector_allreduce", "barrier", "max_over_ranks"]
+           "vector_reduce", "vector_allreduce", "loc_allreduce", "barrier", "max_over_ranks"]
 
 # The fused ops exchange already-transformed partials (sum of x^2, max |x|) and combine them
 # like SUM / MAX across ranks.
@@ -150,6 +150,35 @@ def vector_allreduce(t: torch.Tensor, op: str = "sum", async_op: bool = False):
 def vector_reduce(t: torch.Tensor, op: str = "sum", root: int = 0, async_op: bool = False):
     """Element-wise reduce to ``root`` — the ``MPI_Reduce`` of mpi/reduce.c:76,90."""
     return dist.reduce(t, dst=root, op=reduce_op(op), async_op=async_op)
+
+
+def loc_allreduce(value: torch.Tensor, index: torch.Tensor, op: str = "max", group=None):
+    """``MPI_MAXLOC`` / ``MPI_MINLOC`` of one (value, global index) pair per rank: every rank gets
+    the extreme value and, among the ranks holding it, the smallest index (NaN is the extreme, as
+    in :func:`ops.arg_reduce`). Two 1-element all-gathers, then a device-side pick — no host
+    synchronisation, so it can be captured into a hipGraph with the local arg-reduction."""
+    if op not in ("max", "min"):
+        raise ValueError("loc_allreduce: op must be 'max' or 'min'")
+    world = dist.get_world_size(group)
+    v = value.reshape(1)
+    i = index.reshape(1).to(torch.int64)
+    if dist.get_backend(group) == "gloo" and v.device.type != "cpu":
+        hv, hi = loc_allreduce(v.cpu(), i.cpu(), op, group)
+        return hv.to(v.device), hi.to(v.device)
+    vals = torch.empty(world, dtype=v.dtype, device=v.device)
+    idxs = torch.empty(world, dtype=torch.int64, device=v.device)
+    if dist.get_backend(group) == "gloo":
+        dist.all_gather(list(vals.chunk(world)), v, group=group)
+        dist.all_gather(list(idxs.chunk(world)), i, group=group)
+    else:
+        dist.all_gather_into_tensor(vals, v, group=group)
+        dist.all_gather_into_tensor(idxs, i, group=group)
+    best = vals.amax() if op == "max" else vals.amin()  # torch propagates NaN, like arg_reduce
+    same = vals == best
+    if vals.is_floating_point():
+        same = same | (torch.isnan(vals) & torch.isnan(best))
+    cand = torch.where(same, idxs, torch.full_like(idxs, torch.iinfo(torch.int64).max))
+    return best.reshape(1), cand.min().reshape(1)
 
 
 def max_over_ranks(value: float, ctx: DistContext) -> float:

@@ -227,3 +227,14 @@ def test_reduction_cold_cache_mode(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     d = json.loads(js.read_text().splitlines()[-1])
     assert d["cold"] is True and d["timing"] == "per-iter" and d["verified"] is True
+
+
+@pytest.mark.parametrize("launch", ["graph", "eager"])
+def test_bench_maxloc_config(tmp_path, launch):
+    r = run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "xgmi_1b_double_maxloc", "--steps", "20",
+             "--warmup", "3", "--elements", "50000017", "--launch", launch], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["verified"] is True and d["config"]["op"] == "MAXLOC"
+    assert d["config"]["launch"].startswith(launch)
+    assert d["config"]["kernel_plan"]["splits"] > 1

@@ -154,3 +154,46 @@ def test_moments_across_ranks():
         mean, var, mn, mx = res["ref"]
         assert res["count"] == 100_003 and res["min"] == mn and res["max"] == mx
         assert abs(res["mean"] - mean) < 1e-12 and abs(res["var"] - var) < 1e-12
+
+
+def loc_case(rank, world):
+    from dataclasses import replace
+    from cuda_mpi_reductions_amd.models import CONFIGS, scalar_workload
+    from cuda_mpi_reductions_amd.ops import synthetic
+    from cuda_mpi_reductions_amd.parallel import dist as pdist
+    ctx = pdist.init(device_type="cpu")
+    res = {}
+    # MAXLOC / MINLOC workload: global index equals torch's argmax of the whole (unsharded) array
+    for op in ("maxloc", "minloc"):
+        cfg = replace(CONFIGS["xgmi_1b_double_maxloc"], op=op, n_total=300_007)
+        wl = scalar_workload(cfg, ctx).setup()
+        out = wl.new_slots(1)
+        wl.step(out)
+        full = synthetic(300_007, torch.float64, seed=0x5EED)
+        exp = int(full.argmax() if op == "maxloc" else full.argmin())
+        res[op] = (wl.verify(out)["ok"], int(out[0]) == exp)
+    # ties across ranks: the smallest global index wins; a NaN anywhere wins for both ops
+    v = torch.tensor([5.0])
+    i = torch.tensor([10 * (world - rank)])  # higher ranks hold the smaller indices
+    res["tie"] = [float(x) for x in pdist.loc_allreduce(v, i, "max")] == [5.0, 10.0]
+    v = torch.tensor([float("nan") if rank in (1, 2) else float(rank)])
+    res["nan_max"] = int(pdist.loc_allreduce(v, torch.tensor([100 + rank]), "max")[1]) == 101
+    res["nan_min"] = int(pdist.loc_allreduce(v, torch.tensor([100 + rank]), "min")[1]) == 101
+    pdist.shutdown(ctx)
+    return res
+
+
+def test_loc_reduction_three_ranks():
+    out = _spawn("loc_case", 3)
+    for rank, res in out.items():
+        assert isinstance(res, dict), res
+        assert res["maxloc"] == (True, True) and res["minloc"] == (True, True), res
+        assert res["tie"] and res["nan_max"] and res["nan_min"], res
+
+
+def test_bench_maxloc_config_two_cpu_ranks(tmp_path):
+    r = torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                     "--device", "cpu", "--config", "xgmi_1b_double_maxloc", "--elements", "200003"], cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["verified"] is True and d["config"]["op"] == "MAXLOC" and d["n_gpus"] == 2

@@ -60,3 +60,17 @@ def test_example_norms_dims_many():
     r = run([sys.executable, os.path.join(ROOT, "examples", "04_norms_dims_many.py")], timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "per-tensor sum of squares" in r.stdout and "total grad-norm-style L2" in r.stdout
+
+
+def test_example_argmax_maxloc_cpu(tmp_path):
+    r = torchrun(2, [os.path.join(ROOT, "examples", "05_argmax_maxloc.py"), "--cpu"], cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.count("match torch: True") == 2
+    assert r.stdout.count("arg_reduce agrees: True") == 2
+
+
+@pytest.mark.gpu
+def test_example_argmax_maxloc():
+    r = run([sys.executable, os.path.join(ROOT, "examples", "05_argmax_maxloc.py")], cwd=ROOT, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "match torch: True" in r.stdout and "arg_reduce agrees: True" in r.stdout

@@ -43,6 +43,7 @@ struct LaunchPlan {
   bool pipelined = false;
   bool single_pass = true;
   bool flat = false;   // single-pass fan-in: flat (final arriver folds every partial) vs two-level
+  bool contiguous = false;  // body split: one contiguous run of tiles per workgroup vs interleaved
   uint64_t head = 0;   // scalar elements before the first 16-B aligned vector
   uint64_t nvec = 0;   // 16-byte vectors in the streaming body
   uint64_t tail = 0;   // scalar elements after the body

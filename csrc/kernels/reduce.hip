@@ -70,6 +70,7 @@ struct Args {
   void* out;             // AccT[1]
   int groups;            // 0: two-pass mode (write partials only)
   int flat;              // 1: group last-arrivers only count; the final arriver folds every partial
+  int contig;            // 1: workgroup b streams one contiguous run of tiles; 0: tiles b, b+grid, ...
 };
 
 template <class V, int BLOCK, int UNROLL, bool NT>
@@ -107,11 +108,17 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   const V* __restrict__ vin = static_cast<const V*>(a.body);
   constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
   const uint64_t ntiles = a.nvec / kTile;
+  // This workgroup's full tiles: t0, t0 + step, ... < t1 (interleaved over the grid, or one
+  // contiguous run of ntiles / grid tiles each).
+  const uint64_t grid = gridDim.x;
+  const uint64_t t0 = a.contig ? blockIdx.x * ntiles / grid : blockIdx.x;
+  const uint64_t t1 = a.contig ? (blockIdx.x + 1) * ntiles / grid : ntiles;
+  const uint64_t step = a.contig ? 1 : grid;
   if constexpr (PIPE) {
-    if (blockIdx.x < ntiles) {
+    if (t0 < t1) {
       V cur[UNROLL];
-      load_tile<V, BLOCK, UNROLL, NT>(cur, vin + blockIdx.x * kTile + threadIdx.x);
-      for (uint64_t tn = blockIdx.x + static_cast<uint64_t>(gridDim.x); tn < ntiles; tn += gridDim.x) {
+      load_tile<V, BLOCK, UNROLL, NT>(cur, vin + t0 * kTile + threadIdx.x);
+      for (uint64_t tn = t0 + step; tn < t1; tn += step) {
         V nxt[UNROLL];
         load_tile<V, BLOCK, UNROLL, NT>(nxt, vin + tn * kTile + threadIdx.x);
         consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, cur);
@@ -121,7 +128,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, cur);
     }
   } else {
-    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (uint64_t t = t0; t < t1; t += step) {
       V v[UNROLL];
       load_tile<V, BLOCK, UNROLL, NT>(v, vin + t * kTile + threadIdx.x);
       consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, v);
@@ -428,6 +435,15 @@ bool fanin_flat() {
   return v == 1;
 }
 
+// Work split of the streaming body; MIREDUCE_SPLIT=stride|contig overrides (A/B runs; read per
+// plan so one process can compare both).
+bool split_contiguous() {
+  const char* e = std::getenv("MIREDUCE_SPLIT");
+  if (e && std::strcmp(e, "contig") == 0) return true;
+  if (e && std::strcmp(e, "stride") == 0) return false;
+  return false;
+}
+
 template <class OpT, class AccT>
 void launch_finalize(const void* partials, uint64_t count, void* out, hipStream_t s) {
   hipLaunchKernelGGL((kern::finalize<OpT, AccT>), dim3(1), dim3(256), 0, s,
@@ -537,6 +553,7 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   if (groups > p.grid) groups = p.grid;
   p.groups = p.single_pass ? groups : 0;
   p.flat = p.single_pass && fanin_flat();
+  p.contiguous = split_contiguous();
   return p;
 }
 
@@ -547,6 +564,7 @@ static kern::Args make_args(const void* in, const LaunchPlan& p, DType t) {
   a.head = p.head;
   a.nvec = p.nvec;
   a.tail = p.tail;
+  a.contig = p.contiguous ? 1 : 0;
   return a;
 }
 

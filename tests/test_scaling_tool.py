@@ -1,0 +1,57 @@
+"""tools/scaling.py: bench.py JSON -> reference results format (getAvgs.sh / makePlots.gp)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import scaling  # noqa: E402
+
+
+def _line(n, value, ms, model="xgmi_1b_double_sum: 1B double sum", op="SUM", dtype="fp64"):
+    return {"metric": "reduction bandwidth (GB/s, whole node), 1B-double sum at 1/2/4/8 MI355X",
+            "value": value, "unit": "GB/s", "n_gpus": n, "steps": 50, "warmup": 10,
+            "ms_per_step": ms, "dtype": dtype, "config": {"model": model, "op": op}}
+
+
+def test_parse_jsonl_mixed_with_logs_and_nested_documents():
+    text = "RCCL version : x\n" + json.dumps(_line(1, 7300.0, 1.0959)) + "\nnoise {not json\n"
+    assert [r["n_gpus"] for r in scaling.parse_text(text)] == [1]
+    doc = {"runs": [{"n": 2, "result": _line(2, 14000.0, 0.5714)}, _line(4, 27000.0, 0.2963)]}
+    assert sorted(r["n_gpus"] for r in scaling.parse_text(json.dumps(doc))) == [2, 4]
+
+
+def test_summary_averages_repeats_and_efficiency():
+    rs = [_line(1, 7300.0, 1.0), _line(1, 7100.0, 1.2), _line(2, 14000.0, 0.57), _line(8, 50400.0, 0.16)]
+    s = scaling.summarise(rs)
+    per_n = s[("xgmi_1b_double_sum", "DOUBLE", "SUM")]
+    assert per_n[1]["gbps"] == 7200.0 and per_n[1]["runs"] == 2 and abs(per_n[1]["ms"] - 1.1) < 1e-12
+    eff = scaling.efficiency(per_n)
+    assert abs(eff[8][0] - 7.0) < 1e-12 and abs(eff[8][1] - 0.875) < 1e-12
+    assert scaling.efficiency({2: {"gbps": 1.0}})[2] == (None, None)
+
+
+def test_cli_writes_results_files_readable_by_plot_and_getavgs(tmp_path):
+    src = tmp_path / "scale.jsonl"
+    src.write_text("\n".join(json.dumps(_line(n, 7300.0 * n * 0.95 ** (n > 1), 8.0 / (7.3 * n)))
+                             for n in (1, 2, 4, 8)) + "\n")
+    out = tmp_path / "res"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling.py"), str(src), "--out", str(out)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert "| 8 |" in r.stdout and "95.0 %" in r.stdout
+    rows = (out / "DOUBLE_SUM.txt").read_text().split("\n")
+    assert rows[0] == ""  # getAvgs.sh writes a leading blank line
+    assert rows[1].split()[:3] == ["DOUBLE", "SUM", "1"] and len(rows[1].split()) == 4
+    import plot  # the unchanged reader used for the reference-style figures
+    assert [n for n, _ in plot.read_results(str(out / "DOUBLE_SUM.txt"))] == [1, 2, 4, 8]
+
+
+def test_cli_without_results_fails(tmp_path):
+    empty = tmp_path / "e.txt"
+    empty.write_text("nothing here\n")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling.py"), str(empty),
+                        "--out", str(tmp_path / "o")], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "no bench.py results" in r.stderr

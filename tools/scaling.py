@@ -1,0 +1,136 @@
+#!/usr/bin/env python3
+"""Scaling curve from bench.py JSON lines -> the reference's results format and a scaling table.
+
+The reference's pipeline is: per-run stdout rows ``DATATYPE OP NODES GB/sec`` (mpi/reduce.c:81,95)
+-> mpi/getAvgs.sh:3-14 (mean of column 4 per DATATYPE x OP x NODES into results/<DT>_<OP>.txt,
+starting with a blank line) -> mpi/makePlots.gp:1-40 (``using 3:4``). This tool feeds the headline
+benchmark into the same pipeline: it collects every bench.py result object (one JSON line per run,
+or any JSON document holding such objects, e.g. the driver's scaling file), groups them by
+(config, n_gpus), averages repeated runs like getAvgs.sh, and writes
+
+* ``<out>/<DT>_<OP>.txt``      rows ``DOUBLE SUM <N> <GB/s>`` (GB = 1e9 B, bench.py's unit),
+                               readable by tools/plot.py and tools/makePlots.gp unchanged;
+* ``<out>/scaling.md``         N, GB/s, ms/step, speed-up over N=1 and efficiency.
+
+Efficiency = value(N) / (N * value(1)): the whole-node bandwidth of N GPUs against N copies of the
+1-GPU run (bench.py's headline is strong scaling, so this is also t(1) / (N * t(N))).
+
+    python tools/scaling.py SCALE_r01.json bench_*.json --out results/scaling
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+from collections import defaultdict
+
+_DT = {"fp64": "DOUBLE", "float64": "DOUBLE", "fp32": "FLOAT", "float32": "FLOAT",
+       "int32": "INT", "int64": "LONG", "bf16": "BF16", "bfloat16": "BF16", "fp16": "HALF"}
+
+
+def _walk(obj):
+    """Yield every dict in a JSON document that looks like a bench.py result."""
+    if isinstance(obj, dict):
+        if "n_gpus" in obj and "value" in obj and "metric" in obj:
+            yield obj
+        else:
+            for v in obj.values():
+                yield from _walk(v)
+    elif isinstance(obj, list):
+        for v in obj:
+            yield from _walk(v)
+
+
+def parse_text(text: str):
+    """Bench results from a whole-file JSON document, or from JSON lines mixed with other output."""
+    try:
+        return list(_walk(json.loads(text)))
+    except ValueError:
+        pass
+    out = []
+    for line in text.splitlines():
+        line = line.strip()
+        if line.startswith("{"):
+            try:
+                out.extend(_walk(json.loads(line)))
+            except ValueError:
+                continue
+    return out
+
+
+def key_of(r):
+    cfg = r.get("config") or {}
+    model = str(cfg.get("model", "")).split(":")[0] or "bench"
+    dt = _DT.get(str(r.get("dtype", "")).lower(), str(r.get("dtype", "")).upper() or "DOUBLE")
+    op = str(cfg.get("op", "SUM")).upper()
+    return model, dt, op
+
+
+def summarise(results):
+    """{(model, DT, OP): {N: {"gbps": mean value, "ms": mean ms/step, "runs": k}}}."""
+    acc = defaultdict(lambda: defaultdict(list))
+    for r in results:
+        if r.get("value") is None:
+            continue
+        acc[key_of(r)][int(r["n_gpus"])].append(r)
+    out = {}
+    for k, per_n in acc.items():
+        out[k] = {}
+        for n, rs in sorted(per_n.items()):
+            ms = [float(r["ms_per_step"]) for r in rs if r.get("ms_per_step") is not None]
+            out[k][n] = {"gbps": sum(float(r["value"]) for r in rs) / len(rs),
+                         "ms": sum(ms) / len(ms) if ms else None, "runs": len(rs)}
+    return out
+
+
+def efficiency(per_n):
+    """{N: (speed-up over N=1, efficiency)}; None where there is no N=1 point."""
+    base = per_n.get(1, {}).get("gbps")
+    return {n: ((v["gbps"] / base, v["gbps"] / (n * base)) if base else (None, None))
+            for n, v in per_n.items()}
+
+
+def write(summary, out_dir):
+    os.makedirs(out_dir, exist_ok=True)
+    md = ["| config | dtype | op | N | GB/s (whole node) | ms/step | speed-up | efficiency | runs |",
+          "|---|---|---|---|---|---|---|---|---|"]
+    for (model, dt, op), per_n in sorted(summary.items()):
+        with open(os.path.join(out_dir, f"{dt}_{op}.txt"), "w") as f:
+            f.write("\n")  # getAvgs.sh:5-6 starts each results file with a blank line
+            for n, v in per_n.items():
+                f.write(f"{dt} {op} {n} {v['gbps']:.5f}\n")
+        eff = efficiency(per_n)
+        for n, v in per_n.items():
+            s, e = eff[n]
+            ms = "" if v["ms"] is None else "%.4f" % v["ms"]
+            sp = "" if s is None else "%.2fx" % s
+            ef = "" if e is None else "%.1f %%" % (100 * e)
+            md.append(f"| {model} | {dt} | {op} | {n} | {v['gbps']:.1f} | {ms} | {sp} | {ef} | {v['runs']} |")
+    text = "\n".join(md) + "\n"
+    with open(os.path.join(out_dir, "scaling.md"), "w") as f:
+        f.write(text)
+    return text
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("inputs", nargs="*", help="files with bench.py JSON (default: stdin)")
+    ap.add_argument("--out", default="results/scaling")
+    a = ap.parse_args(argv)
+    results = []
+    if a.inputs:
+        for p in a.inputs:
+            with open(p) as f:
+                results.extend(parse_text(f.read()))
+    else:
+        results.extend(parse_text(sys.stdin.read()))
+    if not results:
+        print("[scaling] no bench.py results found", file=sys.stderr)
+        return 1
+    print(write(summarise(results), a.out), end="")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -312,13 +312,16 @@ bool run_arg_test(const Options& o, Workspace& ws, hipStream_t s) {
   }
   if (!o.json.empty()) {
     Stats st = compute_stats(ms);
+    DeviceInfo di = device_info(o.device);
     Json j;
     j.set("app", "reduction").set("method", std::string("ARG") + op_name(o.op)).set("type", dtype_cli_name(o.dtype))
         .set("n", o.n).set("bytes", static_cast<uint64_t>(bytes)).set("grid", plan.grid).set("splits", plan.splits)
         .set("unroll", plan.unroll).set("wg_per_cu", plan.wg_per_cu).set("iterations", o.iterations)
-        .set("avg_ms", secs * 1e3).set("median_ms", st.median).set("min_ms", st.min)
-        .set("gb_per_s", secs > 0 ? bytes / secs / kGB : 0.0).set("index", gi).set("verified", o.verify && host_copy)
-        .set("passed", ok);
+        .set("avg_ms", secs * 1e3).set("median_ms", st.median).set("min_ms", st.min).set("max_ms", st.max)
+        .set("std_ms", st.stddev).set("gb_per_s", secs > 0 ? bytes / secs / kGB : 0.0)
+        .set("gib_per_s", secs > 0 ? bytes / secs / kGiB : 0.0).set("bytes_per_GB", kGB).set("index", gi)
+        .set("verified", o.verify && host_copy).set("passed", ok).set("device", di.name).set("arch", di.arch)
+        .set("cus", di.cus).set("iteration_ms", ms);
     j.write_file(o.json);
   }
   return ok;

@@ -61,6 +61,8 @@ def test_reduction_app_arg(tmp_path, method, type_, pattern):
     import json
     j = json.loads(out.read_text())
     assert j["method"] == "ARG" + method and j["passed"] and j["verified"] and j["index"] == int(gi)
+    assert len(j["iteration_ms"]) == 5 and j["min_ms"] <= j["median_ms"] <= j["max_ms"] and j["bytes_per_GB"] == 1e9
+    assert j["arch"].startswith("gfx950") and j["cus"] > 0
 
 
 def test_reduction_app_json_and_log(tmp_path):

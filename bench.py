@@ -10,13 +10,23 @@ counter-based U[0,1) fill, untimed) and fixed in size as N grows -> strong scali
 
 Timing: W untimed warm-up steps; then barrier + synchronize, K timed steps, synchronize; the
 MAX elapsed time over ranks defines the measurement. Value = total bytes reduced per step x K /
-elapsed / 1e9 (GB = 1e9 B, the CUDA sample's unit, reduction.cpp:744-745). Steps are
-independent reductions, so by default step i+1's local reduce overlaps step i's all-reduce
-(RCCL runs on its own stream); ``--serial`` makes each step wait for its all-reduce.
-By default the K timed steps are replayed from captured hipGraphs (``--launch``; chunks of up to 128
-steps, captured after the W eager warm-up steps and replayed once untimed): eager Python issue of the
-RCCL all-reduce leaves ~22 us GPU gaps per step, which at N=8 (0.14 ms per step) would cost ~15 %.
-Every step's result is checked after timing against torch's own fp64 reduction of the shards.
+elapsed / 1e9 (GB = 1e9 B, the CUDA sample's unit, reduction.cpp:744-745).
+
+Cross-rank combine (``--collective``): ``rccl`` = a 1-element RCCL all-reduce after the local
+kernel (on RCCL's stream); ``fused`` = the local kernel's last workgroup exchanges the partials
+through IPC-mapped mailboxes over xGMI and folds them itself (csrc/include/mireduce/xrank.hpp),
+one kernel per step. The combine is issued even at N=1 (``--local-only`` skips it), so the 1-GPU
+run executes exactly the N-GPU step.
+
+Two measurements per run: the headline ``value`` is pipelined (independent steps: step i+1's
+local reduce overlaps step i's all-reduce, which runs on its own stream); ``serial_gbps`` /
+``serial_ms_per_step`` time each step to completion before the next starts (the reference's
+per-reduction timing, reduction.cpp:319-374). ``--serial`` makes the serial number the headline.
+Both are replayed from captured hipGraphs by default (``--launch``; chunks of up to 128 steps,
+captured after eager warm-up steps and replayed once untimed): eager Python issue of the RCCL
+all-reduce leaves ~22 us GPU gaps per step, which at N=8 (0.14 ms per step) would cost ~15 %.
+Every step's result is checked after timing against torch's own fp64 reduction of the shards
+(AND over ranks).
 
 Reference number: 92.7729 GB/s (CUDA DOUBLE SUM, mpi/CUdata.txt:2).
 """
@@ -47,7 +57,15 @@ def parse_args(argv=None):
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default=NORTH_STAR, choices=sorted(CONFIGS))
     p.add_argument("--elements", type=int, default=None, help="override the global element count")
-    p.add_argument("--serial", action="store_true", help="no overlap between consecutive steps")
+    p.add_argument("--serial", action="store_true",
+                   help="headline with no overlap between consecutive steps (default: pipelined headline, "
+                        "serial reported as serial_gbps)")
+    p.add_argument("--no-serial-measure", action="store_true", help="skip the second (serial) measurement")
+    p.add_argument("--collective", choices=["rccl", "fused"], default="rccl",
+                   help="cross-rank combine: rccl = 1-element RCCL all-reduce after the local kernel; "
+                        "fused = the kernel's last workgroup folds all ranks' partials via IPC mailboxes")
+    p.add_argument("--local-only", action="store_true",
+                   help="single rank: skip the cross-rank combine (by default it is issued even at N=1)")
     p.add_argument("--streams", type=int, default=1,
                    help="alternate independent steps over this many HIP streams (each with its own workspace)")
     p.add_argument("--block", type=int, default=0)
@@ -174,6 +192,81 @@ def run_vector(args, ctx, cfg, fault) -> int:
     return 0 if verified in (None, True) else 1
 
 
+def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int) -> dict:
+    """Time K steps (after ``warmup`` eager steps); returns elapsed (MAX over ranks), the launch
+    mode and how many slots the timed steps wrote (graph replays rewrite the first chunk)."""
+    C = native()
+    dev = ctx.device
+    K = args.steps
+
+    def run(first: int, count: int):
+        works = []
+        wl.fork()
+        for i in range(first, first + count):
+            C.trace_push("bench.step")
+            corrupt = fault.at(ctx.rank, i, "bench step") if fault.enabled else False
+            w = wl.step(slots[i:i + 1], async_op=True, corrupt=corrupt)
+            C.trace_pop()
+            if w is not None:
+                if serial:
+                    w.wait()
+                else:
+                    works.append(w)
+        for w in works:
+            w.wait()
+        wl.join()
+
+    run(0, warmup)
+    launch, sg = "eager", None
+    capturable = dev.type == "cuda" and not args.trace and not fault.enabled and \
+        (not wl.issues_collective or ctx.backend == "nccl")
+    if (args.launch == "graph" and not fault.enabled) or (args.launch == "auto" and capturable):
+        # Capture the K timed steps as graph replays of --graph-chunk-step chunks (all ranks agree
+        # on success or all fall back to eager issue); one untimed replay uploads the graphs.
+        W = warmup
+        sg = StepGraph(lambda j: wl.step(slots[W + j:W + j + 1], async_op=True), K, dev,
+                       chunk=args.graph_chunk, serial=serial, fork=wl.fork, join=wl.join)
+        if sg.capture(group_agree=ctx.world_size > 1):
+            launch = f"graph (chunk {sg.chunk}, {sg.reps} replays" + (f" + 1 of {sg.rem})" if sg.rem else ")")
+            for g in sg.graphs:
+                g.replay()
+        else:
+            launch = f"eager (graph capture failed: {sg.error})"
+            if ctx.is_root:
+                print(f"[bench] {launch}", file=sys.stderr)
+            sg = None
+    _sync(dev)
+    pdist.barrier(ctx)
+    _sync(dev)
+    t0 = time.perf_counter()
+    if sg is not None:
+        sg.run()
+    else:
+        run(warmup, K)
+    _sync(dev)
+    t1 = time.perf_counter()
+    pdist.barrier(ctx)
+    elapsed = pdist.max_over_ranks(t1 - t0, ctx)
+    written = warmup + (sg.chunk if sg is not None else K)
+    if sg is not None:
+        sg.reset()  # captured RCCL work must not outlive the communicator
+    return {"elapsed": elapsed, "launch": launch, "written": written}
+
+
+def _verify_slots(wl, written: torch.Tensor, ctx) -> tuple:
+    """Every slot must hold the global value (all steps reduce the same data); AND over ranks."""
+    ref = wl.verify(written[-1:])
+    ok = ref["ok"]
+    if written.numel() > 1:
+        s = written
+        if wl.cfg.op in ("sum", "sumsq") and s.dtype.is_floating_point:
+            ok = ok and bool(((s - s[-1]).abs() <= ref["tolerance"]).all().item())
+        else:
+            ok = ok and bool((s == s[-1]).all().item())
+    ok = -pdist.max_over_ranks(-float(ok), ctx) > 0.5
+    return ok, ref
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     C = native()  # fail loudly if the HIP extension is missing
@@ -200,82 +293,56 @@ def main(argv=None) -> int:
                           groups=args.groups,
                           nontemporal=None if args.policy == "auto" else args.policy == "nt",
                           single_pass=not args.two_pass)
-    wl = scalar_workload(cfg, ctx, kernel, streams=1 if args.serial else args.streams).setup()
+    collective = args.collective
+    if collective == "fused" and (ctx.device.type != "cuda" or args.two_pass):
+        raise SystemExit("--collective fused needs GPUs and the single-pass kernel")
+    # The cross-rank combine is issued even on one rank (--local-only skips it): N=1 runs the
+    # exact step the N-GPU job runs.
+    wl = scalar_workload(cfg, ctx, kernel, streams=args.streams, collective=collective,
+                         always_collective=not args.local_only).setup()
     K, W = args.steps, args.warmup
-    slots = wl.new_slots(W + K)
     dev = ctx.device
 
-    def run(first: int, count: int):
-        works = []
-        for i in range(first, first + count):
-            C.trace_push("bench.step")
-            corrupt = fault.at(ctx.rank, i, "bench step") if fault.enabled else False
-            w = wl.step(slots[i:i + 1], async_op=True, corrupt=corrupt)
-            C.trace_pop()
-            if w is not None:
-                if args.serial:
-                    w.wait()
-                else:
-                    works.append(w)
-        for w in works:
-            w.wait()
-
-    run(0, W)
-    launch = "eager"
-    sg = None
-    capturable = dev.type == "cuda" and len(wl.lanes) == 1 and not args.serial and not args.trace and \
-        not fault.enabled and \
-        (ctx.world_size == 1 or ctx.backend == "nccl")
-    if (args.launch == "graph" and not fault.enabled) or (args.launch == "auto" and capturable):
-        # Capture the K timed steps as graph replays of --graph-chunk-step chunks (all ranks agree
-        # on success or all fall back to eager issue); one untimed replay uploads the graphs.
-        sg = StepGraph(lambda j: wl.step(slots[W + j:W + j + 1], async_op=True), K, dev, chunk=args.graph_chunk)
-        if sg.capture(group_agree=ctx.world_size > 1):
-            launch = f"graph (chunk {sg.chunk}, {sg.reps} replays" + (f" + 1 of {sg.rem})" if sg.rem else ")")
-            for g in sg.graphs:
-                g.replay()
-        else:
-            launch = f"eager (graph capture failed: {sg.error})"
-            if ctx.is_root:
-                print(f"[bench] {launch}", file=sys.stderr)
-            sg = None
-    _sync(dev)
-    pdist.barrier(ctx)
-    _sync(dev)
-    t0 = time.perf_counter()
-    if sg is not None:
-        sg.run()
-    else:
-        run(W, K)
-    _sync(dev)
-    t1 = time.perf_counter()
-    pdist.barrier(ctx)
-    elapsed = pdist.max_over_ranks(t1 - t0, ctx)
+    primary_serial = args.serial
+    slots = wl.new_slots(W + K)
+    m1 = _measure(wl, slots, ctx, args, fault, serial=primary_serial, warmup=W)
+    m2 = None
+    if not primary_serial and not args.no_serial_measure:
+        # The honest per-reduction number: every step completes (local reduce AND cross-rank
+        # combine) before the next one starts (reduction.cpp:319-374 times each reduction to
+        # completion). Reported next to the pipelined headline.
+        slots2 = wl.new_slots(min(W, 2) + K)
+        m2 = _measure(wl, slots2, ctx, args, fault, serial=True, warmup=min(W, 2))
 
     verified = None
+    err = wl.check()
     if not args.no_verify:
-        # every timed slot must hold the same global value (all steps reduce the same data)
-        # (warm-up slots too: a wrong warm-up result is a failure as well)
-        written = slots[:W + sg.chunk] if sg is not None else slots
-        ref = wl.verify(written[-1:])
-        ok = ref["ok"]
-        if written.numel() > 1:
-            s = written
-            if cfg.op == "sum" and s.dtype.is_floating_point:
-                ok = ok and bool(((s - s[-1]).abs() <= ref["tolerance"]).all().item())
-            else:
-                ok = ok and bool((s == s[-1]).all().item())
-        verified = ok
-        if not ok and ctx.is_root:
-            print(f"[bench] VERIFICATION FAILED: {ref}", file=sys.stderr)
+        ok, ref = _verify_slots(wl, slots[:m1["written"]], ctx)
+        if m2 is not None:
+            ok2, _ = _verify_slots(wl, slots2[:m2["written"]], ctx)
+            ok = ok and ok2
+        verified = ok and err is None
+        if not verified and ctx.is_root:
+            print(f"[bench] VERIFICATION FAILED: {ref} {err or ''}", file=sys.stderr)
+    elif err is not None:
+        verified = False
 
     torch_gbps = None
     if args.compare_torch and dev.type == "cuda":
         torch_gbps = _time_torch_reduction(wl, K, W, ctx)
     bytes_step = wl.bytes_total
+    elapsed = m1["elapsed"]
     gbps = bytes_step * K / elapsed / 1e9
     ms = elapsed / K * 1e3
+    lanes = len(wl.lanes) if wl.lanes else 1
     if ctx.is_root:
+        if wl.issues_collective:
+            combine = "RCCL all-reduce of the 1-element partial (torch.distributed nccl)" \
+                if ctx.backend == "nccl" else f"{ctx.backend} all-reduce of the 1-element partial"
+        elif collective == "fused":
+            combine = "fused in-kernel cross-rank finish (IPC mailboxes over xGMI, csrc/include/mireduce/xrank.hpp)"
+        else:
+            combine = "none (--local-only)"
         line = {
             "metric": METRIC if cfg.name == NORTH_STAR else f"reduction bandwidth (GB/s), {cfg.name}",
             "value": round(gbps, 3),
@@ -299,10 +366,15 @@ def main(argv=None) -> int:
                 "n_total_elements": wl.n_total,
                 "bytes_per_step": bytes_step,
                 "op": cfg.op.upper(),
-                "overlap": "serial" if args.serial else "pipelined (step i+1 local reduce || step i all-reduce)",
-                "streams": len(wl.lanes) if wl.lanes else 1,
-                "launch": launch,
-                "kernel_plan": wl.reducer.last_plan if wl.reducer else getattr(wl, "plan", None),
+                "collective": collective,
+                "cross_rank_combine": combine,
+                "overlap": "serial (each step completes before the next)" if primary_serial else
+                           ("pipelined (step i+1 local reduce || step i all-reduce)" if wl.issues_collective
+                            else f"pipelined over {lanes} stream lanes" if lanes > 1 else
+                            "serial (one kernel per step: reduce + in-kernel combine)"),
+                "streams": lanes,
+                "launch": m1["launch"],
+                "kernel_plan": wl.reducer.last_plan if getattr(wl, "reducer", None) else getattr(wl, "plan", None),
             },
             "per_gpu_gbps": round(gbps / ctx.world_size, 3),
             "baseline_value": cfg.baseline,
@@ -310,11 +382,13 @@ def main(argv=None) -> int:
             "verified": verified,
             "native_ext": os.path.basename(native_path()),
         }
+        if m2 is not None:
+            line["serial_gbps"] = round(bytes_step * K / m2["elapsed"] / 1e9, 3)
+            line["serial_ms_per_step"] = round(m2["elapsed"] / K * 1e3, 5)
+            line["serial_launch"] = m2["launch"]
         if torch_gbps is not None:
             line["torch_gbps"] = round(torch_gbps, 3)  # same data, torch's own reduction kernels
         print(json.dumps(line), flush=True)
-    if sg is not None:
-        sg.reset()  # captured RCCL work must not outlive the communicator
     _sync(dev)
     pdist.shutdown(ctx)
     return 0 if verified in (None, True) else 1

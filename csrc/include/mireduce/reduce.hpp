@@ -31,6 +31,9 @@ struct ReduceConfig {
   int policy = -1;        // streaming-load cache policy: -1 auto, 0 default, 1 non-temporal (nt)
   int pipeline = -1;      // software-pipelined body: -1 auto, 0 off, 1 on (BLOCK*UNROLL <= 8192)
   bool single_pass = true;   // last-arriver finalisation vs a second finalize launch
+  // Fused cross-rank finish: XrankChannel::device_desc() (xrank.hpp). The launch then writes the
+  // fold over every rank's partial into out (single-pass only).
+  const void* xrank = nullptr;
 };
 
 // What the planner chose (printed by the apps, recorded in JSON sidecars).

@@ -656,6 +656,14 @@ ArgEntry arg_lookup(Op op, DType t) {
 
 size_t ticket_bytes(uint64_t rows) { return (rows * sizeof(unsigned) + 255) / 256 * 256; }
 
+// Split rows have rows < target = num_cus x resident <= num_cus x kMaxResident (arg_layout), so
+// the per-row tickets of EVERY split launch fit one fixed region at the start of the scratch and
+// the partials always start after it. A row-count-dependent boundary would let a later call with
+// more rows read an earlier call's partial bits as tickets (the kernels leave only tickets zero).
+size_t ticket_region_bytes(int num_cus) {
+  return ticket_bytes(static_cast<uint64_t>(num_cus) * kMaxResident);
+}
+
 }  // namespace
 
 size_t arg_reduce_scratch_bytes(size_t rows, size_t cols, DType t, int num_cus) {
@@ -663,7 +671,7 @@ size_t arg_reduce_scratch_bytes(size_t rows, size_t cols, DType t, int num_cus) 
   // enough for the lane-group kernels have a single tile, hence no splits either way).
   const ArgLayout L = arg_layout(kLong, rows, cols, t, num_cus, kMaxResident, 2);
   if (L.splits <= 1) return 0;
-  return ticket_bytes(rows) + rows * L.splits * 16;
+  return ticket_region_bytes(num_cus) + rows * L.splits * 16;
 }
 
 ArgPlan arg_reduce_rows(const void* in, size_t rows, size_t cols, DType t, Op op, void* out_value, int64_t* out_index,
@@ -708,8 +716,9 @@ ArgPlan arg_reduce_rows(const void* in, size_t rows, size_t cols, DType t, Op op
   a.out_index = out_index;
   if (L.splits > 1) {
     MIREDUCE_REQUIRE(scratch != nullptr, "arg_reduce: this shape needs scratch (arg_reduce_scratch_bytes)");
+    MIREDUCE_REQUIRE(rows < static_cast<size_t>(num_cus) * kMaxResident, "arg_reduce: split rows exceed the ticket region");
     a.tickets = static_cast<unsigned*>(scratch);
-    a.partials = reinterpret_cast<uint64_t*>(static_cast<char*>(scratch) + ticket_bytes(rows));
+    a.partials = reinterpret_cast<uint64_t*>(static_cast<char*>(scratch) + ticket_region_bytes(num_cus));
   }
   e.fn(a, variant, unroll, L.grid, stream);
   MIREDUCE_HIP_THROW(hipGetLastError());

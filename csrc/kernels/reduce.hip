@@ -31,6 +31,7 @@
 #include "mireduce/ops.hpp"
 #include "mireduce/vec16.hpp"
 #include "mireduce/reduce.hpp"
+#include "mireduce/xrank.hpp"
 
 namespace mireduce {
 namespace kern {
@@ -71,7 +72,73 @@ struct Args {
   int groups;            // 0: two-pass mode (write partials only)
   int flat;              // 1: group last-arrivers only count; the final arriver folds every partial
   int contig;            // 1: workgroup b streams one contiguous run of tiles; 0: tiles b, b+grid, ...
+  const XrankDesc* xrank;  // non-null: fold the ranks' partials in-kernel before writing out (xrank.hpp)
 };
+
+template <class T>
+__device__ __forceinline__ uint64_t to_bits64(T v) {
+  if constexpr (sizeof(T) == 8) {
+    return __builtin_bit_cast(uint64_t, v);
+  } else {
+    return static_cast<uint64_t>(__builtin_bit_cast(uint32_t, v));
+  }
+}
+
+template <class T>
+__device__ __forceinline__ T from_bits64(uint64_t b) {
+  if constexpr (sizeof(T) == 8) {
+    return __builtin_bit_cast(T, b);
+  } else {
+    return __builtin_bit_cast(T, static_cast<uint32_t>(b));
+  }
+}
+
+// Cross-rank finish (xrank.hpp), run by the 64 lanes of the finishing workgroup's wave 0 with
+// this rank's partial `t` in every lane; returns the fold over all ranks in every lane.
+// Lane p pushes to rank p's mailbox and then polls slot p of its own: the world pushes leave in
+// one store round and the polls overlap. Words are (epoch << 32 | 32 data bits), written and
+// read with system-scope atomics (8-byte single-copy atomic over xGMI), so a matching epoch in
+// both words of a slot means the whole partial of this launch has landed.
+template <class OpT, class AccT>
+__device__ __forceinline__ AccT xrank_finish(const XrankDesc* d, AccT t) {
+  const int lane = threadIdx.x & 63;
+  unsigned e = 0, err = 0;
+  if (lane == 0) {
+    e = __hip_atomic_fetch_add(d->epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    err = __hip_atomic_load(d->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  e = __shfl(e, 0, 64);
+  err = __shfl(err, 0, 64);
+  const int world = d->world;
+  const int rank = d->rank;
+  const uint64_t parity = static_cast<uint64_t>(e & 1u) * kMaxXrankRanks;
+  const uint64_t tag = static_cast<uint64_t>(e) << 32;
+  const uint64_t bits = to_bits64(t);
+  AccT v = OpT::template identity<AccT>();
+  if (lane < world) {
+    uint64_t* dst = d->peer_mbox[lane] + (parity + rank) * 2;
+    __hip_atomic_store(dst, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t* src = d->own_mbox + (parity + lane) * 2;
+    // A sticky error (an earlier launch timed out) means a peer is gone: look once, do not wait.
+    const uint64_t limit = err ? 0 : d->timeout_ticks;
+    const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
+    for (;;) {
+      const uint64_t lo = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint64_t hi = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if ((lo >> 32) == e && (hi >> 32) == e) {
+        v = from_bits64<AccT>((lo & 0xffffffffull) | (hi << 32));
+        break;
+      }
+      if (static_cast<uint64_t>(wall_clock64()) - t0 > limit) {
+        __hip_atomic_fetch_or(d->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return wave_reduce<OpT>(v);
+}
 
 template <class V, int BLOCK, int UNROLL, bool NT>
 __device__ __forceinline__ void load_tile(V (&v)[UNROLL], const V* p) {
@@ -187,9 +254,12 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     AccT t = OpT::template identity<AccT>();
     for (unsigned i = threadIdx.x; i < gridDim.x; i += BLOCK) t = OpT::apply(t, load_sc1(&partials[i]));
     t = block_reduce<OpT, AccT, BLOCK>(t, lds);
-    if (threadIdx.x == 0) {
-      *static_cast<AccT*>(a.out) = t;
-      __hip_atomic_store(&a.tickets[G * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 64) {
+      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, t);
+      if (threadIdx.x == 0) {
+        *static_cast<AccT*>(a.out) = t;
+        __hip_atomic_store(&a.tickets[G * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     return;
   }
@@ -215,6 +285,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     const int lane = threadIdx.x;
     AccT t = lane < static_cast<int>(G) ? load_sc1(&gpart[lane]) : OpT::template identity<AccT>();
     t = wave_reduce<OpT>(t);
+    if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, t);
     if (lane == 0) {
       *static_cast<AccT*>(a.out) = t;
       __hip_atomic_store(&a.tickets[G * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -525,6 +596,8 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   p.unroll = cfg.unroll ? cfg.unroll : d.unroll;
   p.nontemporal = cfg.policy < 0 ? d.policy == 1 : cfg.policy == 1;
   p.single_pass = cfg.single_pass;
+  MIREDUCE_REQUIRE(cfg.xrank == nullptr || cfg.single_pass,
+                   "the fused cross-rank finish needs the single-pass kernel");
   p.pipelined = (cfg.pipeline < 0 ? d.pipeline == 1 : cfg.pipeline == 1) && p.block * p.unroll <= 8192;
   MIREDUCE_REQUIRE(block_index(p.block) >= 0, "block must be 256, 512 or 1024");
   MIREDUCE_REQUIRE(unroll_index(p.unroll) >= 0, "unroll must be 2, 4, 8 or 16");
@@ -581,6 +654,7 @@ LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out
   a.out = out;
   a.groups = p.groups;
   a.flat = p.flat ? 1 : 0;
+  a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
   const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0];
   fn(a, p.grid, stream);
   MIREDUCE_HIP_THROW(hipGetLastError());
@@ -610,6 +684,7 @@ BoundReduce::BoundReduce(const void* in, size_t n, DType t, Op op, DType acc, vo
   a.out = out;
   a.groups = p.groups;
   a.flat = p.flat ? 1 : 0;
+  a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
   impl_ = new Impl{a, table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0],
                    p, op, acc};
 }
@@ -632,6 +707,7 @@ LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, 
   MIREDUCE_REQUIRE(c >= 0, "unsupported (dtype, op, accumulator) combination");
   ReduceConfig c2 = cfg;
   c2.single_pass = false;
+  c2.xrank = nullptr;
   LaunchPlan p = plan_reduce(in, n, t, c2, num_cus, max_grid);
   kern::Args a = make_args(in, p, t);
   a.partials = partials;

@@ -510,11 +510,18 @@ DimEntry lookup(Op op, DType t, DType acc) {
 
 }  // namespace
 
+// Rows split only when rows < num_cus x 16 (row_layout's target_waves), so every split launch's
+// per-row tickets fit one fixed region at the start of the scratch; the partials always start
+// after it (a row-count-dependent boundary let a later, taller launch read an earlier launch's
+// partial bits as tickets — the kernels leave only the ticket words zero).
+size_t row_ticket_region_bytes(int num_cus) {
+  return (static_cast<size_t>(num_cus) * 16 * sizeof(unsigned) + 255) / 256 * 256;
+}
+
 size_t reduce_rows_scratch_bytes(size_t rows, size_t cols, DType t, int num_cus) {
   const RowLayout L = row_layout(rows, cols, t, num_cus);
   if (L.splits <= 1) return 0;
-  const size_t tickets = (rows * sizeof(unsigned) + 255) / 256 * 256;
-  return tickets + rows * L.splits * 8;
+  return row_ticket_region_bytes(num_cus) + rows * L.splits * 8;
 }
 
 size_t reduce_cols_scratch_bytes(size_t outer, size_t rows, size_t cols, DType t, DType acc, int num_cus) {
@@ -544,8 +551,9 @@ DimPlan reduce_rows(const void* in, size_t rows, size_t cols, DType t, Op op, DT
   a.out = out;
   if (L.splits > 1) {
     MIREDUCE_REQUIRE(scratch != nullptr, "reduce_rows: this shape needs scratch (reduce_rows_scratch_bytes)");
+    MIREDUCE_REQUIRE(rows < static_cast<size_t>(num_cus) * 16, "reduce_rows: split rows exceed the ticket region");
     a.tickets = static_cast<unsigned*>(scratch);
-    a.partials = static_cast<char*>(scratch) + (rows * sizeof(unsigned) + 255) / 256 * 256;
+    a.partials = static_cast<char*>(scratch) + row_ticket_region_bytes(num_cus);
   }
   e.rows(a, L.grid, stream);
   MIREDUCE_HIP_THROW(hipGetLastError());

@@ -23,6 +23,7 @@
 #include "mireduce/reduce_many.hpp"
 #include "mireduce/trace.hpp"
 #include "mireduce/types.hpp"
+#include "mireduce/xrank.hpp"
 
 namespace py = pybind11;
 using namespace mireduce;
@@ -164,19 +165,45 @@ PYBIND11_MODULE(_C, m) {
   py::class_<BoundReduce>(m, "BoundReduce")
       .def(py::init([](Workspace& ws, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out,
                        int block, int unroll, int wg_per_cu, int max_blocks, int groups, int policy,
-                       bool single_pass, int pipeline) {
+                       bool single_pass, int pipeline, uintptr_t xrank) {
+             ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline);
+             cfg.xrank = as_ptr<const void>(xrank);
              return new BoundReduce(as_ptr<const void>(in), n, static_cast<DType>(dtype), static_cast<Op>(op),
-                                    static_cast<DType>(acc), as_ptr<void>(out), ws,
-                                    make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass,
-                                             pipeline));
+                                    static_cast<DType>(acc), as_ptr<void>(out), ws, cfg);
            }),
            py::arg("ws"), py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"), py::arg("acc"),
            py::arg("out_ptr"), py::arg("block") = 0, py::arg("unroll") = 0, py::arg("wg_per_cu") = 0,
            py::arg("max_blocks") = 0, py::arg("groups") = 0, py::arg("policy") = -1,
-           py::arg("single_pass") = true, py::arg("pipeline") = -1, py::keep_alive<1, 2>())
+           py::arg("single_pass") = true, py::arg("pipeline") = -1, py::arg("xrank") = 0, py::keep_alive<1, 2>())
       .def("launch", [](const BoundReduce& b, uintptr_t stream, uintptr_t out) { b.launch(as_stream(stream), as_ptr<void>(out)); },
            py::arg("stream"), py::arg("out_ptr") = 0)
       .def_property_readonly("plan", [](const BoundReduce& b) { return plan_dict(b.plan()); });
+
+  // Fused cross-rank finish (xrank.hpp): exchange handle() bytes with every rank, connect(), then
+  // pass desc_ptr as BoundReduce(..., xrank=desc_ptr).
+  py::class_<XrankChannel, std::shared_ptr<XrankChannel>>(m, "XrankChannel")
+      .def(py::init<int, double>(), py::arg("device") = -1, py::arg("timeout_s") = 2.0)
+      .def("handle", [](const XrankChannel& c) {
+        const IpcHandleBytes h = c.handle();
+        return py::bytes(h.data(), h.size());
+      })
+      .def("connect", [](XrankChannel& c, int rank, int world, const std::vector<py::bytes>& handles) {
+        std::vector<IpcHandleBytes> hs(handles.size());
+        for (size_t i = 0; i < handles.size(); ++i) {
+          const std::string s = handles[i];
+          if (s.size() != sizeof(IpcHandleBytes)) throw Error("XrankChannel.connect: bad handle size");
+          std::memcpy(hs[i].data(), s.data(), s.size());
+        }
+        c.connect(rank, world, hs);
+      }, py::arg("rank"), py::arg("world"), py::arg("handles"))
+      .def_property_readonly("connected", &XrankChannel::connected)
+      .def_property_readonly("desc_ptr", [](const XrankChannel& c) { return reinterpret_cast<uintptr_t>(c.device_desc()); })
+      .def_property_readonly("rank", &XrankChannel::rank)
+      .def_property_readonly("world", &XrankChannel::world)
+      .def("error", &XrankChannel::error)
+      .def("epoch", &XrankChannel::epoch)
+      .def("clear_error", &XrankChannel::clear_error);
+  m.attr("XRANK_MAX_RANKS") = kMaxXrankRanks;
 
   m.def(
       "reduce",

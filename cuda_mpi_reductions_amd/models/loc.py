@@ -37,7 +37,7 @@ class LocReduction:
     """Global first index (and value) of the maximum / minimum of a sharded array."""
 
     def __init__(self, cfg, ctx: pdist.DistContext, kernel: Optional[KernelConfig] = None, seed: int = 0x5EED,
-                 acc_dtype: Optional[torch.dtype] = None, streams: int = 1):
+                 acc_dtype: Optional[torch.dtype] = None, streams: int = 1, always_collective: bool = False):
         if cfg.op not in LOC_OPS:
             raise ValueError(f"LocReduction needs op maxloc|minloc, got {cfg.op!r}")
         self.cfg = cfg
@@ -50,6 +50,9 @@ class LocReduction:
         self.reducer = None
         self.lanes: list = []
         self.plan: Optional[dict] = None
+        self.collective = "rccl"
+        self.always_collective = bool(always_collective)
+        self.channels: list = []
 
     def setup(self) -> "LocReduction":
         dev = self.ctx.device
@@ -99,9 +102,22 @@ class LocReduction:
         gi = self.idx + self._offset_t
         if corrupt:
             gi = gi + 1
-        if self.ctx.world_size > 1:
+        if self.issues_collective:
             _, gi = pdist.loc_allreduce(self.val, gi, self.kind)
         out.copy_(gi.reshape(1))
+        return None
+
+    @property
+    def issues_collective(self) -> bool:
+        return self.ctx.world_size > 1 or self.always_collective
+
+    def fork(self) -> None:
+        pass
+
+    def join(self) -> None:
+        pass
+
+    def check(self):
         return None
 
     def reference(self) -> int:

@@ -13,6 +13,7 @@ then an RCCL all-reduce of that slot over xGMI (SURVEY.md §5.8 "mode scalar").
 """
 from __future__ import annotations
 
+import contextlib
 import math
 from dataclasses import dataclass, field, replace
 from typing import Optional
@@ -22,7 +23,7 @@ import torch
 from ..ops import KernelConfig, Reducer, default_acc_dtype, fill_, sum_tolerance
 from ..parallel import dist as pdist
 
-__all__ = ["WorkloadConfig", "CONFIGS", "NORTH_STAR", "ScalarReduction", "VectorReduction",
+__all__ = ["WorkloadConfig", "CONFIGS", "NORTH_STAR", "COLLECTIVES", "ScalarReduction", "VectorReduction",
            "element_size"]
 
 
@@ -91,6 +92,9 @@ CONFIGS: dict[str, WorkloadConfig] = {
 NORTH_STAR = "xgmi_1b_double_sum"
 
 
+_nullcontext = contextlib.nullcontext
+
+
 def _current_stream_handle(device: torch.device) -> int:
     try:
         return torch._C._cuda_getCurrentRawStream(device.index)
@@ -98,30 +102,56 @@ def _current_stream_handle(device: torch.device) -> int:
         return int(torch.cuda.current_stream(device).cuda_stream)
 
 
+COLLECTIVES = ("rccl", "fused")
+
+
 class ScalarReduction:
-    """Global reduction of a sharded array to one value on every rank."""
+    """Global reduction of a sharded array to one value on every rank.
+
+    ``collective`` picks how the ranks' partials are combined:
+
+    * ``"rccl"`` — the local single-pass kernel writes this rank's partial, then a 1-element
+      ``torch.distributed`` all-reduce (RCCL over xGMI) combines them (a second kernel, on RCCL's
+      stream);
+    * ``"fused"`` — the local kernel's last workgroup exchanges the partials through IPC-mapped
+      mailboxes and writes the global value itself (:mod:`parallel.xrank`): one kernel per step.
+
+    ``always_collective``: issue the cross-rank combine even on a single rank (the bench and the
+    smoke test run the exact N-GPU step on one GPU this way).
+    ``streams`` > 1 alternates independent steps over that many HIP streams ("lanes"), each with
+    its own workspace (and channel), so one step's tail overlaps the next step's body.
+    """
 
     def __init__(self, cfg: WorkloadConfig, ctx: pdist.DistContext,
                  kernel: Optional[KernelConfig] = None, seed: int = 0x5EED,
-                 acc_dtype: Optional[torch.dtype] = None, streams: int = 1):
+                 acc_dtype: Optional[torch.dtype] = None, streams: int = 1,
+                 collective: str = "rccl", always_collective: bool = False,
+                 xrank_timeout_s: float = 2.0):
         if cfg.mode != "scalar":
             raise ValueError("ScalarReduction needs a scalar-mode config")
+        if collective not in COLLECTIVES:
+            raise ValueError(f"collective must be one of {COLLECTIVES}, got {collective!r}")
         self.cfg = cfg
         self.ctx = ctx
         self.kernel = kernel or KernelConfig()
         self.seed = seed
         self.acc = acc_dtype or default_acc_dtype(cfg.dtype, cfg.op)
+        self.collective = collective
+        self.always_collective = bool(always_collective)
+        self.xrank_timeout_s = xrank_timeout_s
         self.x: Optional[torch.Tensor] = None
         self.offset = 0
         self.count = 0
         self.n_total = 0
         self.reducer: Optional[Reducer] = None
-        # Independent steps may alternate over `streams` HIP streams (one Reducer — one ticket
-        # workspace — per stream), so step i+1's ramp-up overlaps step i's tail.
         self.n_streams = max(1, int(streams))
+        # lanes[k] = (stream, reducer, bound launch, xrank channel or None); lane 0 runs on the
+        # caller's current stream when there is a single lane.
         self.lanes: list = []
+        self.channels: list = []
         self._next = 0
-        self.bound = None  # _C.BoundReduce of lane 0 (prepared launch), set by setup()
+        self._fork = None
+        self.bound = None  # lane 0's prepared launch, set by setup()
 
     # ------------------------------------------------------------------ setup
     def _size_for_hbm(self) -> int:
@@ -148,57 +178,85 @@ class ScalarReduction:
         self.x = torch.empty(self.count, dtype=self.cfg.dtype, device=dev)
         fill_(self.x, self.cfg.pattern, seed=self.seed, offset=self.offset)
         if dev.type == "cuda":
-            self.reducer = Reducer(dev, config=self.kernel)
-            self.lanes = [(torch.cuda.current_stream(dev), self.reducer)]
-            for _ in range(self.n_streams - 1):
-                self.lanes.append((torch.cuda.Stream(dev), Reducer(dev, config=self.kernel)))
+            if self.collective == "fused":
+                from ..parallel.xrank import open_channel
             self._bound_out = self.new_slots(1)  # default target; steps pass their own slot
-            self.bound = self.reducer.bind(self.x, self.cfg.op, self.acc, out=self._bound_out)
+            for k in range(self.n_streams):
+                stream = torch.cuda.current_stream(dev) if self.n_streams == 1 else torch.cuda.Stream(dev)
+                reducer = Reducer(dev, config=self.kernel)
+                ch = open_channel(dev, timeout_s=self.xrank_timeout_s) if self.collective == "fused" else None
+                bound = reducer.bind(self.x, self.cfg.op, self.acc, out=self._bound_out, xrank=ch)
+                self.lanes.append((stream, reducer, bound, ch))
+                if ch is not None:
+                    self.channels.append(ch)
+            self.reducer, self.bound = self.lanes[0][1], self.lanes[0][2]
             torch.cuda.synchronize(dev)
+        elif self.collective == "fused":
+            raise RuntimeError("the fused cross-rank finish needs GPUs")
         return self
 
     @property
     def bytes_total(self) -> int:
         return self.n_total * element_size(self.cfg.dtype)
 
+    @property
+    def issues_collective(self) -> bool:
+        """Whether a step issues an RCCL / gloo collective (the fused finish is in-kernel)."""
+        return self.collective == "rccl" and (self.ctx.world_size > 1 or self.always_collective)
+
     # ------------------------------------------------------------------ step
     def new_slots(self, k: int) -> torch.Tensor:
         return torch.empty(k, dtype=self.acc, device=self.ctx.device)
 
-    def _local_into(self, out: torch.Tensor) -> None:
-        if self.bound is not None:
-            self.bound.launch(_current_stream_handle(self.ctx.device), out.data_ptr())
-        else:
-            self.local(out)
-
     def local(self, out: torch.Tensor) -> torch.Tensor:
-        if self.reducer is not None:
+        """This rank's partial only (no cross-rank combine; never through a fused channel)."""
+        if self.ctx.device.type == "cuda":  # an unbound launch on lane 0's workspace: no channel
             return self.reducer(self.x, self.cfg.op, self.acc, out=out)
         from ..ops import reduce as host_reduce
         return host_reduce(self.x, self.cfg.op, self.acc, out=out)
 
-    def step(self, out: torch.Tensor, async_op: bool = True, corrupt: bool = False):
-        """Local reduce into ``out`` (1 element) then all-reduce it across ranks. Returns the
-        collective's work handle (``None`` for a single rank). ``corrupt`` (fault injection)
-        perturbs the local result before the collective; verification must catch it."""
-        if corrupt:
-            self._local_into(out)
-            out.sub_(1) if self.cfg.op == "min" else out.add_(1)
-            if self.ctx.world_size == 1:
-                return None
-            return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op)
+    def fork(self) -> None:
+        """Multi-lane steps: make every lane's stream follow the caller's current stream (call
+        before a batch of steps; inside a graph capture this is the fork of the captured DAG)."""
         if len(self.lanes) > 1:
-            stream, reducer = self.lanes[self._next % len(self.lanes)]
-            self._next += 1
-            with torch.cuda.stream(stream):
-                reducer(self.x, self.cfg.op, self.acc, out=out)
-                if self.ctx.world_size == 1:
-                    return None
+            cur = torch.cuda.current_stream(self.ctx.device)
+            for stream, *_ in self.lanes:
+                stream.wait_stream(cur)
+
+    def join(self) -> None:
+        """Multi-lane steps: make the caller's current stream wait for every lane."""
+        if len(self.lanes) > 1:
+            cur = torch.cuda.current_stream(self.ctx.device)
+            for stream, *_ in self.lanes:
+                cur.wait_stream(stream)
+
+    def step(self, out: torch.Tensor, async_op: bool = True, corrupt: bool = False):
+        """Local reduce into ``out`` (1 element) then the cross-rank combine. Returns the RCCL
+        collective's work handle, or ``None`` (fused finish, or a single rank without
+        ``always_collective``). ``corrupt`` (fault injection) perturbs the local result before
+        the collective; verification must catch it (rccl only)."""
+        if self.ctx.device.type != "cuda":
+            self.local(out)
+            if corrupt:
+                out.sub_(1) if self.cfg.op == "min" else out.add_(1)
+            return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op) if self.issues_collective else None
+        stream, _, bound, _ = self.lanes[self._next % len(self.lanes)]
+        self._next += 1
+        ctx = torch.cuda.stream(stream) if len(self.lanes) > 1 else _nullcontext()
+        with ctx:
+            bound.launch(_current_stream_handle(self.ctx.device), out.data_ptr())
+            if corrupt:
+                out.sub_(1) if self.cfg.op == "min" else out.add_(1)
+            if self.issues_collective:
                 return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op)
-        self._local_into(out)  # prepared launch on the *current* stream (graph-capturable)
-        if self.ctx.world_size == 1:
+        return None
+
+    def check(self) -> Optional[str]:
+        """None, or the fused finish's error (a peer's partial never arrived). Collective."""
+        if not self.channels:
             return None
-        return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op)
+        from ..parallel.xrank import check_channel
+        return check_channel(self.channels)
 
     # ------------------------------------------------------------------ verify
     def reference(self, chunk: int = 1 << 28):

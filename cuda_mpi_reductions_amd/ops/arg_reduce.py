@@ -70,7 +70,8 @@ def arg_reduce(x: torch.Tensor, op: str = "max", dim: Optional[int] = None, keep
     """``(values, indices)`` of the first maximum (``op="max"``) or minimum (``op="min"``).
 
     ``dim=None`` reduces the whole (flattened) tensor to 0-d results; otherwise along ``dim``.
-    ``group`` (``dim=None`` only): reduce over all ranks' shards of one logical array.
+    ``group`` (``dim=None`` only): reduce over all ranks' shards of one logical array (pass
+    ``torch.distributed.group.WORLD`` for the default group); without it the call is rank-local.
     """
     op = op.lower()
     if op not in ("max", "min"):
@@ -80,7 +81,7 @@ def arg_reduce(x: torch.Tensor, op: str = "max", dim: Optional[int] = None, keep
             raise ValueError("arg_reduce of an empty tensor")
         v, i = _rows(x.contiguous().view(1, -1), op)
         v, i = v.reshape(()), i.reshape(())
-        if group is not None or _distributed():
+        if group is not None:  # global only when asked: a rank-local call must stay local
             v, i = _global(v, i, x.numel(), op, group)
         if keepdim:
             shape = [1] * x.dim()
@@ -108,11 +109,6 @@ def argmax(x: torch.Tensor, dim: Optional[int] = None, keepdim: bool = False) ->
 def argmin(x: torch.Tensor, dim: Optional[int] = None, keepdim: bool = False) -> torch.Tensor:
     """First index of the minimum (``torch.argmin`` semantics)."""
     return arg_reduce(x, "min", dim, keepdim)[1]
-
-
-def _distributed() -> bool:
-    d = torch.distributed
-    return d.is_available() and d.is_initialized() and d.get_world_size() > 1
 
 
 def _global(v: torch.Tensor, i: torch.Tensor, local_n: int, op: str, group):

@@ -157,12 +157,16 @@ class Reducer:
         return out
 
     def bind(self, x: torch.Tensor, op: str = "sum", acc_dtype: Optional[torch.dtype] = None,
-             out: Optional[torch.Tensor] = None, config: Optional[KernelConfig] = None):
+             out: Optional[torch.Tensor] = None, config: Optional[KernelConfig] = None, xrank=None):
         """Resolve plan, kernel variant and arguments once (``_C.BoundReduce``).
 
         ``bound.launch(stream_handle[, out_ptr])`` is then a single kernel launch with no planning
         or argument marshalling — the per-step path of bench loops and hipGraph capture. ``x``,
         ``out`` and this Reducer must outlive the returned object.
+
+        ``xrank`` (a connected ``_C.XrankChannel``, see :mod:`parallel.xrank`): every launch then
+        also folds all ranks' partials in-kernel, so ``out`` receives the GLOBAL result — every rank
+        must launch its bound reductions of that channel in the same order.
         """
         C = native()
         if x.device != self.device or not x.is_contiguous():
@@ -173,8 +177,10 @@ class Reducer:
         elif out.dtype != acc or out.device != self.device or out.numel() < 1:
             raise ValueError("out must be a 1+ element tensor of the accumulator dtype on the same device")
         cfg = config or self.config
+        if xrank is not None and not xrank.connected:
+            raise ValueError("bind: the XrankChannel is not connected")
         b = C.BoundReduce(self.ws, x.data_ptr(), x.numel(), dtype_code(x.dtype), op_code(op), dtype_code(acc),
-                          out.data_ptr(), **cfg.kwargs())
+                          out.data_ptr(), xrank=xrank.desc_ptr if xrank is not None else 0, **cfg.kwargs())
         self.last_plan = b.plan
         return b
 

@@ -10,7 +10,12 @@ had no equivalent (one blocking MPI_Reduce per measurement, mpi/reduce.c:76,90);
 :class:`StepGraph` captures ``chunk`` consecutive steps (each enqueued by ``step_fn(j)``, which may
 return a ``torch.distributed`` work handle) into one graph — the all-reduce of step j overlaps
 the local reduce of step j+1 inside the graph — plus a remainder graph, so ``run()`` executes
-exactly ``n_steps`` steps. All ranks must capture (``capture`` is collective when a process group
+exactly ``n_steps`` steps. With ``serial=True`` every step's work handle is waited on before the
+next step is enqueued (the captured graph then has the dependency chain reduce -> all-reduce ->
+reduce ..., i.e. every replayed step completes before the next starts: the reference's timing of
+one reduction to completion, reduction.cpp:319-374). ``fork`` / ``join`` (optional) are called at
+the start / end of every captured chunk (multi-stream steps: fork the side streams off the capture
+stream and join them back). All ranks must capture (``capture`` is collective when a process group
 is given): capture success is agreed with an all-reduce so either every rank replays graphs or
 every rank falls back to eager issue.
 """
@@ -29,8 +34,12 @@ def pick_chunk(n_steps: int, max_chunk: int = 32) -> int:
 
 class StepGraph:
     def __init__(self, step_fn: Callable[[int], object], n_steps: int, device: torch.device,
-                 chunk: Optional[int] = None):
+                 chunk: Optional[int] = None, serial: bool = False,
+                 fork: Optional[Callable[[], None]] = None, join: Optional[Callable[[], None]] = None):
         self.step_fn = step_fn
+        self.serial = bool(serial)
+        self.fork = fork
+        self.join = join
         self.n_steps = int(n_steps)
         self.device = device
         self.chunk = pick_chunk(self.n_steps) if chunk is None else max(1, min(int(chunk), self.n_steps))
@@ -43,10 +52,20 @@ class StepGraph:
         # thread_local: HIP calls made by other threads meanwhile (ProcessGroupNCCL's watchdog
         # querying events of earlier eager collectives) must not invalidate this capture.
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            works = [self.step_fn(j) for j in range(count)]
-            for w in works:
+            if self.fork is not None:
+                self.fork()
+            works = []
+            for j in range(count):
+                w = self.step_fn(j)
                 if w is not None:
-                    w.wait()
+                    if self.serial:
+                        w.wait()
+                    else:
+                        works.append(w)
+            for w in works:
+                w.wait()
+            if self.join is not None:
+                self.join()
         return g
 
     def capture(self, group_agree: bool = False) -> bool:

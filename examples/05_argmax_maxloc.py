@@ -4,8 +4,8 @@
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/05_argmax_maxloc.py   # MPI_MAXLOC over GPUs
     torchrun --nproc-per-node 2 --master-addr 127.0.0.1 examples/05_argmax_maxloc.py --cpu
 
-* ``arg_reduce(x, "max")``: first index of the maximum of a whole array (+ its value); under a
-  process group the array is every rank's shard concatenated in rank order;
+* ``arg_reduce(x, "max", group=...)``: first index of the maximum of a whole array (+ its value);
+  with ``group`` the array is every rank's shard concatenated in rank order (without it, rank-local);
 * ``argmax(logits, dim=-1)``: per row — greedy decoding over a vocabulary, top-1 expert routing;
 * ``loc_allreduce``: MPI_MAXLOC / MPI_MINLOC of per-rank (value, global index) pairs over RCCL.
 """
@@ -41,8 +41,8 @@ print(f"[rank {ctx.rank}] greedy tokens {tokens[:4].tolist()}  experts {experts[
 # MPI_MAXLOC across ranks: every rank learns the global max and its global index (shards in rank order)
 offset = ctx.rank * n
 gv, gi = pdist.loc_allreduce(lv, li + offset, "max") if ctx.world_size > 1 else (lv, li + offset)
-# the same answer in one call: a whole-array arg_reduce is global under a process group
-av, ai = arg_reduce(x, "max")
+# the same answer in one call: a whole-array arg_reduce over the group's shards
+av, ai = arg_reduce(x, "max", group=torch.distributed.group.WORLD)
 ok = gv.item() == av.item() and gi.item() == ai.item()
 print(f"[rank {ctx.rank}] global max {gv.item():.12f} at global index {gi.item()} "
       f"of {ctx.world_size} shards (arg_reduce agrees: {ok})")

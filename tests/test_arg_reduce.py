@@ -105,8 +105,8 @@ def test_global_two_cpu_ranks(tmp_path):
         "x = torch.zeros(1000 + 7 * r)\n"
         "x[100 + r] = 5.0   # tie across ranks: rank 0's copy is first\n"
         "x[900] = -3.0 if r == 1 else 0.0\n"
-        "v, i = arg_reduce(x, 'max')\n"
-        "v2, i2 = arg_reduce(x, 'min')\n"
+        "v, i = arg_reduce(x, 'max', group=dist.group.WORLD)\n"
+        "v2, i2 = arg_reduce(x, 'min', group=dist.group.WORLD)\n"
         f"open(os.path.join({str(tmp_path)!r}, 'res%d' % r), 'w').write('%r %d %r %d' % (float(v), int(i), float(v2), int(i2)))\n"
         "dist.destroy_process_group()\n")
     r = torchrun(2, [str(script)], timeout=240)
@@ -115,6 +115,30 @@ def test_global_two_cpu_ranks(tmp_path):
         v, i, v2, i2 = (tmp_path / f"res{rank}").read_text().split()
         assert float(v) == 5.0 and int(i) == 100  # rank 0's element 100
         assert float(v2) == -3.0 and int(i2) == 1000 + 900  # rank 1's element 900 after rank 0's 1000
+
+
+def test_rank_local_without_group_in_a_job(tmp_path):
+    # without group=, a whole-array arg_reduce stays rank-local even when a
+    # world>1 process group exists (a rank-local argmax in a DDP job must not become a collective).
+    from helpers import torchrun
+    script = tmp_path / "argl.py"
+    script.write_text(
+        "import os, sys, torch\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import torch.distributed as dist\n"
+        "from cuda_mpi_reductions_amd.ops import arg_reduce\n"
+        "dist.init_process_group('gloo')\n"
+        "r = dist.get_rank()\n"
+        "x = torch.zeros(50)\n"
+        "x[10 + r] = 1.0\n"
+        "if r == 0:\n"
+        "    v, i = arg_reduce(x, 'max')  # only rank 0 calls it: must not hang\n"
+        "    open(os.path.join(%r, 'res'), 'w').write('%%d' %% int(i))\n" % str(tmp_path) +
+        "dist.barrier()\n"
+        "dist.destroy_process_group()\n")
+    r = torchrun(2, [str(script)], timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert int((tmp_path / "res").read_text()) == 10
 
 
 # ---- device kernels ------------------------------------------------------------------------
@@ -194,6 +218,19 @@ def test_device_repeat_and_stream_reuse():
         i = argmax(x, 1)
     s.synchronize()
     assert torch.equal(i.cpu(), x.cpu().argmax(1))
+
+
+@pytest.mark.gpu
+def test_device_split_scratch_reuse_with_more_rows():
+    # a split launch with few rows followed, on the same stream and scratch, by a
+    # split launch with MORE rows must not read the first launch's partials as its tickets.
+    x1 = _data((30_000_000,), torch.float32, seed=11, device="cuda")  # 1 row, hundreds of segments
+    _check(x1, "max")
+    x2 = _data((128, 131072), torch.bfloat16, seed=12, device="cuda")  # 128 rows < CUs: split rows
+    for _ in range(3):
+        _check(x2, "max", 1)
+        _check(x1, "min")
+        _check(x2, "min", 1)
 
 
 @pytest.mark.gpu

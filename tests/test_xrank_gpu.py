@@ -1,0 +1,135 @@
+"""Fused cross-rank finish (csrc/include/mireduce/xrank.hpp) and the exact N-GPU bench step run on
+one GPU: the cross-rank combine is issued (and graph-captured) even at world 1, serial and
+pipelined; several ranks share the one GPU of the box through HIP IPC for the multi-rank protocol
+(not xGMI speed)."""
+import json
+import os
+import sys
+import time
+
+import pytest
+import torch
+
+from helpers import ROOT, run, torchrun
+
+pytestmark = pytest.mark.gpu
+
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _json(r):
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+
+
+# ---------------------------------------------------------------- kernel numerics at world 1
+
+@pytest.mark.parametrize("dt,op", [(torch.float64, "sum"), (torch.float64, "min"), (torch.int64, "min"),
+                                   (torch.int64, "sum"), (torch.int32, "sum"), (torch.int32, "max"),
+                                   (torch.float32, "sum"), (torch.float32, "max"), (torch.bfloat16, "sum"),
+                                   (torch.float64, "sumsq"), (torch.float32, "amax")])
+@pytest.mark.parametrize("n", [1, 1000, 3_000_017])
+def test_fused_world1_matches_torch(dt, op, n):
+    from cuda_mpi_reductions_amd.ops import Reducer, default_acc_dtype
+    from cuda_mpi_reductions_amd.parallel.xrank import open_channel
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(n)
+    if dt.is_floating_point:
+        x = (torch.rand(n, generator=g, dtype=torch.float64) * 2 - 1).to(dt).to(dev)
+    else:
+        x = torch.randint(-1000, 1000, (n,), generator=g).to(dt).to(dev)
+    acc = default_acc_dtype(dt, op)
+    out = torch.empty(1, dtype=acc, device=dev)
+    ch = open_channel(dev)
+    b = Reducer(dev).bind(x, op, acc, out=out, xrank=ch)
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):  # epochs 1..3: both mailbox parities
+        out.fill_(0)
+        b.launch(s)
+    torch.cuda.synchronize()
+    xd = x.double()
+    ref = {"sum": lambda: xd.sum(), "min": lambda: xd.min(), "max": lambda: xd.max(),
+           "sumsq": lambda: (xd * xd).sum(), "amax": lambda: xd.abs().max()}[op]().item()
+    got = out.item()
+    assert ch.error() == 0 and ch.epoch() == 3
+    if op in ("sum", "sumsq") and dt.is_floating_point:
+        from cuda_mpi_reductions_amd.ops import sum_tolerance
+        tol = sum_tolerance(dt, acc, n, (xd * xd).sum().item() if op == "sumsq" else xd.abs().sum().item())
+        assert abs(got - ref) <= tol, (got, ref, tol)
+    else:
+        assert got == ref
+
+
+# ---------------------------------------------------------------- bench: exact N-GPU step at N=1
+
+@pytest.mark.parametrize("collective", ["rccl", "fused"])
+def test_bench_torchrun_one_rank_graphs_both_modes(tmp_path, collective):
+    # the cross-rank combine is issued at world 1 and captured into graphs for both
+    # the pipelined headline and the serial measurement.
+    r = torchrun(1, [BENCH, "--gpus", "1", "--steps", "8", "--warmup", "2", "--elements", "50000017",
+                     "--collective", collective], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r)
+    assert d["verified"] is True and d["n_gpus"] == 1 and d["config"]["collective"] == collective
+    assert d["config"]["launch"].startswith("graph"), d["config"]["launch"]
+    assert d["serial_launch"].startswith("graph"), d["serial_launch"]
+    assert d["serial_gbps"] > 0 and d["serial_ms_per_step"] > 0
+    combine = d["config"]["cross_rank_combine"]
+    assert ("RCCL" in combine) if collective == "rccl" else ("fused" in combine)
+
+
+def test_bench_fused_two_lanes(tmp_path):
+    r = run([sys.executable, BENCH, "--steps", "24", "--warmup", "2", "--elements", "50000017", "--collective",
+             "fused", "--streams", "2", "--graph-chunk", "8"], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r)
+    assert d["verified"] is True and d["config"]["streams"] == 2
+    assert d["config"]["launch"].startswith("graph")
+
+
+# ---------------------------------------------------------------- several ranks on the one GPU
+
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_bench_fused_ranks_share_one_gpu(tmp_path, nproc, monkeypatch):
+    monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    r = torchrun(nproc, [BENCH, "--gpus", str(nproc), "--backend", "gloo", "--collective", "fused", "--steps", "10",
+                         "--warmup", "2", "--elements", "20000003", "--graph-chunk", "5"], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r)
+    assert d["verified"] is True and d["n_gpus"] == nproc
+    assert d["config"]["launch"].startswith("graph")
+
+
+def test_fused_missing_peer_times_out_not_hangs(tmp_path):
+    # Rank 1 never launches: rank 0's kernel must give up after its timeout, flag the channel
+    # (sticky: the next launch does not wait again) and the collective check must report it.
+    script = tmp_path / "xr.py"
+    script.write_text(
+        "import os, sys, time, torch\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import torch.distributed as dist\n"
+        "from cuda_mpi_reductions_amd.ops import Reducer\n"
+        "from cuda_mpi_reductions_amd.parallel.xrank import open_channel, check_channel\n"
+        "dist.init_process_group('gloo')\n"
+        "r = dist.get_rank()\n"
+        "dev = torch.device('cuda', 0); torch.cuda.set_device(dev)\n"
+        "x = torch.ones(1 << 20, dtype=torch.float64, device=dev)\n"
+        "out = torch.zeros(1, dtype=torch.float64, device=dev)\n"
+        "ch = open_channel(dev, timeout_s=0.5)\n"
+        "b = Reducer(dev).bind(x, 'sum', out=out, xrank=ch)\n"
+        "s = torch.cuda.current_stream().cuda_stream\n"
+        "t0 = time.time()\n"
+        "if r == 0:\n"
+        "    b.launch(s); torch.cuda.synchronize()\n"
+        "    t1 = time.time() - t0\n"
+        "    b.launch(s); torch.cuda.synchronize()\n"
+        "    t2 = time.time() - t0 - t1\n"
+        f"    open(os.path.join({str(tmp_path)!r}, 'res'), 'w').write('%d %.3f %.3f' % (ch.error(), t1, t2))\n"
+        "msg = check_channel([ch])\n"
+        f"open(os.path.join({str(tmp_path)!r}, 'msg%d' % r), 'w').write(str(msg))\n"
+        "dist.destroy_process_group()\n")
+    r = torchrun(2, [str(script)], timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    err, t1, t2 = (tmp_path / "res").read_text().split()
+    assert int(err) == 1 and 0.4 < float(t1) < 10 and float(t2) < 0.3
+    for k in range(2):
+        assert "timed out" in (tmp_path / f"msg{k}").read_text()

@@ -61,9 +61,10 @@ def parse_args(argv=None):
                    help="headline with no overlap between consecutive steps (default: pipelined headline, "
                         "serial reported as serial_gbps)")
     p.add_argument("--no-serial-measure", action="store_true", help="skip the second (serial) measurement")
-    p.add_argument("--collective", choices=["rccl", "fused"], default="rccl",
+    p.add_argument("--collective", choices=["auto", "rccl", "fused"], default="auto",
                    help="cross-rank combine: rccl = 1-element RCCL all-reduce after the local kernel; "
-                        "fused = the kernel's last workgroup folds all ranks' partials via IPC mailboxes")
+                        "fused = the kernel's last workgroup folds all ranks' partials via IPC mailboxes; "
+                        "auto = fused if its self-check passes on every rank, else rccl (GPU scalar configs)")
     p.add_argument("--local-only", action="store_true",
                    help="single rank: skip the cross-rank combine (by default it is issued even at N=1)")
     p.add_argument("--streams", type=int, default=1,
@@ -253,6 +254,29 @@ def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int) -> dict:
     return {"elapsed": elapsed, "launch": launch, "written": written}
 
 
+def _try_fused(wl, ctx) -> "str | None":
+    """Switch the workload to the fused in-kernel finish and check it on every rank: 3 steps, no
+    channel timeout, results equal to torch's reference. On any failure (agreed over ranks) switch
+    back to RCCL and return the reason."""
+    try:
+        wl.use_collective("fused")  # collective; raises on every rank if any rank cannot map
+    except Exception as e:  # noqa: BLE001
+        wl.use_collective("rccl")
+        return f"setup: {e}"[:300]
+    slots = wl.new_slots(3)
+    for i in range(3):
+        wl.step(slots[i:i + 1])
+    _sync(ctx.device)
+    err = wl.check()
+    if err is None:
+        ok, ref = _verify_slots(wl, slots, ctx)
+        if not ok:
+            err = f"self-check mismatch: {ref}"
+    if err is not None:
+        wl.use_collective("rccl")
+    return err
+
+
 def _verify_slots(wl, written: torch.Tensor, ctx) -> tuple:
     """Every slot must hold the global value (all steps reduce the same data); AND over ranks."""
     ref = wl.verify(written[-1:])
@@ -294,12 +318,21 @@ def main(argv=None) -> int:
                           nontemporal=None if args.policy == "auto" else args.policy == "nt",
                           single_pass=not args.two_pass)
     collective = args.collective
-    if collective == "fused" and (ctx.device.type != "cuda" or args.two_pass):
-        raise SystemExit("--collective fused needs GPUs and the single-pass kernel")
+    fused_ok = ctx.device.type == "cuda" and not args.two_pass and cfg.op not in LOC_OPS and not args.local_only
+    if collective == "fused" and not fused_ok:
+        raise SystemExit("--collective fused needs GPUs, the single-pass kernel and a non-LOC operator")
     # The cross-rank combine is issued even on one rank (--local-only skips it): N=1 runs the
     # exact step the N-GPU job runs.
-    wl = scalar_workload(cfg, ctx, kernel, streams=args.streams, collective=collective,
+    wl = scalar_workload(cfg, ctx, kernel, streams=args.streams, collective="rccl" if collective == "auto" else collective,
                          always_collective=not args.local_only).setup()
+    collective_note = None
+    if collective == "auto":
+        collective = "rccl"
+        if fused_ok:
+            collective_note = _try_fused(wl, ctx)
+            collective = "fused" if collective_note is None else "rccl"
+            if collective_note and ctx.is_root:
+                print(f"[bench] fused finish unavailable, using RCCL: {collective_note}", file=sys.stderr)
     K, W = args.steps, args.warmup
     dev = ctx.device
 
@@ -307,7 +340,9 @@ def main(argv=None) -> int:
     slots = wl.new_slots(W + K)
     m1 = _measure(wl, slots, ctx, args, fault, serial=primary_serial, warmup=W)
     m2 = None
-    if not primary_serial and not args.no_serial_measure:
+    if not primary_serial and not wl.issues_collective and len(wl.lanes) <= 1:
+        m2 = m1  # one kernel per step (fused finish): the pipelined run IS the serial run
+    elif not primary_serial and not args.no_serial_measure:
         # The honest per-reduction number: every step completes (local reduce AND cross-rank
         # combine) before the next one starts (reduction.cpp:319-374 times each reduction to
         # completion). Reported next to the pipelined headline.
@@ -318,7 +353,7 @@ def main(argv=None) -> int:
     err = wl.check()
     if not args.no_verify:
         ok, ref = _verify_slots(wl, slots[:m1["written"]], ctx)
-        if m2 is not None:
+        if m2 is not None and m2 is not m1:
             ok2, _ = _verify_slots(wl, slots2[:m2["written"]], ctx)
             ok = ok and ok2
         verified = ok and err is None
@@ -366,7 +401,8 @@ def main(argv=None) -> int:
                 "n_total_elements": wl.n_total,
                 "bytes_per_step": bytes_step,
                 "op": cfg.op.upper(),
-                "collective": collective,
+                "collective": collective + (f" (auto; fused unavailable: {collective_note})" if collective_note else
+                                            " (auto)" if args.collective == "auto" else ""),
                 "cross_rank_combine": combine,
                 "overlap": "serial (each step completes before the next)" if primary_serial else
                            ("pipelined (step i+1 local reduce || step i all-reduce)" if wl.issues_collective

@@ -52,20 +52,23 @@ constexpr uint64_t kNumDoubles = 256ull * 1024 * 1024;  // mpi/constants.h:2
 const std::set<std::string> kKnown = {"mode", "collective", "dtypes", "ops", "ints", "doubles", "longs", "floats",
                                       "n", "retries", "warmup", "iters", "root", "json", "graph", "mt19937",
                                       "noverify", "seed", "help", "unroll", "block", "wg-per-cu", "policy",
-                                      "units", "timeout", "trace", "single-process", "inject-fault"};
+                                      "units", "timeout", "trace", "single-process", "inject-fault",
+                                      "direct-grid"};
 
 struct Ctx {
   LaunchEnv env;
   int device = 0;
   std::unique_ptr<TcpBootstrap> boot;
   std::unique_ptr<RcclComm> comm;      // RCCL collectives
-  std::unique_ptr<DirectPeers> direct;  // --collective=direct|direct-reduce (peer reads over xGMI)
+  std::unique_ptr<DirectAllreduce> direct;  // --collective=direct|direct-reduce (peer reads over xGMI)
+  int direct_grid = 0;                       // workgroups per direct collective (0: one per CU)
   hipStream_t stream = nullptr;
   int retries = 5, warmup = 1, iters = 10, root = 0;
   std::string mode = "vector", collective, json;
   bool graph = false, verify = true, mt = false;
   uint64_t seed = 0x5EED;
   double timeout_s = 300;
+  double direct_timeout_s = 10;  // device-side wait bound of the direct kernels (--timeout sets both)
   bool units_gb = false;  // gnuplot column in 2^30 (reduce.c) unless --units=gb
   ReduceConfig kcfg;
   FaultInjector fault;  // --inject-fault / MIREDUCE_INJECT_FAULT (failure-detection tests)
@@ -122,6 +125,9 @@ uint64_t global_count(DType t, uint64_t ints, uint64_t longs, uint64_t floats, u
 void sync_stream(Ctx& c) {
   if (c.comm) c.comm->synchronize(c.stream, c.timeout_s);
   else HIP_CHECK(hipStreamSynchronize(c.stream));
+  // The direct kernels never hang on a lost peer: their bounded waits set a sticky error word.
+  if (c.direct && c.direct->error())
+    throw Error("direct: a peer's barrier flag never arrived (device-side wait timed out after --timeout)");
 }
 
 bool is_direct(const Ctx& c) { return c.collective == "direct" || c.collective == "direct-reduce"; }
@@ -241,7 +247,15 @@ bool run_vector(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>&
   if (is_direct(c)) {  // registered (IPC-shared) buffers sized for the largest dtype
     size_t mx = 0;
     for (auto& b : bufs) mx = std::max(mx, b.count * dtype_size(b.t));
-    c.direct = std::make_unique<DirectPeers>(*c.boot, c.device, mx);
+    c.direct = std::make_unique<DirectAllreduce>(c.device, mx, c.direct_grid, c.direct_timeout_s);
+    const std::vector<char> mine = c.direct->handles();
+    std::vector<char> all(mine.size() * c.env.world);
+    c.boot->allgather(mine.data(), all.data(), mine.size());
+    std::vector<std::vector<char>> hs(c.env.world);
+    for (int r = 0; r < c.env.world; ++r)
+      hs[r].assign(all.begin() + static_cast<long>(r * mine.size()), all.begin() + static_cast<long>((r + 1) * mine.size()));
+    c.direct->connect(c.env.rank, c.env.world, hs);
+    c.boot->barrier();  // every rank mapped every peer before the first collective
   }
   auto body_for = [&](B& b, Op o) {
     return [&c, &b, o] {
@@ -255,7 +269,7 @@ bool run_vector(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>&
   auto stage = [&](B& b) {  // direct mode: this dtype's data into the registered input buffer
     if (c.direct) {
       HIP_CHECK(hipMemcpyAsync(c.direct->in(), b.send.get(), b.count * dtype_size(b.t), hipMemcpyDeviceToDevice, c.stream));
-      HIP_CHECK(hipStreamSynchronize(c.stream));
+      HIP_CHECK(hipStreamSynchronize(c.stream));  // (the kernel's entry barrier orders it for the peers)
     }
   };
   const void* (*in_ptr)(Ctx&, B&) = [](Ctx& cc, B& bb) -> const void* { return cc.direct ? cc.direct->in() : bb.send.get(); };
@@ -532,13 +546,15 @@ void usage() {
       "  --dtypes=INT,DOUBLE  --ops=MAX,MIN,SUM  --retries=5  --warmup=1  --iters=10  --root=0\n"
       "  --ints=N --doubles=N --longs=N --floats=N   global element counts (reduce.c defaults)\n"
       "  --n=N                        global count for every dtype (scalar mode north star: 1e9)\n"
-      "  --graph                      replay the timed iterations from a captured hipGraph\n"
+      "  --graph                      replay the timed iterations from a captured hipGraph (any collective)\n"
+      "  --direct-grid=N              workgroups per direct collective (default: one per CU; same on all ranks)\n"
       "  --single-process[=N]         one process drives N (all) GPUs, scalar mode: grouped RCCL over\n"
       "                               ncclCommInitAll (--collective=allreduce) or host fold (--collective=host)\n"
       "  --mt19937                    vector mode: reduce.c's exact per-rank MT19937 data (host-generated)\n"
       "  --units=gib|gb               GNUPlot column unit (default gib = reduce.c's 2^30)\n"
       "  --json=PATH  --noverify  --seed=N  --block= --unroll= --wg-per-cu= --policy=auto|nt|default\n"
-      "  --timeout=S                  RCCL wait deadline (s); bootstrap: MIREDUCE_BOOTSTRAP_TIMEOUT\n"
+      "  --timeout=S                  RCCL wait deadline / direct kernels' device-side wait bound (s);\n"
+      "                               bootstrap: MIREDUCE_BOOTSTRAP_TIMEOUT\n"
       "  --inject-fault=KIND[@RANK][:STEP]  exit|hang|corrupt|delay=<ms> at a timed collective (tests)\n"
       "launch: torchrun --nproc-per-node=8 --master-addr 127.0.0.1 ... | mpirun -np 8 ...\n");
 }
@@ -613,15 +629,15 @@ int main(int argc, char** argv) {
     c.root = args.int_or<int>("root", c.root);
     c.json = args.str_or("json", "");
     c.graph = args.has("graph");
-    if (c.graph && (c.collective == "direct" || c.collective == "direct-reduce"))
-      throw CliError("--graph cannot capture the host-synchronised direct collectives");
+    c.direct_grid = args.int_or<int>("direct-grid", 0);
+    if (c.direct_grid < 0 || c.direct_grid > kMaxDirectBlocks) throw CliError("--direct-grid must be 0..1024");
     set_tracing(args.has("trace"));
     c.mt = args.has("mt19937");
     c.verify = !args.has("noverify");
     c.seed = args.int_or<uint64_t>("seed", c.seed);
     c.units_gb = args.str_or("units", "gib") == "gb";
     double to = 0;
-    if (args.get_double("timeout", &to)) c.timeout_s = to;
+    if (args.get_double("timeout", &to)) c.timeout_s = c.direct_timeout_s = to;
     try {
       c.fault = FaultInjector::from_flag_or_env(args.str_or("inject-fault", ""));
     } catch (const std::invalid_argument& e) {

@@ -15,6 +15,7 @@
 #include "mireduce/arg_reduce.hpp"
 #include "mireduce/check.hpp"
 #include "mireduce/cpu_reference.hpp"
+#include "mireduce/direct.hpp"
 #include "mireduce/ladder.hpp"
 #include "mireduce/moments.hpp"
 #include "mireduce/mt19937.hpp"
@@ -204,6 +205,37 @@ PYBIND11_MODULE(_C, m) {
       .def("epoch", &XrankChannel::epoch)
       .def("clear_error", &XrankChannel::clear_error);
   m.attr("XRANK_MAX_RANKS") = kMaxXrankRanks;
+
+  // One-kernel direct all-reduce / reduce over IPC-mapped peer buffers (direct.hpp): exchange
+  // handles() with every rank, connect(), copy data into in_ptr, then allreduce()/reduce().
+  py::class_<DirectAllreduce, std::shared_ptr<DirectAllreduce>>(m, "DirectAllreduce")
+      .def(py::init<int, size_t, int, double>(), py::arg("device") = -1, py::arg("bytes") = 16,
+           py::arg("grid") = 0, py::arg("timeout_s") = 10.0)
+      .def("handles", [](const DirectAllreduce& d) {
+        const std::vector<char> h = d.handles();
+        return py::bytes(h.data(), h.size());
+      })
+      .def("connect", [](DirectAllreduce& d, int rank, int world, const std::vector<py::bytes>& all) {
+        std::vector<std::vector<char>> hs;
+        for (const auto& b : all) {
+          const std::string s = b;
+          hs.emplace_back(s.begin(), s.end());
+        }
+        d.connect(rank, world, hs);
+      }, py::arg("rank"), py::arg("world"), py::arg("handles"))
+      .def_property_readonly("in_ptr", [](const DirectAllreduce& d) { return reinterpret_cast<uintptr_t>(d.in()); })
+      .def_property_readonly("out_ptr", [](const DirectAllreduce& d) { return reinterpret_cast<uintptr_t>(d.out()); })
+      .def_property_readonly("bytes", &DirectAllreduce::bytes)
+      .def_property_readonly("grid", &DirectAllreduce::grid)
+      .def_property_readonly("connected", &DirectAllreduce::connected)
+      .def("allreduce", [](DirectAllreduce& d, uint64_t count, int dtype, int op, uintptr_t stream) {
+        d.allreduce(count, static_cast<DType>(dtype), static_cast<Op>(op), as_stream(stream));
+      }, py::arg("count"), py::arg("dtype"), py::arg("op"), py::arg("stream") = 0)
+      .def("reduce", [](DirectAllreduce& d, uint64_t count, int dtype, int op, int root, uintptr_t stream) {
+        d.reduce(count, static_cast<DType>(dtype), static_cast<Op>(op), root, as_stream(stream));
+      }, py::arg("count"), py::arg("dtype"), py::arg("op"), py::arg("root") = 0, py::arg("stream") = 0)
+      .def("error", &DirectAllreduce::error)
+      .def("epoch", &DirectAllreduce::epoch);
 
   m.def(
       "reduce",

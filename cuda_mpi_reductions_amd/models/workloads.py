@@ -67,7 +67,8 @@ CONFIGS: dict[str, WorkloadConfig] = {
     "xgmi_1b_double_sum": WorkloadConfig(
         name="xgmi_1b_double_sum", dtype=torch.float64, op="sum", n_total=1_000_000_000,
         baseline=92.7729, baseline_source="mpi/CUdata.txt:2 (CUDA DOUBLE SUM, best reference GB/s)",
-        description="1B double sum across N MI355X: local HIP reduce + RCCL all-reduce over xGMI",
+        description="1B double sum across N MI355X: local HIP reduce + cross-rank combine over xGMI "
+                    "(fused in-kernel mailbox exchange, or a 1-element RCCL all-reduce)",
     ),
     "xgmi_1b_double_norm2": WorkloadConfig(
         name="xgmi_1b_double_norm2", dtype=torch.float64, op="sumsq", n_total=1_000_000_000,
@@ -194,6 +195,28 @@ class ScalarReduction:
         elif self.collective == "fused":
             raise RuntimeError("the fused cross-rank finish needs GPUs")
         return self
+
+    def use_collective(self, collective: str) -> None:
+        """Re-bind every lane for another cross-rank combine (e.g. fall back from ``fused`` to
+        ``rccl``), keeping the data. Collective when switching to ``fused``."""
+        if collective not in COLLECTIVES:
+            raise ValueError(f"collective must be one of {COLLECTIVES}")
+        if self.ctx.device.type != "cuda":
+            self.collective = collective
+            return
+        if collective == "fused":
+            from ..parallel.xrank import open_channel
+        lanes, self.channels = [], []
+        for stream, reducer, _, _ in self.lanes:
+            ch = open_channel(self.ctx.device, timeout_s=self.xrank_timeout_s) if collective == "fused" else None
+            bound = reducer.bind(self.x, self.cfg.op, self.acc, out=self._bound_out, xrank=ch)
+            lanes.append((stream, reducer, bound, ch))
+            if ch is not None:
+                self.channels.append(ch)
+        self.lanes = lanes
+        self.bound = lanes[0][2]
+        self.collective = collective
+        torch.cuda.synchronize(self.ctx.device)
 
     @property
     def bytes_total(self) -> int:

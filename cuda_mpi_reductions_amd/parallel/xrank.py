@@ -13,6 +13,7 @@ allocates a mailbox, the IPC handles are all-gathered, every peer's mailbox is m
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -27,19 +28,39 @@ def open_channel(device: torch.device, group=None, timeout_s: float = 2.0):
     """Create and connect this rank's :class:`_C.XrankChannel` (collective)."""
     C = native()
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    ch = C.XrankChannel(idx, timeout_s)
-    if dist.is_available() and dist.is_initialized():
-        world = dist.get_world_size(group)
-        rank = dist.get_rank(group)
-        if world > C.XRANK_MAX_RANKS:
-            raise ValueError(f"fused finish supports at most {C.XRANK_MAX_RANKS} ranks, got {world}")
-        handles: list = [None] * world
-        dist.all_gather_object(handles, ch.handle(), group=group)
-    else:
-        rank, world, handles = 0, 1, [ch.handle()]
-    ch.connect(rank, world, handles)
-    if world > 1:
-        dist.barrier(group=group)  # every rank mapped every mailbox before anyone pushes
+    if not (dist.is_available() and dist.is_initialized()):
+        ch = C.XrankChannel(idx, timeout_s)
+        ch.connect(0, 1, [ch.handle()])
+        return ch
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if world > C.XRANK_MAX_RANKS:
+        raise ValueError(f"fused finish supports at most {C.XRANK_MAX_RANKS} ranks, got {world}")
+    # Every step below is reached by every rank (errors are agreed on, not raised mid-protocol),
+    # so one rank's failure to allocate or map cannot leave the others blocked in a collective.
+    err, ch, handle = None, None, b""
+    try:
+        if os.environ.get("MIREDUCE_XRANK_FAIL_RANK") == str(rank):  # failure-path test hook
+            raise RuntimeError("injected mailbox failure (MIREDUCE_XRANK_FAIL_RANK)")
+        ch = C.XrankChannel(idx, timeout_s)
+        handle = ch.handle()
+    except Exception as e:  # noqa: BLE001 - reported collectively below
+        err = f"{type(e).__name__}: {e}"
+    handles: list = [None] * world
+    dist.all_gather_object(handles, handle, group=group)
+    if err is None:
+        if any(not h for h in handles):
+            err = "a peer could not create its mailbox"
+        else:
+            try:
+                ch.connect(rank, world, handles)
+            except Exception as e:  # noqa: BLE001
+                err = f"{type(e).__name__}: {e}"
+    errs: list = [None] * world
+    dist.all_gather_object(errs, err, group=group)  # also the barrier: all mailboxes mapped
+    bad = [f"rank {r}: {m}" for r, m in enumerate(errs) if m]
+    if bad:
+        raise RuntimeError("fused cross-rank finish unavailable: " + "; ".join(bad)[:500])
     return ch
 
 

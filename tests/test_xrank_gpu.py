@@ -133,3 +133,24 @@ def test_fused_missing_peer_times_out_not_hangs(tmp_path):
     assert int(err) == 1 and 0.4 < float(t1) < 10 and float(t2) < 0.3
     for k in range(2):
         assert "timed out" in (tmp_path / f"msg{k}").read_text()
+
+
+def test_bench_auto_falls_back_to_rccl_on_every_rank(tmp_path, monkeypatch):
+    # One rank cannot create its mailbox: every rank must agree and run the RCCL/gloo combine.
+    monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    monkeypatch.setenv("MIREDUCE_XRANK_FAIL_RANK", "1")
+    r = torchrun(2, [BENCH, "--gpus", "2", "--backend", "gloo", "--steps", "4", "--warmup", "1",
+                     "--elements", "20000003"], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r)
+    assert d["verified"] is True
+    assert d["config"]["collective"].startswith("rccl (auto; fused unavailable"), d["config"]["collective"]
+
+
+def test_bench_auto_picks_fused(tmp_path):
+    r = run([sys.executable, BENCH, "--steps", "6", "--warmup", "2", "--elements", "50000017"], cwd=tmp_path,
+            timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r)
+    assert d["verified"] is True and d["config"]["collective"] == "fused (auto)"
+    assert d["serial_gbps"] == d["value"]

@@ -65,6 +65,12 @@ def parse_args(argv=None):
                    help="cross-rank combine: rccl = 1-element RCCL all-reduce after the local kernel; "
                         "fused = the kernel's last workgroup folds all ranks' partials via IPC mailboxes; "
                         "auto = fused if its self-check passes on every rank, else rccl (GPU scalar configs)")
+    p.add_argument("--vector-impl", choices=["rccl", "direct"], default="rccl",
+                   help="vector (reduce.c) configs: torch.distributed collective, or the one-kernel direct "
+                        "peer-read collective over xGMI (GPUs)")
+    p.add_argument("--no-vector-extras", dest="vector_extras", action="store_false",
+                   help="north-star runs also time reduce.c's element-wise 2 GiB DOUBLE SUM (reduce / allreduce, "
+                        "RCCL and direct) and report it as reduce_c_vector; this skips that")
     p.add_argument("--local-only", action="store_true",
                    help="single rank: skip the cross-rank combine (by default it is issued even at N=1)")
     p.add_argument("--streams", type=int, default=1,
@@ -143,39 +149,45 @@ def _time_torch_reduction(wl, K: int, W: int, ctx) -> float:
     return wl.bytes_total * K / el / 1e9
 
 
-def run_vector(args, ctx, cfg, fault) -> int:
-    """reduce.c semantics (BASELINE config 1): element-wise reduce of an N/P vector per rank to
-    root 0. Each collective is timed on its own between a barrier and a synchronisation (the
-    in-place buffer is restored outside the clock, like reduce.c's bzero, mpi/reduce.c:74-77);
-    the step time is the MAX over ranks; GB = 2^30 B of total data (mpi/reduce.c:79)."""
-    from cuda_mpi_reductions_amd.models import VectorReduction
-    wl = VectorReduction(cfg, ctx).setup(mt19937=(ctx.device.type == "cpu"))
+def _time_vector(wl, ctx, K: int, W: int, fault, verify: bool) -> tuple:
+    """Time K element-wise collectives (after W warm-ups), each on its own between a barrier and a
+    synchronisation (the in-place buffer is restored outside the clock, like reduce.c's bzero,
+    mpi/reduce.c:74-77); returns (sum over steps of the MAX-over-ranks time, verified)."""
     dev = ctx.device
-    for i in range(args.warmup):
+    for i in range(W):
         wl.restore()
-        if fault.enabled and fault.at(ctx.rank, i, "bench step"):
-            wl.y.view(-1)[0] += 1
+        if fault is not None and fault.enabled and fault.at(ctx.rank, i, "bench step"):
+            wl.corrupt()
         wl.collective()
     times, checks = [], []
-    holder = cfg.collective == "allreduce" or ctx.rank == 0
-    for i in range(args.warmup, args.warmup + args.steps):
+    holder = wl.cfg.collective == "allreduce" or ctx.rank == 0
+    for i in range(W, W + K):
         wl.restore()
-        if fault.enabled and fault.at(ctx.rank, i, "bench step"):
-            wl.y.view(-1)[0] += 1  # this rank contributes a wrong element: verification must fail
+        if fault is not None and fault.enabled and fault.at(ctx.rank, i, "bench step"):
+            wl.corrupt()  # this rank contributes a wrong element: verification must fail
         _sync(dev)
         pdist.barrier(ctx)
         t0 = time.perf_counter()
         wl.collective()
         _sync(dev)
         times.append(pdist.max_over_ranks(time.perf_counter() - t0, ctx))
-        if not args.no_verify and holder:  # per-step checksum (untimed): every step must agree
-            checks.append(wl.y.to(torch.float64).sum().reshape(1))
-    elapsed = sum(times)
+        if verify and holder:  # per-step checksum (untimed): every step must agree
+            checks.append(wl.result().to(torch.float64).sum().reshape(1))
     verified = None
-    if not args.no_verify:
+    if verify:
         same = bool((torch.cat(checks) == checks[-1]).all().item()) if checks else True
         same = -pdist.max_over_ranks(-float(same), ctx) > 0.5  # AND over ranks
         verified = wl.verify()["ok"] and same
+    return sum(times), verified
+
+
+def run_vector(args, ctx, cfg, fault) -> int:
+    """reduce.c semantics (BASELINE config 1): element-wise reduce of an N/P vector per rank to
+    root 0; the step time is the MAX over ranks; GB = 2^30 B of total data (mpi/reduce.c:79)."""
+    from cuda_mpi_reductions_amd.models import VectorReduction
+    wl = VectorReduction(cfg, ctx, impl=args.vector_impl).setup(mt19937=(ctx.device.type == "cpu"))
+    dev = ctx.device
+    elapsed, verified = _time_vector(wl, ctx, args.steps, args.warmup, fault, not args.no_verify)
     gib = wl.bytes_total * args.steps / elapsed / float(1 << 30)
     if ctx.is_root:
         print(json.dumps({
@@ -183,14 +195,43 @@ def run_vector(args, ctx, cfg, fault) -> int:
             "value": round(gib, 3), "unit": "GiB/s", "n_gpus": ctx.world_size if dev.type == "cuda" else 0,
             "n_ranks": ctx.world_size, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": str(cfg.dtype).replace("torch.", ""), "device": dev.type,
+            "vs_baseline": round(gib / cfg.baseline, 3) if cfg.baseline else None,
+            "dtype": str(cfg.dtype).replace("torch.", ""), "device": dev.type,
             "data": "reduce.c MT19937 per-rank data" if dev.type == "cpu" else "synthetic rank-seeded device fill",
             "config": {"model": f"{cfg.name}: {cfg.description}", "global_batch": wl.count * ctx.world_size,
                        "seq_len": 1, "parallelism": f"dp{ctx.world_size}", "backend": ctx.backend,
-                       "op": cfg.op.upper(), "count_per_rank": wl.count},
+                       "impl": wl.impl, "op": cfg.op.upper(), "count_per_rank": wl.count},
+            "baseline_value": cfg.baseline, "baseline_unit": cfg.baseline_unit if cfg.baseline else None,
+            "baseline_source": cfg.baseline_source or None,
             "verified": verified,
         }), flush=True)
     return 0 if verified in (None, True) else 1
+
+
+def _vector_extras(ctx, steps: int = 5) -> dict:
+    """reduce.c's own measurement on this job's GPUs, next to the scalar headline: element-wise
+    DOUBLE SUM of 2 GiB of total data (NUM_DOUBLES, mpi/constants.h:2) to root 0 (MPI_Reduce,
+    reduce.c:90) and to every rank, over RCCL and over the direct one-kernel collective; RETRY_COUNT
+    (5) timed collectives each; GiB/s of total data (reduce.c:93). Errors are recorded, not raised."""
+    from dataclasses import replace as _replace
+
+    from cuda_mpi_reductions_amd.models import CONFIGS as _C, VectorReduction
+    out = {"units": "GiB/s (2^30 B of total data per collective, reduce.c:93)", "dtype": "DOUBLE", "op": "SUM",
+           "total_bytes": 256 * 1024 * 1024 * 8}
+    for collective in ("reduce", "allreduce"):
+        cfg = _replace(_C["xgmi_2g_double_sum_reduce"], collective=collective)
+        for impl in ("rccl", "direct"):
+            key = f"{collective}_{impl}"
+            try:
+                wl = VectorReduction(cfg, ctx, impl=impl, direct_timeout_s=5.0).setup()
+                el, ok = _time_vector(wl, ctx, steps, 1, None, True)
+                out[key] = {"gibps": round(wl.bytes_total * steps / el / float(1 << 30), 3),
+                            "ms": round(el / steps * 1e3, 4), "verified": ok}
+                del wl
+            except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
+                out[key] = {"error": f"{type(e).__name__}: {e}"[:200]}
+            torch.cuda.empty_cache()
+    return out
 
 
 def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int) -> dict:
@@ -365,6 +406,9 @@ def main(argv=None) -> int:
     torch_gbps = None
     if args.compare_torch and dev.type == "cuda":
         torch_gbps = _time_torch_reduction(wl, K, W, ctx)
+    extras = None
+    if args.vector_extras and dev.type == "cuda" and cfg.name == NORTH_STAR:
+        extras = _vector_extras(ctx)
     bytes_step = wl.bytes_total
     elapsed = m1["elapsed"]
     gbps = bytes_step * K / elapsed / 1e9
@@ -424,6 +468,8 @@ def main(argv=None) -> int:
             line["serial_launch"] = m2["launch"]
         if torch_gbps is not None:
             line["torch_gbps"] = round(torch_gbps, 3)  # same data, torch's own reduction kernels
+        if extras is not None:
+            line["reduce_c_vector"] = extras
         print(json.dumps(line), flush=True)
     _sync(dev)
     pdist.shutdown(ctx)

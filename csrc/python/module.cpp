@@ -206,6 +206,12 @@ PYBIND11_MODULE(_C, m) {
       .def("clear_error", &XrankChannel::clear_error);
   m.attr("XRANK_MAX_RANKS") = kMaxXrankRanks;
 
+  // Stream-ordered device copy between raw pointers (registered IPC buffers <-> torch tensors).
+  m.def("memcpy_d2d", [](uintptr_t dst, uintptr_t src, uint64_t bytes, uintptr_t stream) {
+    check_hip(hipMemcpyAsync(as_ptr<void>(dst), as_ptr<const void>(src), bytes, hipMemcpyDeviceToDevice,
+                             as_stream(stream)), "hipMemcpyAsync");
+  }, py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("stream") = 0);
+
   // One-kernel direct all-reduce / reduce over IPC-mapped peer buffers (direct.hpp): exchange
   // handles() with every rank, connect(), copy data into in_ptr, then allreduce()/reduce().
   py::class_<DirectAllreduce, std::shared_ptr<DirectAllreduce>>(m, "DirectAllreduce")

@@ -23,7 +23,7 @@ import torch
 from ..ops import KernelConfig, Reducer, default_acc_dtype, fill_, sum_tolerance
 from ..parallel import dist as pdist
 
-__all__ = ["WorkloadConfig", "CONFIGS", "NORTH_STAR", "COLLECTIVES", "ScalarReduction", "VectorReduction",
+__all__ = ["WorkloadConfig", "CONFIGS", "NORTH_STAR", "COLLECTIVES", "VECTOR_IMPLS", "ScalarReduction", "VectorReduction",
            "element_size"]
 
 
@@ -53,6 +53,20 @@ CONFIGS: dict[str, WorkloadConfig] = {
         name="mpi_1m_int32_sum_cpu2", dtype=torch.int32, op="sum", n_total=1 << 20,
         mode="vector", collective="reduce", pattern="fullrange", device="cpu",
         description="1M int32 sum via MPI_Reduce on 2 CPU ranks (reduce.c plumbing, no GPU)",
+    ),
+    "xgmi_2g_double_sum_reduce": WorkloadConfig(
+        name="xgmi_2g_double_sum_reduce", dtype=torch.float64, op="sum", n_total=256 * 1024 * 1024,
+        mode="vector", collective="reduce", baseline=60.97540, baseline_unit="GiB/s",
+        baseline_source="mpi/results/DOUBLE_SUM.txt:2 (MPI_Reduce DOUBLE SUM, BG/L 1024 ranks)",
+        description="reduce.c on GPUs: element-wise DOUBLE SUM of NUM_DOUBLES (2 GiB total) to root 0, "
+                    "N/P per rank (mpi/reduce.c:90, mpi/constants.h:2)",
+    ),
+    "xgmi_2g_int_sum_reduce": WorkloadConfig(
+        name="xgmi_2g_int_sum_reduce", dtype=torch.int32, op="sum", n_total=512 * 1024 * 1024,
+        mode="vector", collective="reduce", pattern="fullrange", baseline=146.81800, baseline_unit="GiB/s",
+        baseline_source="mpi/results/INT_SUM.txt:2 (MPI_Reduce INT SUM, BG/L 1024 ranks)",
+        description="reduce.c on GPUs: element-wise INT SUM of NUM_INTS (2 GiB total) to root 0, N/P per "
+                    "rank (mpi/reduce.c:76, mpi/constants.h:1)",
     ),
     "gpu_256m_double_sum": WorkloadConfig(
         name="gpu_256m_double_sum", dtype=torch.float64, op="sum", n_total=256 * 1024 * 1024,
@@ -330,16 +344,32 @@ class ScalarReduction:
         return {"ok": bool(ok), "got": got, "expected": exp, "tolerance": tol}
 
 
-class VectorReduction:
-    """reduce.c semantics: each rank holds N/P elements; element-wise reduce to root 0 (or all)."""
+VECTOR_IMPLS = ("rccl", "direct")
 
-    def __init__(self, cfg: WorkloadConfig, ctx: pdist.DistContext, seed: int = 0x5EED):
+
+class VectorReduction:
+    """reduce.c semantics: each rank holds N/P elements; element-wise reduce to root 0 (or all).
+
+    ``impl``: ``"rccl"`` — ``torch.distributed`` reduce / all_reduce (RCCL on GPUs, gloo on CPUs);
+    ``"direct"`` — the one-kernel peer-read collective over xGMI (:class:`parallel.DirectComm`,
+    GPUs only): x is staged into the registered input buffer by ``restore()`` (outside the clock,
+    like reduce.c's bzero) and the result read back from the registered output by ``verify()``.
+    """
+
+    def __init__(self, cfg: WorkloadConfig, ctx: pdist.DistContext, seed: int = 0x5EED, impl: str = "rccl",
+                 direct_grid: int = 0, direct_timeout_s: float = 10.0):
+        if impl not in VECTOR_IMPLS:
+            raise ValueError(f"impl must be one of {VECTOR_IMPLS}")
         self.cfg = cfg
         self.ctx = ctx
         self.seed = seed
+        self.impl = impl
+        self.direct_grid = direct_grid
+        self.direct_timeout_s = direct_timeout_s
         self.count = cfg.n_total // ctx.world_size if cfg.n_total else 0
         self.x: Optional[torch.Tensor] = None
         self.y: Optional[torch.Tensor] = None
+        self.comm = None
 
     def setup(self, mt19937: bool = False) -> "VectorReduction":
         dev = self.ctx.device
@@ -352,6 +382,12 @@ class VectorReduction:
             # per-rank distinct streams, like reduce.c's rank-seeded generator
             fill_(self.x, self.cfg.pattern, seed=self.seed + self.ctx.rank, offset=0)
         self.y = torch.empty_like(self.x)
+        if self.impl == "direct":
+            if dev.type != "cuda":
+                raise RuntimeError("the direct collective needs GPUs")
+            from ..parallel.direct import DirectComm
+            self.comm = DirectComm(dev, max(16, self.x.numel() * self.x.element_size()),
+                                   grid=self.direct_grid, timeout_s=self.direct_timeout_s)
         return self
 
     @property
@@ -362,12 +398,42 @@ class VectorReduction:
 
     def restore(self) -> None:
         """Reset the in-place collective buffer (reduce.c's bzero of the receive buffer)."""
-        self.y.copy_(self.x)
+        if self.comm is not None:
+            from .._native import native
+            native().memcpy_d2d(self.comm._d.in_ptr, self.x.data_ptr(), self.x.numel() * self.x.element_size(),
+                                torch.cuda.current_stream(self.ctx.device).cuda_stream)
+        else:
+            self.y.copy_(self.x)
 
     def collective(self, async_op: bool = False):
+        if self.comm is not None:
+            if self.cfg.collective == "reduce":
+                self.comm.launch_reduce(self.count, self.cfg.dtype, self.cfg.op, root=0)
+            else:
+                self.comm.launch_allreduce(self.count, self.cfg.dtype, self.cfg.op)
+            return None
         if self.cfg.collective == "reduce":
             return pdist.vector_reduce(self.y, self.cfg.op, root=0, async_op=async_op)
         return pdist.vector_allreduce(self.y, self.cfg.op, async_op=async_op)
+
+    def corrupt(self) -> None:
+        """Fault injection: this rank's staged contribution at element 0 becomes wrong (the clean
+        ``x`` still defines the expected result, so verification must fail)."""
+        if self.comm is not None:
+            from .._native import native
+            bad = self.x[:1] + 1
+            native().memcpy_d2d(self.comm._d.in_ptr, bad.data_ptr(), bad.element_size(),
+                                torch.cuda.current_stream(self.ctx.device).cuda_stream)
+        else:
+            self.y.view(-1)[0] += 1
+
+    def result(self) -> torch.Tensor:
+        """This rank's result buffer (meaningful on the holders: root for reduce, all for allreduce)."""
+        if self.comm is not None:
+            from .._native import native
+            native().memcpy_d2d(self.y.data_ptr(), self.comm._d.out_ptr, self.y.numel() * self.y.element_size(),
+                                torch.cuda.current_stream(self.ctx.device).cuda_stream)
+        return self.y
 
     def step(self, async_op: bool = False):
         self.restore()
@@ -376,6 +442,7 @@ class VectorReduction:
     def verify(self) -> dict:
         """Gather every rank's input and combine on the result holders; integer SUM wraps like
         MPI_INT / ncclInt32 (two's complement)."""
+        self.result()
         world = self.ctx.world_size
         gathered = [torch.empty_like(self.x) for _ in range(world)]
         if world > 1:
@@ -400,6 +467,8 @@ class VectorReduction:
             else:
                 exp = st.min(0).values if self.cfg.op == "min" else st.max(0).values
                 ok = bool(torch.equal(exp, self.y))
+        if self.comm is not None and self.comm.check() is not None:
+            ok = False
         t = torch.tensor([1 if ok else 0], dtype=torch.int32,
                          device=self.ctx.device if self.ctx.backend == "nccl" else "cpu")
         if world > 1:

@@ -154,3 +154,46 @@ def test_bench_auto_picks_fused(tmp_path):
     d = _json(r)
     assert d["verified"] is True and d["config"]["collective"] == "fused (auto)"
     assert d["serial_gbps"] == d["value"]
+
+
+# ---------------------------------------------------------------- direct collective from Python
+
+def test_direct_comm_world1_views_and_staging():
+    from cuda_mpi_reductions_amd.parallel import DirectComm
+    dev = torch.device("cuda", 0)
+    comm = DirectComm(dev, 1 << 20)
+    t = torch.arange(1000, dtype=torch.float64, device=dev)
+    ref = t.clone()
+    comm.allreduce(t, "sum")
+    torch.cuda.synchronize()
+    assert torch.equal(t, ref) and comm.check() is None and comm.epoch == 1
+    iv, ov = comm.in_view(77, torch.int32), comm.out_view(77, torch.int32)
+    iv.copy_(torch.arange(77, dtype=torch.int32, device=dev) - 30)
+    comm.launch_reduce(77, torch.int32, "max", root=0)
+    torch.cuda.synchronize()
+    assert torch.equal(ov, iv) and comm.epoch == 2
+
+
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_bench_vector_direct_ranks_share_one_gpu(tmp_path, nproc, monkeypatch):
+    # reduce.c semantics through bench.py with the direct one-kernel collective (verified against the
+    # gathered inputs), and the same over the torch.distributed path for comparison.
+    monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    for impl in ("direct",):  # (gloo cannot reduce GPU tensors; RCCL refuses 2 ranks on 1 GPU)
+        r = torchrun(nproc, [BENCH, "--gpus", str(nproc), "--backend", "gloo", "--device", "cuda", "--config",
+                             "xgmi_2g_double_sum_reduce", "--elements", "3000017", "--steps", "4", "--warmup", "1",
+                             "--vector-impl", impl],
+                     cwd=tmp_path, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        d = _json(r)
+        assert d["verified"] is True and d["config"]["impl"] == impl and d["unit"] == "GiB/s"
+
+
+def test_bench_vector_extras_in_headline(tmp_path):
+    r = run([sys.executable, BENCH, "--steps", "4", "--warmup", "1", "--elements", "50000017"], cwd=tmp_path,
+            timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r)
+    ex = d["reduce_c_vector"]
+    for k in ("reduce_rccl", "reduce_direct", "allreduce_rccl", "allreduce_direct"):
+        assert ex[k].get("verified") is True and ex[k]["gibps"] > 0, (k, ex[k])

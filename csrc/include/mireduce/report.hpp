@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <map>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace mireduce {
@@ -52,5 +53,12 @@ class Json {
 };
 
 std::string json_escape(const std::string& s);
+
+// Peer (xGMI) bandwidth test (bandwidth_test --peer): the ordered (src, dst) device pairs, src !=
+// dst, row-major — the simpleP2P copy of cuda/C/src/simpleP2P/simpleP2P.cu:314-329 for every pair.
+std::vector<std::pair<int, int>> peer_pairs(int ndev);
+// Matrix table of per-pair values (rows = src, columns = dst, ndev x ndev row-major; "-" on the
+// diagonal), one line per source device.
+std::string peer_matrix(int ndev, const std::vector<double>& values, const char* unit);
 
 }  // namespace mireduce

@@ -101,4 +101,36 @@ bool Json::write_file(const std::string& path) const {
   return static_cast<bool>(f);
 }
 
+
+std::vector<std::pair<int, int>> peer_pairs(int ndev) {
+  std::vector<std::pair<int, int>> v;
+  for (int s = 0; s < ndev; ++s)
+    for (int d = 0; d < ndev; ++d)
+      if (s != d) v.emplace_back(s, d);
+  return v;
+}
+
+std::string peer_matrix(int ndev, const std::vector<double>& values, const char* unit) {
+  std::string out = std::string("   src\\dst (") + unit + ")";
+  char buf[64];
+  out += "\n      ";
+  for (int d = 0; d < ndev; ++d) {
+    std::snprintf(buf, sizeof buf, "%9d", d);
+    out += buf;
+  }
+  out += "\n";
+  for (int s = 0; s < ndev; ++s) {
+    std::snprintf(buf, sizeof buf, "%6d", s);
+    out += buf;
+    for (int d = 0; d < ndev; ++d) {
+      const size_t k = static_cast<size_t>(s) * ndev + d;
+      if (s == d || k >= values.size()) std::snprintf(buf, sizeof buf, "%9s", "-");
+      else std::snprintf(buf, sizeof buf, "%9.1f", values[k]);
+      out += buf;
+    }
+    out += "\n";
+  }
+  return out;
+}
+
 }  // namespace mireduce

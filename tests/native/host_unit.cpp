@@ -25,6 +25,25 @@ static int g_fail = 0;
     }                                                                     \
   } while (0)
 
+static void test_peer_plan() {
+  // bandwidth_test --peer: ordered pairs, no self pairs, row-major; matrix table shape
+  CHECK(peer_pairs(0).empty() && peer_pairs(1).empty());
+  const auto p2 = peer_pairs(2);
+  CHECK(p2.size() == 2 && p2[0] == std::make_pair(0, 1) && p2[1] == std::make_pair(1, 0));
+  const auto p8 = peer_pairs(8);
+  CHECK(p8.size() == 56);
+  for (auto [s, d] : p8) CHECK(s != d && s >= 0 && d < 8);
+  std::vector<double> v(9, 0.0);
+  v[1] = 12.5;
+  v[3] = 99.0;
+  const std::string t = peer_matrix(3, v, "GB/s");
+  CHECK(t.find("12.5") != std::string::npos && t.find("99.0") != std::string::npos);
+  CHECK(t.find("(GB/s)") != std::string::npos);
+  int lines = 0;
+  for (char c : t) lines += c == '\n';
+  CHECK(lines == 5);  // title, column header, 3 source rows
+}
+
 static void test_cli() {
   const char* argv[] = {"prog", "--method=SUM", "-type=double", "--cpufinal", "-n=16M", "--list=a,b,,c", "--neg=-5"};
   CmdArgs a(7, argv);
@@ -138,6 +157,7 @@ static void test_fault_spec() {
 
 int main() {
   test_cli();
+  test_peer_plan();
   test_fault_spec();
   test_types();
   test_mt();

@@ -41,6 +41,15 @@ def test_reduction_waives_without_gpu_and_qa_lines(tmp_path):
     assert "&&&& WAIVED reduction --method=SUM --qatest" in r.stderr
 
 
+def test_bandwidth_peer_waives_below_two_devices():
+    # bandwidth_test --peer (xGMI roofline, simpleP2P parity) on a host with fewer than two visible
+    # devices: a clear WAIVED line, QA protocol, exit 0 (HIP_VISIBLE_DEVICES=-1 also hides any GPU).
+    r = run([os.path.join(BIN, "bandwidth_test"), "--peer", "--qatest"], env={"HIP_VISIBLE_DEVICES": "-1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert re.search(r"Peer-to-peer \(xGMI\) bandwidth: \d visible device\(s\), needs >= 2 -> WAIVED", r.stdout)
+    assert "&&&& WAIVED bandwidth_test --peer --qatest" in r.stderr
+
+
 def test_reduction_help(tmp_path):
     r = run([os.path.join(BIN, "reduction"), "--help"], cwd=tmp_path)
     assert r.returncode == 0 and "--cpufinal" in r.stdout and "--shmoo" in r.stdout

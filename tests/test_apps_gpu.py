@@ -106,6 +106,19 @@ def test_bandwidth_test_app():
     r = run([os.path.join(BIN, "bandwidth_test"), "--size=256M", "--iters=5"], timeout=300)
     assert r.returncode == 0, r.stderr
     assert "Device to Device copy" in r.stdout and "Read stream" in r.stdout
+    assert "peer_read kernel, local" in r.stdout
+
+
+def test_bandwidth_peer_on_this_box(tmp_path):
+    # One GPU on the test box: WAIVED; on a node with >= 2 GPUs: every ordered pair measured.
+    js = tmp_path / "peer.json"
+    r = run([os.path.join(BIN, "bandwidth_test"), "--peer", "--size=16M", "--iters=5", f"--json={js}"], timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    if "WAIVED" in r.stdout:
+        assert "1 visible device(s)" in r.stdout
+    else:
+        d = json.loads(js.read_text().splitlines()[-1])
+        assert d["node_ingress_gbps"] > 0 and d["all_pairs_peer_access"] is True
 
 
 def test_cpp_consumer_example():

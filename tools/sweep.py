@@ -11,6 +11,13 @@ reduce.c-format line into ``<out>/collected.txt``, averages them (tools/getAvgs.
     python tools/sweep.py --app reduce_xgmi --ranks 1,2,4,8 --out runs/vector -- --mode=vector
     python tools/sweep.py --app bench --ranks 1,2,4,8 --out runs/bench -- --steps 50 --warmup 10
     python tools/sweep.py --app reduce_mpi --ranks 2,4 --out runs/mpi -- --ints=1M --doubles=1M
+    python tools/sweep.py --preset node --out runs/node      # the whole 1/2/4/8-GPU matrix below
+
+``--preset node`` runs, resumable point by point: the xGMI roofline (``bandwidth_test --peer``, once);
+reduce.c's vector benchmark over every collective — RCCL ``reduce`` / ``allreduce`` and the one-kernel
+direct ``direct-reduce`` / ``direct`` (csrc/kernels/direct.hip), each graph-replayed — at every rank
+count; and the north-star bench.py at every rank count. Each entry gets its own collected.txt /
+results/ (getAvgs format) under ``<out>/<name>/``.
 """
 from __future__ import annotations
 
@@ -51,9 +58,89 @@ def command(app: str, p: int, extra: list[str]) -> list[str]:
     return tr + [target] + args
 
 
+VECTOR_COLLECTIVES = ("reduce", "allreduce", "direct-reduce", "direct")
+
+
+def node_preset(extra: list[str]) -> list[tuple]:
+    """(app, name, ranks or None for one single-process run, args) of ``--preset node``."""
+    entries = [("bandwidth_test", "fabric", None, ["--peer", "--json=fabric.json"])]
+    for coll in VECTOR_COLLECTIVES:
+        entries.append(("reduce_xgmi", f"vector-{coll}", "ranks",
+                        ["--mode=vector", f"--collective={coll}", "--graph", "--dtypes=INT,DOUBLE"] + extra))
+    entries.append(("bench", "bench", "ranks", ["--steps", "50", "--warmup", "10"]))
+    return entries
+
+
+def run_points(app: str, name: str, ranks: list, extra: list[str], out: str, timeout: float, force: bool) -> int:
+    failures = 0
+    for p in ranks:
+        base = os.path.join(out, f"stdout-{name}-P{p}")
+        rc_path = base + ".rc"
+        if not force and os.path.exists(rc_path) and open(rc_path).read().strip() == "0":
+            print(f"[sweep] {name} P={p}: done, skipping ({base}.txt)")
+            continue
+        if p is None:  # one single-process run (all visible GPUs)
+            cmd = [os.path.join(ROOT, "build", "bin", app)] + extra
+        else:
+            cmd = command(app, p, extra)
+        print(f"[sweep] {name} P={p}: {' '.join(cmd)}", flush=True)
+        t0 = time.time()
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=out)
+            rc, stdout, err = r.returncode, r.stdout, r.stderr
+        except subprocess.TimeoutExpired as e:
+            rc, stdout, err = 124, e.stdout or "", (e.stderr or "") + "\n[sweep] timeout"
+        with open(base + ".txt", "w") as f:
+            f.write(stdout if isinstance(stdout, str) else stdout.decode())
+        with open(base + ".err", "w") as f:
+            f.write(err if isinstance(err, str) else err.decode())
+        with open(rc_path, "w") as f:
+            f.write(f"{rc}\n")
+        print(f"[sweep] {name} P={p}: rc={rc} in {time.time() - t0:.1f} s", flush=True)
+        failures += rc != 0
+    return failures
+
+
+def run_preset(a) -> int:
+    ranks = [int(x) for x in a.ranks.split(",") if x]
+    failures = 0
+    for app, name, rk, args in node_preset(a.extra):
+        sub = os.path.join(a.out, name)
+        os.makedirs(sub, exist_ok=True)
+        failures += run_points(app, name, [None] if rk is None else ranks, args, sub, a.timeout, a.force)
+        collect(sub, name)
+    return 1 if failures else 0
+
+
+def collect(out: str, name: str) -> None:
+    collected, jsonl = [], []
+    for fn in sorted(os.listdir(out)):
+        if fn.startswith(f"stdout-{name}-P") and fn.endswith(".txt"):
+            for line in open(os.path.join(out, fn)):
+                if line.startswith("{"):
+                    jsonl.append(line.strip())
+                elif not line.startswith("#") and len(line.split()) == 4:
+                    collected.append(line)
+    if collected:
+        cpath = os.path.join(out, "collected.txt")
+        with open(cpath, "w") as f:
+            f.writelines(collected)
+        getavgs.write_results(cpath, os.path.join(out, "results"))
+    if jsonl:
+        with open(os.path.join(out, "bench.jsonl"), "w") as f:
+            f.write("\n".join(jsonl) + "\n")
+        rows = [json.loads(j) for j in jsonl]
+        base1 = next((r["value"] for r in rows if r.get("n_gpus") == 1), None)
+        for r in sorted(rows, key=lambda r: r.get("n_gpus", 0)):
+            eff = (r["value"] / (r["n_gpus"] * base1)) if base1 else float("nan")
+            print(f"[sweep] N={r['n_gpus']}: {r['value']:.1f} {r['unit']}  ms/step {r['ms_per_step']}  "
+                  f"scaling efficiency {eff:.3f}")
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
-    ap.add_argument("--app", required=True, choices=["bench", "reduce_xgmi", "reduce_mpi", "reduction"])
+    ap.add_argument("--app", choices=["bench", "reduce_xgmi", "reduce_mpi", "reduction"])
+    ap.add_argument("--preset", choices=["node"], help="run a predefined matrix instead of one --app")
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--out", required=True)
     ap.add_argument("--name", default="")
@@ -62,53 +149,14 @@ def main(argv=None) -> int:
     ap.add_argument("extra", nargs="*")
     a = ap.parse_args(argv)
     os.makedirs(a.out, exist_ok=True)
+    if a.preset:
+        return run_preset(a)
+    if not a.app:
+        ap.error("--app or --preset is required")
     name = a.name or a.app
-    failures = 0
-    for p in [int(x) for x in a.ranks.split(",") if x]:
-        base = os.path.join(a.out, f"stdout-{name}-P{p}")
-        rc_path = base + ".rc"
-        if not a.force and os.path.exists(rc_path) and open(rc_path).read().strip() == "0":
-            print(f"[sweep] P={p}: done, skipping ({base}.txt)")
-            continue
-        cmd = command(a.app, p, a.extra)
-        print(f"[sweep] P={p}: {' '.join(cmd)}", flush=True)
-        t0 = time.time()
-        try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=a.timeout)
-            rc, out, err = r.returncode, r.stdout, r.stderr
-        except subprocess.TimeoutExpired as e:
-            rc, out, err = 124, e.stdout or "", (e.stderr or "") + "\n[sweep] timeout"
-        with open(base + ".txt", "w") as f:
-            f.write(out if isinstance(out, str) else out.decode())
-        with open(base + ".err", "w") as f:
-            f.write(err if isinstance(err, str) else err.decode())
-        with open(rc_path, "w") as f:
-            f.write(f"{rc}\n")
-        print(f"[sweep] P={p}: rc={rc} in {time.time() - t0:.1f} s", flush=True)
-        failures += rc != 0
-    # collect
-    collected, jsonl = [], []
-    for fn in sorted(os.listdir(a.out)):
-        if fn.startswith(f"stdout-{name}-P") and fn.endswith(".txt"):
-            for line in open(os.path.join(a.out, fn)):
-                if line.startswith("{"):
-                    jsonl.append(line.strip())
-                elif not line.startswith("#") and len(line.split()) == 4:
-                    collected.append(line)
-    if collected:
-        cpath = os.path.join(a.out, "collected.txt")
-        with open(cpath, "w") as f:
-            f.writelines(collected)
-        getavgs.write_results(cpath, os.path.join(a.out, "results"))
-    if jsonl:
-        with open(os.path.join(a.out, "bench.jsonl"), "w") as f:
-            f.write("\n".join(jsonl) + "\n")
-        rows = [json.loads(j) for j in jsonl]
-        base1 = next((r["value"] for r in rows if r["n_gpus"] == 1), None)
-        for r in sorted(rows, key=lambda r: r["n_gpus"]):
-            eff = (r["value"] / (r["n_gpus"] * base1)) if base1 else float("nan")
-            print(f"[sweep] N={r['n_gpus']}: {r['value']:.1f} {r['unit']}  ms/step {r['ms_per_step']}  "
-                  f"scaling efficiency {eff:.3f}")
+    ranks = [int(x) for x in a.ranks.split(",") if x]
+    failures = run_points(a.app, name, ranks, a.extra, os.path.abspath(a.out), a.timeout, a.force)
+    collect(a.out, name)
     return 1 if failures else 0
 
 

@@ -14,7 +14,7 @@
 // ranks of the per-iteration time is reported (fixes reduce.c's root-only, barrier-less rdtsc,
 // bug B8). Verification: vector mode checks sampled indices against the host-combined inputs of
 // all ranks; scalar mode checks the all-reduced value against the host fold of every rank's
-// local result and each local result against the two-launch oracle path.
+// local result and each local result against the ladder's kernel 6 (an independent kernel).
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -36,6 +36,7 @@
 #include "mireduce/device.hpp"
 #include "mireduce/direct.hpp"
 #include "mireduce/fault.hpp"
+#include "mireduce/ladder.hpp"
 #include "mireduce/mt19937.hpp"
 #include "mireduce/reduce.hpp"
 #include "mireduce/report.hpp"
@@ -365,9 +366,10 @@ bool run_scalar(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>&
           unsigned char g[8] = {0}, l[8] = {0}, orc[8] = {0};
           HIP_CHECK(hipMemcpy(g, out.get(), 8, hipMemcpyDeviceToHost));
           reduce(x.get(), count, t, o, acc, loc.get(), ws, c.stream, c.kcfg);
-          ReduceConfig two = c.kcfg;
-          two.single_pass = false;
-          reduce(x.get(), count, t, o, acc, oracle.get(), ws, c.stream, two);
+          // Independent oracle for the local result: the ladder's kernel 6 (a different kernel,
+          // grid and fold order), not the streaming kernel's other mode.
+          DeviceBuffer lscratch(ladder_scratch_bytes(6, count, 256, 1024));
+          ladder_reduce(6, x.get(), count, t, o, acc, oracle.get(), lscratch.get(), 256, 1024, c.stream);
           HIP_CHECK(hipStreamSynchronize(c.stream));
           HIP_CHECK(hipMemcpy(l, loc.get(), 8, hipMemcpyDeviceToHost));
           HIP_CHECK(hipMemcpy(orc, oracle.get(), 8, hipMemcpyDeviceToHost));

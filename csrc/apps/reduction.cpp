@@ -86,7 +86,8 @@ void usage() {
       "reduction --method=SUM|MIN|MAX [options]\n"
       "  --type=int|int64|float|double  element type (case-insensitive, default int)\n"
       "  --n=N            elements (default 16777216; k/M/G suffixes and 1e9 accepted)\n"
-      "  --threads=256|512|1024  workgroup size (default: tuned plan; 256 = reference)\n"
+      "  --threads=N             workgroup size, a power of two (default: tuned plan; 256 = reference);\n"
+      "                          kernels 0..6 take 1..1024, kernels 7/8 256|512|1024 (smaller: 256)\n"
       "  --kernel=0..8    7 = single-pass (default), 8 = two-launch, 0..6 = Harris ladder\n"
       "  --maxblocks=N    cap the grid (default: persistent grid, 8 WG/CU)\n"
       "  --cpufinal       fold the per-workgroup partials on the host\n"
@@ -157,10 +158,27 @@ struct Runner {
     return c;
   }
 
-  // Returns true if the result was produced on the host into host_out.
+  int passes = 0;             // kernel launches of the last run_once
+  uint64_t host_folded = 0;   // partials folded on the host by the last run_once (0: none)
+  const void* result_dev = nullptr;  // where the device result of the last run_once is
+
+  // The reference's host fold of what the relaunch loop left (reduction.cpp:332,362-370).
+  bool host_fold_partials(const void* partials, uint64_t left, unsigned char* host_out) {
+    HIP_CHECK(hipMemcpyAsync(b.pinned, partials, left * dtype_size(o.acc), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    cpu_fold(b.pinned, left, o.acc, o.op, host_out);
+    host_folded = left;
+    return true;
+  }
+
+  // One timed reduction, as benchmarkReduce* (reduction.cpp:319-374): first pass, then relaunches
+  // on the partials while more than --cputhresh remain (none with --cpufinal), then a host fold of
+  // what is left. Returns true if the result was produced on the host into host_out.
   bool run_once(uint64_t n, unsigned char* host_out) {
     TraceRange tr("reduction.iteration");
     const void* in = b.in.get();
+    host_folded = 0;
+    result_dev = b.out.get();
     if (o.kernel <= 6) {
       const int mb = o.max_blocks > 0 ? o.max_blocks : 64;  // reference default (reduction.cpp:668)
       const int th = o.threads ? o.threads : 256;            // reference default (reduction.cpp:666)
@@ -169,25 +187,26 @@ struct Runner {
         HIP_CHECK(hipStreamSynchronize(s));
         b.ladder.allocate(need);
       }
+      const LadderPasses lp = ladder_reduce_passes(o.kernel, in, n, o.dtype, o.op, o.acc, b.out.get(), b.ladder.get(),
+                                                   th, mb, o.cputhresh, o.cpufinal, s);
       plan.block = th;
-      plan.grid = ladder_reduce(o.kernel, in, n, o.dtype, o.op, o.acc, b.out.get(), b.ladder.get(), th, mb, s);
-      return false;
+      plan.grid = lp.first_grid;
+      passes = lp.passes;
+      return lp.left > 1 ? host_fold_partials(lp.partials, lp.left, host_out) : false;
     }
     const bool want_host = o.cpufinal || o.cputhresh > 1;
     if (!want_host) {
       plan = reduce(in, n, o.dtype, o.op, o.acc, b.out.get(), ws, s, cfg());
+      passes = plan.single_pass ? 1 : 2;
       return false;
     }
-    plan = reduce_partials(in, n, o.dtype, o.op, o.acc, b.partials.get(), ws.max_grid(), ws.num_cus(), s, cfg());
-    const size_t es = dtype_size(o.acc);
-    if (!o.cpufinal && plan.grid > o.cputhresh) {  // device finalisation, like the relaunch loop
-      reduce_finalize(b.partials.get(), plan.grid, o.acc, o.op, b.out.get(), s);
-      return false;
-    }
-    HIP_CHECK(hipMemcpyAsync(b.pinned, b.partials.get(), plan.grid * es, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
-    cpu_fold(b.pinned, plan.grid, o.acc, o.op, host_out);
-    return true;
+    const ReducePasses rp = reduce_passes(in, n, o.dtype, o.op, o.acc, b.partials.get(), ws.max_grid(), ws.num_cus(),
+                                          o.cputhresh, o.cpufinal, s, cfg());
+    plan = rp.plan;
+    passes = rp.passes;
+    if (rp.left > 1 || o.cpufinal) return host_fold_partials(rp.partials, rp.left, host_out);
+    result_dev = rp.partials;  // one partial left: the result, in place like d_odata[0]
+    return false;
   }
 };
 
@@ -202,7 +221,7 @@ Timing time_iterations(Runner& r, uint64_t n, int iters) {
   Timing t;
   EventTimer ev;
   HIP_CHECK(hipDeviceSynchronize());
-  const bool host_path = r.o.kernel >= 7 && (r.o.cpufinal || r.o.cputhresh > 1);
+  const bool host_path = r.o.cpufinal || r.o.cputhresh > 1;
   if (r.o.cold && r.b.flush.bytes() < kFlushBytes) r.b.flush.allocate(kFlushBytes);
   if (r.o.batch_timing && !host_path && !r.o.cold) {  // back-to-back launches, one event pair: throughput
     ev.start(r.s);
@@ -211,7 +230,7 @@ Timing time_iterations(Runner& r, uint64_t n, int iters) {
     const double ms = ev.elapsed_ms();
     t.ms.assign(iters, ms / iters);
     t.avg_ms = ms / iters;
-    HIP_CHECK(hipMemcpy(t.result, r.b.out.get(), dtype_size(r.o.acc), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(t.result, r.result_dev, dtype_size(r.o.acc), hipMemcpyDeviceToHost));
     return t;
   }
   for (int i = 0; i < iters; ++i) {
@@ -233,7 +252,7 @@ Timing time_iterations(Runner& r, uint64_t n, int iters) {
   double sum = 0;
   for (double m : t.ms) sum += m;
   t.avg_ms = iters ? sum / iters : 0;
-  if (!t.host_result) HIP_CHECK(hipMemcpy(t.result, r.b.out.get(), dtype_size(r.o.acc), hipMemcpyDeviceToHost));
+  if (!t.host_result) HIP_CHECK(hipMemcpy(t.result, r.result_dev, dtype_size(r.o.acc), hipMemcpyDeviceToHost));
   return t;
 }
 
@@ -338,7 +357,7 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
   const size_t es = dtype_size(o.dtype);
   b.in.allocate(std::max<uint64_t>(o.n, 1) * es);
   b.out.allocate(8);
-  b.partials.allocate(static_cast<size_t>(std::max(ws.max_grid(), 1 << 16)) * 8);
+  b.partials.allocate(2 * static_cast<size_t>(std::max(ws.max_grid(), 1 << 16)) * 8);  // ping-pong passes
   HIP_CHECK(hipHostMalloc(&b.pinned, static_cast<size_t>(std::max(ws.max_grid(), 1 << 16)) * 8, hipHostMallocDefault));
 
   FillSpec fs;
@@ -369,6 +388,7 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
   unsigned char cpu[8] = {0};
   double tol = 0;
   bool checked = false;
+  std::string oracle = "host reference (Kahan / exact)";
   if (o.verify && host_copy) {
     cpu_reduce(b.host.data(), o.n, o.dtype, o.op, o.acc, cpu);
     checked = true;
@@ -383,26 +403,47 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
       ok = acc_as_int64(t.result, o.acc) == acc_as_int64(cpu, o.acc);
     }
   } else if (o.verify) {
-    // Huge device-filled arrays: the two-launch path (different combine order and code path) is
-    // the oracle for the single-pass kernel.
-    Options o2 = o;
-    o2.kernel = (o.kernel == 8) ? 7 : 8;
-    o2.cpufinal = false;
-    o2.cputhresh = 1;
-    Runner r2{o2, ws, b, s};
-    r2.run_once(o.n, scratch);
-    HIP_CHECK(hipMemcpy(cpu, b.out.get(), dtype_size(o.acc), hipMemcpyDeviceToHost));
+    // Huge device-filled arrays (no host copy), independent oracles:
+    //  * --pattern=iotamod: the closed-form result (no device code involved);
+    //  * reference element types: the ladder's kernel 6 (a different kernel, grid and fold);
+    //  * bf16/fp16 or fused ops: the other streaming path (two-launch vs single-pass).
     checked = true;
-    if (dtype_is_float(o.acc) && (o.op == Op::Sum || o.op == Op::SumSq)) {
-      const double g = acc_as_double(t.result, o.acc), c = acc_as_double(cpu, o.acc);
-      tol = 1e-9 * std::fabs(c) + 1e-12;
-      ok = std::fabs(g - c) <= tol;
+    const bool summed_f = dtype_is_float(o.acc) && (o.op == Op::Sum || o.op == Op::SumSq);
+    if (o.pattern == Pattern::IotaMod && analytic_iotamod(o.n, 0, o.dtype, o.op, o.acc, cpu)) {
+      oracle = "closed-form iotamod";
+      if (summed_f && o.acc == DType::Float32) {
+        const double g = acc_as_double(t.result, o.acc), c = acc_as_double(cpu, o.acc);
+        tol = sum_tolerance(o.dtype, o.acc, o.n, std::fabs(c));
+        ok = std::fabs(g - c) <= tol;
+      } else {
+        ok = std::memcmp(t.result, cpu, dtype_size(o.acc)) == 0;  // exact: integer-valued terms
+      }
     } else {
-      ok = std::memcmp(t.result, cpu, dtype_size(o.acc)) == 0;
+      Options o2 = o;
+      const bool ladder_ok = !dtype_is_half(o.dtype) && !op_is_fused(o.op);
+      o2.kernel = ladder_ok ? 6 : (o.kernel == 8 ? 7 : 8);
+      o2.threads = ladder_ok ? 256 : o.threads;
+      o2.max_blocks = ladder_ok ? 1024 : o.max_blocks;
+      o2.cpufinal = false;
+      o2.cputhresh = 1;
+      oracle = ladder_ok ? "ladder kernel 6" : (o2.kernel == 7 ? "single-pass kernel 7" : "two-launch kernel 8");
+      Runner r2{o2, ws, b, s};
+      r2.run_once(o.n, scratch);
+      HIP_CHECK(hipStreamSynchronize(s));
+      HIP_CHECK(hipMemcpy(cpu, r2.result_dev, dtype_size(o.acc), hipMemcpyDeviceToHost));
+      if (summed_f) {
+        const double g = acc_as_double(t.result, o.acc), c = acc_as_double(cpu, o.acc);
+        tol = 1e-9 * std::fabs(c) + 1e-12;
+        ok = std::fabs(g - c) <= tol;
+      } else {
+        ok = std::memcmp(t.result, cpu, dtype_size(o.acc)) == 0;
+      }
     }
   }
   L.log(kLogBoth, "\nGPU result = %s\n", fmt_result(t.result, o.acc).c_str());
   if (checked) L.log(kLogBoth, "CPU result = %s\n\n", fmt_result(cpu, o.acc).c_str());
+  if (r.passes > 1 || r.host_folded)
+    L.log(kLogBoth, "%d kernel pass(es), %" PRIu64 " partial(s) folded on the host\n", r.passes, r.host_folded);
 
   if (!o.json.empty()) {
     Stats st = compute_stats(t.ms);
@@ -417,7 +458,8 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
         .set("gib_per_s", secs > 0 ? bytes / secs / kGiB : 0.0).set("bytes_per_GB", kGB)
         .set("gpu_result", acc_as_double(t.result, o.acc)).set("verified", checked ? ok : true)
         .set("tolerance", tol).set("device", di.name).set("arch", di.arch).set("cus", di.cus)
-        .set("iteration_ms", t.ms);
+        .set("passes", r.passes).set("host_folded", r.host_folded).set("cputhresh", o.cputhresh)
+        .set("oracle", checked ? oracle : std::string("none")).set("iteration_ms", t.ms);
     j.write_file(o.json);
   }
   return ok;
@@ -547,11 +589,18 @@ int main(int argc, char** argv) {
       throw CliError("--kernel 0..6 (the reference's ladder) implement SUM/MIN/MAX; SUMSQ/AMAX use kernels 7/8");
     if (o.kernel <= 6 && dtype_is_half(o.dtype))
       throw CliError("--kernel 0..6 (the reference's ladder) covers int/int64/float/double; bf16/half use kernels 7/8");
-    if (o.kernel >= 7 && o.threads != 0 && o.threads != 256 && o.threads != 512 && o.threads != 1024)
-      throw CliError("--threads must be 256, 512 or 1024 for kernels 7/8");
+    // The reference accepts any power of two up to 512 (reduction.cpp:272-291, instantiations
+    // reduction_kernel.cu:292-343). The ladder (0..6) runs every one of them (and 1024); the
+    // streaming kernels (7/8) use whole-CU workgroups of 256/512/1024 — a smaller request is
+    // rounded up to 256 with a note, so parity runs of the reference's flag values still run.
+    if (o.threads != 0 && (o.threads < 1 || o.threads > 1024 || (o.threads & (o.threads - 1))))
+      throw CliError("--threads must be a power of two in [1, 1024]");
+    if (o.kernel >= 7 && o.threads != 0 && o.threads < 256) {
+      std::fprintf(stderr, "note: --threads=%d: kernels 7/8 use 256/512/1024-thread workgroups; using 256\n",
+                   o.threads);
+      o.threads = 256;
+    }
     if (o.kernel <= 6 && o.threads == 0) o.threads = 256;
-    if (o.kernel <= 6 && (o.threads < 64 || o.threads > 1024 || (o.threads & (o.threads - 1))))
-      throw CliError("--threads must be a power of two in [64, 1024] for kernels 0..6");
     if (o.iterations < 1) throw CliError("--iterations must be >= 1");
     o.arg = args.has("arg");
     if (o.arg && o.op != Op::Min && o.op != Op::Max) throw CliError("--arg needs --method=MIN or MAX");

@@ -28,6 +28,12 @@ void cpu_fold(const void* partials, size_t count, DType acc, Op op, void* out);
 double sum_tolerance(DType t, DType acc, size_t n, double abs_sum);
 
 // Value of the first element of an accumulator-typed buffer as double / int64 (for printing).
+// Closed-form result of reducing n elements of the IotaMod pattern (x[i] = i mod 1024, i from
+// `offset`) — an oracle for arrays too large to copy to the host that shares no code with any
+// device kernel. Exact for integer accumulators and for fp64; returns
+// false for 16-bit element types (their elements above 256 are rounded). Writes `acc` bytes.
+bool analytic_iotamod(uint64_t n, uint64_t offset, DType t, Op op, DType acc, void* out);
+
 double acc_as_double(const void* p, DType acc);
 int64_t acc_as_int64(const void* p, DType acc);
 

@@ -24,7 +24,8 @@
 
 namespace mireduce {
 
-// First-pass launch geometry, as getNumBlocksAndThreads (reduction.cpp:272-291).
+// First-pass launch geometry, as getNumBlocksAndThreads (reduction.cpp:272-291); any power-of-two
+// thread count up to 1024 (blocks narrower than a wave reduce over their active lanes).
 void ladder_geometry(int kernel, uint64_t n, int max_threads, int max_blocks, int* blocks, int* threads);
 
 // Bytes of scratch ladder_reduce needs for (kernel, n) — two ping-pong partial buffers.
@@ -34,5 +35,19 @@ size_t ladder_scratch_bytes(int kernel, uint64_t n, int max_threads, int max_blo
 // ladder_scratch_bytes(...) bytes. Returns the first-pass grid size.
 int ladder_reduce(int kernel, const void* in, uint64_t n, DType t, Op op, DType acc, void* out,
                   void* scratch, int max_threads, int max_blocks, hipStream_t stream);
+
+// The reference's timed multi-pass reduction (benchmarkReduce*, reduction.cpp:319-374): first
+// pass, then relaunches on the partials while more than `cpu_thresh` remain (--cputhresh), or none
+// at all with `cpu_final` (--cpufinal). `left` == 1: the result is in out[0]; `left` > 1: the
+// remaining partials (acc type) are at `partials` (inside scratch) for the caller's host fold.
+struct LadderPasses {
+  int first_grid = 0;
+  int passes = 0;             // kernel launches
+  uint64_t left = 0;          // partials remaining
+  const void* partials = nullptr;
+};
+LadderPasses ladder_reduce_passes(int kernel, const void* in, uint64_t n, DType t, Op op, DType acc, void* out,
+                                  void* scratch, int max_threads, int max_blocks, uint64_t cpu_thresh,
+                                  bool cpu_final, hipStream_t stream);
 
 }  // namespace mireduce

@@ -117,6 +117,21 @@ LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, 
                            int max_grid, int num_cus, hipStream_t stream,
                            const ReduceConfig& cfg = {});
 
+// The reference's timed multi-pass reduction (benchmarkReduce*, reduction.cpp:319-374) on the
+// streaming kernel: first level into partials, then the same first-level kernel relaunched on
+// the partials (ping-pong, never in place) while more than `cpu_thresh` remain; `cpu_final`:
+// first level only (--cpufinal, reduction.cpp:328-340). The `left` partials (acc type; 1 = the
+// result) are at `partials`, inside `scratch` (>= 2 * max_grid * 8 bytes), for a host fold.
+struct ReducePasses {
+  LaunchPlan plan;          // first level
+  int passes = 0;           // kernel launches
+  uint64_t left = 0;
+  const void* partials = nullptr;
+};
+ReducePasses reduce_passes(const void* in, size_t n, DType t, Op op, DType acc, void* scratch, int max_grid,
+                           int num_cus, uint64_t cpu_thresh, bool cpu_final, hipStream_t stream,
+                           const ReduceConfig& cfg = {});
+
 // Fold `count` partials on the device with one workgroup.
 void reduce_finalize(const void* partials, size_t count, DType acc, Op op, void* out,
                      hipStream_t stream);

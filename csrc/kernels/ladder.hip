@@ -23,10 +23,14 @@
 namespace mireduce {
 namespace ladder {
 
+// Butterfly over the first `width` lanes (a power of two <= 64): lane l only ever reads lane
+// l ^ off < width, so a block of fewer than 64 threads (the reference accepts --threads down to 1,
+// reduction.cpp:272-291) never reads an inactive lane.
 template <class OpT, class AccT>
-__device__ __forceinline__ AccT wave_tail(AccT v) {
+__device__ __forceinline__ AccT wave_tail(AccT v, unsigned width = 64) {
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = OpT::apply(v, __shfl_xor(v, off, 64));
+  for (unsigned off = 32; off > 0; off >>= 1)
+    if (off < width) v = OpT::apply(v, __shfl_xor(v, off, 64));
   return v;
 }
 
@@ -88,7 +92,7 @@ __global__ void k34(const Tin* __restrict__ in, uint64_t n, AccT* __restrict__ o
     if (tid < 64) {
       v = sdata[tid];
       if (blockDim.x >= 128) v = OpT::apply(v, sdata[tid + 64]);
-      v = wave_tail<OpT>(v);
+      v = wave_tail<OpT>(v, blockDim.x < 64 ? blockDim.x : 64);
       if (tid == 0) out[blockIdx.x] = v;
     }
   }
@@ -103,7 +107,7 @@ __device__ __forceinline__ void unrolled_tail(AccT* sdata, AccT v, AccT* out) {
   if constexpr (BLOCK >= 256) { if (tid < 128) sdata[tid] = v = OpT::apply(v, sdata[tid + 128]); __syncthreads(); }
   if (tid < 64) {
     if constexpr (BLOCK >= 128) v = OpT::apply(v, sdata[tid + 64]);
-    v = wave_tail<OpT>(v);
+    v = wave_tail<OpT>(v, BLOCK < 64 ? BLOCK : 64);
     if (tid == 0) out[blockIdx.x] = v;
   }
 }
@@ -163,38 +167,53 @@ void launch(int kernel, const void* vin, uint64_t n, AccT* dst, int blocks, int 
     case 4: hipLaunchKernelGGL((k34<4, OpT, Tin, AccT>), dim3(blocks), dim3(threads), smem, s, in, n, dst); break;
     default:
       switch (threads) {
+        case 1: launch_block<1, OpT>(kernel, in, n, dst, blocks, s); break;
+        case 2: launch_block<2, OpT>(kernel, in, n, dst, blocks, s); break;
+        case 4: launch_block<4, OpT>(kernel, in, n, dst, blocks, s); break;
+        case 8: launch_block<8, OpT>(kernel, in, n, dst, blocks, s); break;
+        case 16: launch_block<16, OpT>(kernel, in, n, dst, blocks, s); break;
+        case 32: launch_block<32, OpT>(kernel, in, n, dst, blocks, s); break;
         case 64: launch_block<64, OpT>(kernel, in, n, dst, blocks, s); break;
         case 128: launch_block<128, OpT>(kernel, in, n, dst, blocks, s); break;
         case 256: launch_block<256, OpT>(kernel, in, n, dst, blocks, s); break;
         case 512: launch_block<512, OpT>(kernel, in, n, dst, blocks, s); break;
         case 1024: launch_block<1024, OpT>(kernel, in, n, dst, blocks, s); break;
-        default: throw Error("ladder: threads must be a power of two in [64, 1024]");
+        default: throw Error("ladder: threads must be a power of two in [1, 1024]");
       }
   }
   MIREDUCE_HIP_THROW(hipGetLastError());
 }
 
 template <class OpT, class T, class AccT>
-int run(int kernel, const void* in, uint64_t n, void* out, void* scratch, int max_threads, int max_blocks,
-        hipStream_t s) {
+LadderPasses run(int kernel, const void* in, uint64_t n, void* out, void* scratch, int max_threads, int max_blocks,
+                 uint64_t cpu_thresh, bool cpu_final, hipStream_t s) {
   int blocks = 0, threads = 0;
   ladder_geometry(kernel, n, max_threads, max_blocks, &blocks, &threads);
   AccT* a = static_cast<AccT*>(scratch);
   AccT* b = a + std::max(blocks, 1);
   AccT* dst = blocks == 1 ? static_cast<AccT*>(out) : a;
   launch<OpT, T, AccT>(kernel, in, n, dst, blocks, threads, s);
+  LadderPasses r;
+  r.first_grid = blocks;
+  r.passes = 1;
   uint64_t left = static_cast<uint64_t>(blocks);
   AccT* cur = a;
   AccT* other = b;
-  while (left > 1) {  // the reference's relaunch loop (reduction.cpp:344-357), ping-pong buffers
+  // The reference's relaunch loop (reduction.cpp:344-357): the same kernel on the partials while
+  // more than cputhresh remain (ping-pong buffers instead of in place); --cpufinal stops after the
+  // first pass (reduction.cpp:328-340). What is left (> 1) is folded on the host by the caller.
+  while (!cpu_final && left > std::max<uint64_t>(cpu_thresh, 1)) {
     int b2 = 0, t2 = 0;
     ladder_geometry(kernel, left, max_threads, max_blocks, &b2, &t2);
     AccT* d2 = b2 == 1 ? static_cast<AccT*>(out) : other;
     launch<OpT, AccT, AccT>(kernel, cur, left, d2, b2, t2, s);
     left = static_cast<uint64_t>(b2);
+    ++r.passes;
     std::swap(cur, other);
   }
-  return blocks;
+  r.left = left;
+  r.partials = left > 1 ? static_cast<const void*>(cur) : out;
+  return r;
 }
 
 }  // namespace ladder
@@ -208,7 +227,7 @@ void ladder_geometry(int kernel, uint64_t n, int max_threads, int max_blocks, in
     t = n < 2ull * max_threads ? ladder::next_pow2((n + 1) / 2) : max_threads;
     b = (n + t * 2 - 1) / (t * 2);
   }
-  if (t < 64) t = 64;  // at least one full wave64
+  if (t < 1) t = 1;  // (any power of two: sub-wave blocks reduce over their active lanes only)
   if (kernel == 6 && b > static_cast<uint64_t>(max_blocks)) b = max_blocks;
   if (b < 1) b = 1;
   MIREDUCE_REQUIRE(b <= 0x7FFFFFFFull, "ladder: grid too large; use kernel 6 or 7 for this size");
@@ -224,13 +243,20 @@ size_t ladder_scratch_bytes(int kernel, uint64_t n, int max_threads, int max_blo
 
 int ladder_reduce(int kernel, const void* in, uint64_t n, DType t, Op op, DType acc, void* out, void* scratch,
                   int max_threads, int max_blocks, hipStream_t s) {
+  return ladder_reduce_passes(kernel, in, n, t, op, acc, out, scratch, max_threads, max_blocks, 1, false, s).first_grid;
+}
+
+LadderPasses ladder_reduce_passes(int kernel, const void* in, uint64_t n, DType t, Op op, DType acc, void* out,
+                                  void* scratch, int max_threads, int max_blocks, uint64_t cpu_thresh, bool cpu_final,
+                                  hipStream_t s) {
   MIREDUCE_REQUIRE(kernel >= 0 && kernel <= 6, "ladder kernel must be 0..6");
   MIREDUCE_REQUIRE(acc_supported(t, op, acc), "unsupported (dtype, op, accumulator) combination");
   MIREDUCE_REQUIRE(!op_is_fused(op), "ladder kernels 0..6 implement the reference's SUM/MIN/MAX");
   MIREDUCE_REQUIRE(!dtype_is_half(t), "ladder kernels 0..6 cover the reference's element types (int, float, double, "
                                       "int64); bf16/half use the streaming kernel (7/8)");
   using namespace ladder;
-#define MIREDUCE_LADDER_CASE(OPT, T, A) return run<OPT, T, A>(kernel, in, n, out, scratch, max_threads, max_blocks, s)
+#define MIREDUCE_LADDER_CASE(OPT, T, A) \
+  return run<OPT, T, A>(kernel, in, n, out, scratch, max_threads, max_blocks, cpu_thresh, cpu_final, s)
   switch (op) {
     case Op::Sum:
       switch (t) {

@@ -718,6 +718,30 @@ LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, 
   return p;
 }
 
+ReducePasses reduce_passes(const void* in, size_t n, DType t, Op op, DType acc, void* scratch, int max_grid,
+                           int num_cus, uint64_t cpu_thresh, bool cpu_final, hipStream_t stream,
+                           const ReduceConfig& cfg) {
+  ReducePasses r;
+  char* a = static_cast<char*>(scratch);
+  char* b = a + static_cast<size_t>(max_grid) * 8;
+  r.plan = reduce_partials(in, n, t, op, acc, a, max_grid, num_cus, stream, cfg);
+  r.passes = 1;
+  uint64_t left = static_cast<uint64_t>(r.plan.grid);
+  // Later passes fold already-transformed partials: SUMSQ folds like SUM, AMAX like MAX.
+  const Op fold = op == Op::SumSq ? Op::Sum : (op == Op::AbsMax ? Op::Max : op);
+  ReduceConfig c2 = cfg;
+  c2.max_blocks = 0;  // the partial passes use the planner's own grid
+  while (!cpu_final && left > std::max<uint64_t>(cpu_thresh, 1)) {
+    const LaunchPlan p = reduce_partials(a, left, acc, fold, acc, b, max_grid, num_cus, stream, c2);
+    left = static_cast<uint64_t>(p.grid);
+    ++r.passes;
+    std::swap(a, b);
+  }
+  r.left = left;
+  r.partials = a;
+  return r;
+}
+
 void reduce_finalize(const void* partials, size_t count, DType acc, Op op, void* out,
                      hipStream_t stream) {
   switch (op) {  // partials are already transformed: SUMSQ folds like SUM, AMAX like MAX

@@ -205,4 +205,51 @@ int64_t acc_as_int64(const void* p, DType acc) {
   return 0;
 }
 
+bool analytic_iotamod(uint64_t n, uint64_t offset, DType t, Op op, DType acc, void* out) {
+  if (dtype_is_half(t)) return false;
+  // Σ and Σ² over one index range [a, b) of the 1024-periodic pattern, as exact integers
+  // (n < 2^64 elements: Σ x <= 1023 n and Σ x² <= 1023² n fit in unsigned __int128).
+  using U = unsigned __int128;
+  auto prefix = [](uint64_t m, int pw) -> U {  // Σ_{k<m} (k mod 1024)^pw
+    const uint64_t c = m / 1024, r = m % 1024;
+    U full = 0, part = 0;
+    for (uint64_t k = 0; k < 1024; ++k) {
+      const U v = pw == 1 ? U(k) : U(k) * k;
+      full += v;
+      if (k < r) part += v;
+    }
+    return full * c + part;
+  };
+  const U s1 = prefix(offset + n, 1) - prefix(offset, 1);
+  const U s2 = prefix(offset + n, 2) - prefix(offset, 2);
+  uint64_t mn = 1023, mx = 0;
+  if (n >= 1024) {
+    mn = 0;
+    mx = 1023;
+  } else {
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint64_t v = (offset + i) & 1023u;
+      mn = std::min(mn, v);
+      mx = std::max(mx, v);
+    }
+  }
+  long double v = 0;
+  uint64_t iv = 0;
+  switch (op) {
+    case Op::Sum: v = static_cast<long double>(s1); iv = static_cast<uint64_t>(s1); break;
+    case Op::SumSq: v = static_cast<long double>(s2); iv = static_cast<uint64_t>(s2); break;
+    case Op::Min: v = mn; iv = mn; break;
+    case Op::Max:
+    case Op::AbsMax: v = mx; iv = mx; break;
+  }
+  switch (acc) {
+    case DType::Int32: { const int32_t x = static_cast<int32_t>(static_cast<uint32_t>(iv)); std::memcpy(out, &x, 4); break; }
+    case DType::Int64: { const int64_t x = static_cast<int64_t>(iv); std::memcpy(out, &x, 8); break; }
+    case DType::Float32: { const float x = static_cast<float>(v); std::memcpy(out, &x, 4); break; }
+    case DType::Float64: { const double x = static_cast<double>(v); std::memcpy(out, &x, 8); break; }
+    default: return false;
+  }
+  return true;
+}
+
 }  // namespace mireduce

@@ -47,6 +47,67 @@ def test_reduction_app_paths(tmp_path, flags):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+# ---- C6 parity: the reference's timed multi-pass loop (reduction.cpp:319-374). n = 2^24 doubles
+# (the reference default): kernel 6 makes 64 partials (maxblocks 64); kernels 7/8 make their
+# persistent grid of partials. (kernel, cputhresh|cpufinal) -> (passes, partials folded on host).
+C6_CASES = [
+    (6, "--cpufinal", 1, 64), (6, "--cputhresh=1", 2, 0), (6, "--cputhresh=2", 2, 0),
+    (6, "--cputhresh=33", 2, 0), (6, "--cputhresh=1000", 1, 64),
+    (7, "--cputhresh=1", 1, 0), (8, "--cputhresh=1", 2, 0),
+    (7, "--cputhresh=2", 2, 0), (7, "--cputhresh=33", 2, 0), (8, "--cputhresh=1000", 1, "grid"),
+    (7, "--cpufinal", 1, "grid"), (2, "--cputhresh=1000", 2, 256), (0, "--cputhresh=33", None, None),
+]
+
+
+@pytest.mark.parametrize("kernel,flag,passes,folded", C6_CASES, ids=lambda v: str(v))
+@pytest.mark.parametrize("method", ["SUM", "MIN"])
+def test_reduction_multipass_cputhresh(tmp_path, kernel, flag, passes, folded, method):
+    js = tmp_path / "c6.json"
+    r = reduction(tmp_path, f"--method={method}", "--type=double", f"--kernel={kernel}", flag,
+                  "--iterations=3", f"--json={js}")
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(js.read_text().splitlines()[-1])
+    assert d["verified"] is True
+    if passes is not None:
+        assert d["passes"] == passes, d
+    if folded == "grid":
+        assert d["host_folded"] == d["grid"] > 1, d
+    elif folded is not None:
+        assert d["host_folded"] == folded, d
+    if kernel == 0:  # kernel 0: 2^24 / 256 partials, relaunched until <= 33 remain
+        assert d["passes"] >= 2 and d["host_folded"] <= 33
+
+
+@pytest.mark.parametrize("kernel,threads", [(6, 32), (6, 1), (0, 32), (4, 16), (5, 8), (3, 128), (7, 128)])
+def test_reduction_threads_reference_range(tmp_path, kernel, threads):
+    # the reference accepts any power of two up to 512 (reduction.cpp:272-291)
+    r = reduction(tmp_path, "--method=SUM", "--type=int", f"--kernel={kernel}", f"--threads={threads}",
+                  "--n=1000003", "--iterations=2")
+    assert r.returncode == 0, r.stdout + r.stderr
+    if kernel == 7:
+        assert "using 256" in r.stderr
+
+
+@pytest.mark.parametrize("type_,method", [("int64", "SUM"), ("double", "MAX"), ("int", "MIN")])
+def test_reduction_huge_device_fill_closed_form_oracle(tmp_path, type_, method):
+    # > 2^30 elements, device fill, no host copy: the closed-form iotamod result is the oracle
+    js = tmp_path / "huge.json"
+    r = reduction(tmp_path, f"--method={method}", f"--type={type_}", "--n=3000000000", "--fill=device",
+                  "--pattern=iotamod", "--iterations=2", f"--json={js}")
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(js.read_text().splitlines()[-1])
+    assert d["verified"] is True and d["oracle"] == "closed-form iotamod", d
+
+
+def test_reduction_huge_device_fill_ladder_oracle(tmp_path):
+    js = tmp_path / "huge.json"
+    r = reduction(tmp_path, "--method=SUM", "--type=double", "--n=1200000000", "--fill=device", "--pattern=uniform",
+                  "--iterations=2", f"--json={js}")
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(js.read_text().splitlines()[-1])
+    assert d["verified"] is True and d["oracle"] == "ladder kernel 6", d
+
+
 @pytest.mark.parametrize("method,type_,pattern", [("MAX", "double", "uniform"), ("MIN", "int", "smallint"),
                                                     ("MAX", "bf16", "uniform"), ("MIN", "int64", "fullrange")])
 def test_reduction_app_arg(tmp_path, method, type_, pattern):

@@ -226,6 +226,14 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   }
 
   // ---- single-pass finalisation (cdna_hip_programming.md §6 Guideline 16, sc1 form) ----
+  // Ordering rests on the gfx950 code hipcc emits for these relaxed agent-scope atomics (the full
+  // acq_rel form would add an L2 write-back per arrival). Generated for <SumOp,double,512,16,nt>
+  // and pinned by tests/test_isa_ordering.py:
+  //   global_store_dwordx2 v4, v[2:3], s[30:31] sc1     ; partial, write-through past L2
+  //   s_waitcnt vmcnt(0)                                ; ... acknowledged before
+  //   global_atomic_add v6, v4, v6, s[34:35] sc0        ; the (returning) ticket
+  //   s_barrier                                         ; is_last broadcast
+  //   global_load_dwordx2 v[8:9], v[8:9], off sc1       ; last arriver reads partials past L1
   const unsigned G = static_cast<unsigned>(a.groups);
   const unsigned g = blockIdx.x % G;  // group label only; correctness is placement-independent
   if (threadIdx.x == 0) {

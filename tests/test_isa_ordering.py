@@ -1,0 +1,75 @@
+"""Pin the memory-ordering instruction sequences the single-pass / cross-rank / direct kernels rely
+on. The kernels publish with relaxed atomics plus an explicit wait instead of a
+full agent-scope release (which would write back the whole L2 on every arrival); that is correct
+for the gfx950 ISA the compiler emits today, and these tests fail if a compiler change stops
+emitting it. They read the gfx950 code object inside the built objects (CPU only: llvm-objdump)."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from helpers import ROOT, ensure_built
+
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+pytestmark = pytest.mark.skipif(not os.path.exists(OBJDUMP), reason="llvm-objdump not available")
+
+STREAM_F64 = "_ZN8mireduce4kern13reduce_streamINS_5SumOpEddLi512ELi16ELb1ELb0EEEvNS0_4ArgsE"
+DIRECT_F64_W8 = "_ZN8mireduce4kern13direct_kernelINS_5SumOpEdLi8EEEvPKNS_10DirectDescEmi"
+
+
+def _disasm(tmp_path, obj: str, symbol: str) -> list:
+    ensure_built()
+    src = os.path.join(ROOT, "build", "obj", "kernels", obj)
+    local = tmp_path / obj
+    shutil.copy(src, local)
+    subprocess.run([OBJDUMP, "--offloading", str(local)], check=True, capture_output=True, cwd=tmp_path)
+    dev = [p for p in os.listdir(tmp_path) if p.startswith(obj) and p.endswith("gfx950")]
+    assert dev, "no gfx950 code object in " + obj
+    out = subprocess.run([OBJDUMP, "-d", f"--disassemble-symbols={symbol}", str(tmp_path / dev[0])], check=True,
+                         capture_output=True, text=True).stdout
+    ins = [ln.split("//")[0].strip() for ln in out.splitlines() if ln.startswith("\t")]
+    assert len(ins) > 100, f"{symbol} not found in {obj}"
+    return ins
+
+
+def _first(ins, pattern, start=0):
+    rx = re.compile(pattern)
+    for i in range(start, len(ins)):
+        if rx.search(ins[i]):
+            return i
+    return None
+
+
+def test_single_pass_publish_then_ticket_then_consume(tmp_path):
+    ins = _disasm(tmp_path, "reduce.o", STREAM_F64)
+    # producer: partial stored write-through (sc1), drained, THEN the ticket (returning atomic)
+    st = _first(ins, r"^global_store_dwordx2 .* sc1$")
+    assert st is not None, "partial publish is no longer a sc1 (write-through) store"
+    wait = _first(ins, r"^s_waitcnt vmcnt\(0\)", st)
+    atom = _first(ins, r"^global_atomic_add .* sc0", st)
+    assert wait is not None and atom is not None and wait < atom, "the publish is not drained before the ticket"
+    # consumer: after the workgroup barrier that broadcasts is_last, partials are read with sc1
+    bar = _first(ins, r"^s_barrier", atom)
+    ld = _first(ins, r"^global_load_dwordx2 .* sc1$", bar)
+    assert bar is not None and ld is not None, "the last arriver does not read partials L1-bypassing (sc1)"
+
+
+def test_xrank_exchange_is_system_scope(tmp_path):
+    ins = _disasm(tmp_path, "reduce.o", STREAM_F64)
+    # fused cross-rank finish: mailbox words stored and polled at system scope (sc0 sc1), bounded
+    st = _first(ins, r"^flat_store_dwordx2 .* sc0 sc1$")
+    ld = _first(ins, r"^flat_load_dwordx2 .* sc0 sc1$", st or 0)
+    assert st is not None and ld is not None and st < ld
+    assert _first(ins, r"^s_sleep", ld) is not None
+    assert _first(ins, r"^s_memrealtime", st) is not None, "the poll is no longer time-bounded"
+
+
+def test_direct_barrier_release_and_acquire(tmp_path):
+    ins = _disasm(tmp_path, "direct.o", DIRECT_F64_W8)
+    wb = _first(ins, r"^buffer_wbl2 sc0 sc1")  # system-scope release before raising a flag
+    flag = _first(ins, r"^flat_store_dword .* sc0 sc1$", wb or 0)
+    poll = _first(ins, r"^flat_load_dword .* sc0 sc1$", flag or 0)
+    inv = _first(ins, r"^buffer_inv sc0 sc1", poll or 0)  # system-scope acquire after the wait
+    assert None not in (wb, flag, poll, inv) and wb < flag < poll < inv

@@ -32,7 +32,8 @@ class BoundReduceMany {
   BoundReduceMany(const BoundReduceMany&) = delete;
   BoundReduceMany& operator=(const BoundReduceMany&) = delete;
 
-  void launch(hipStream_t stream) const;
+  // `out` (optional) redirects this launch's results to another device array of ptrs.size() values.
+  void launch(hipStream_t stream, void* out = nullptr) const;
   size_t tensors() const { return tensors_; }
   size_t segments() const { return segments_; }
   int grid() const { return grid_; }

@@ -278,13 +278,13 @@ BoundReduceMany::~BoundReduceMany() {
   (void)hipFree(tickets_);
 }
 
-void BoundReduceMany::launch(hipStream_t stream) const {
+void BoundReduceMany::launch(hipStream_t stream, void* out) const {
   const size_t seg_bytes = segments_ * sizeof(kern::Seg);
   kern::ManyArgs a{};
   a.segs = static_cast<const kern::Seg*>(table_);
   a.info = reinterpret_cast<const kern::TensorInfo*>(static_cast<const char*>(table_) + (seg_bytes + 255) / 256 * 256);
   a.nseg = static_cast<uint32_t>(segments_);
-  a.out = out_;
+  a.out = out ? out : out_;
   a.partials = partials_;
   a.tickets = tickets_;
   many_lookup(op_, t_, acc_).fn(a, grid_, stream);

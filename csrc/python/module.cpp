@@ -407,8 +407,8 @@ PYBIND11_MODULE(_C, m) {
            }),
            py::arg("ptrs"), py::arg("counts"), py::arg("dtype"), py::arg("op"), py::arg("acc"), py::arg("out_ptr"),
            py::arg("device"), py::arg("num_cus"), py::arg("stream") = 0)
-      .def("launch", [](const BoundReduceMany& b, uintptr_t stream) { b.launch(as_stream(stream)); },
-           py::arg("stream"))
+      .def("launch", [](const BoundReduceMany& b, uintptr_t stream, uintptr_t out) { b.launch(as_stream(stream), as_ptr<void>(out)); },
+           py::arg("stream"), py::arg("out_ptr") = 0)
       .def_property_readonly("tensors", &BoundReduceMany::tensors)
       .def_property_readonly("segments", &BoundReduceMany::segments)
       .def_property_readonly("grid", &BoundReduceMany::grid);

@@ -194,6 +194,12 @@ def _default_reducer(device: torch.device) -> Reducer:
     with _lock:
         r = _reducers.get(key)
         if r is None:
+            if torch.cuda.is_current_stream_capturing():
+                # A new Reducer allocates and zeroes its workspace synchronously, which would
+                # invalidate the capture: make it before capturing.
+                raise RuntimeError("reduce(): first call on this stream inside a hipGraph capture; call reduce() "
+                                   "once on the capture stream before capturing, or capture a Reducer / "
+                                   "Reducer.bind() launch created beforehand")
             r = Reducer(device)
             _reducers[key] = r
         return r

@@ -11,6 +11,7 @@ the per-step shape of e.g. gradient-norm clipping over a model's parameter shard
 from __future__ import annotations
 
 import math
+from collections import OrderedDict
 from typing import Optional, Sequence
 
 import torch
@@ -58,16 +59,47 @@ class ReduceMany:
         return self.out
 
 
+_bindings: "OrderedDict[tuple, ReduceMany]" = OrderedDict()
+_MAX_BINDINGS = 32
+
+
+def _binding(tensors: Sequence[torch.Tensor], op: str, acc_dtype) -> ReduceMany:
+    """A cached :class:`ReduceMany` for this exact list (pointers, sizes, dtype, op, stream): repeated
+    calls on the same parameters (a per-step grad norm) reuse its device table — no allocation,
+    upload or synchronisation per call. Evicted bindings are freed after their stream drains."""
+    dev = tensors[0].device
+    stream = torch.cuda.current_stream(dev)
+    key = (dev.index, stream.cuda_stream, tensors[0].dtype, op, acc_dtype,
+           tuple(t.data_ptr() for t in tensors), tuple(t.numel() for t in tensors))
+    rm = _bindings.get(key)
+    if rm is not None:
+        _bindings.move_to_end(key)
+        return rm
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("reduce_many: first call for this tensor list inside a graph capture; call it once "
+                           "before capturing (or capture a ReduceMany object built beforehand)")
+    rm = ReduceMany(list(tensors), op, acc_dtype)
+    _bindings[key] = rm
+    while len(_bindings) > _MAX_BINDINGS:
+        _, old = _bindings.popitem(last=False)
+        stream.synchronize()  # launches of the evicted binding may still be in flight
+        del old
+    return rm
+
+
 def reduce_many(tensors: Sequence[torch.Tensor], op: str = "sum", acc_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
     """Per-tensor reduction of a list in one launch (device tensors); host lists fall back to the
-    native host reducer per tensor."""
+    native host reducer per tensor. Returns a fresh tensor each call (the binding is cached)."""
     if tensors and tensors[0].device.type != "cuda":
         from .reduce import reduce
         acc = acc_dtype or default_acc_dtype(tensors[0].dtype, op)
         return torch.cat([reduce(t.reshape(-1), op, acc) for t in tensors])
-    rm = ReduceMany([t.contiguous() for t in tensors], op, acc_dtype)
-    out = rm()
-    torch.cuda.current_stream(rm.device).synchronize()  # the binding (and its table) dies here
+    tensors = [t.contiguous() for t in tensors]
+    if any(not t.is_contiguous() for t in tensors):  # pragma: no cover
+        raise ValueError("reduce_many needs contiguous tensors")
+    rm = _binding(tensors, op, acc_dtype)
+    out = torch.empty_like(rm.out)
+    rm._b.launch(torch.cuda.current_stream(rm.device).cuda_stream, out.data_ptr())
     return out
 
 

@@ -102,6 +102,38 @@ def test_bound_relaunch_and_graph_capture():
 
 
 @pytest.mark.gpu
+def test_reduce_many_caches_the_binding_and_returns_fresh_tensors():
+    # repeated calls on the same list reuse one binding (no per-call allocation,
+    # upload or sync) and every call returns its own result tensor.
+    from cuda_mpi_reductions_amd.ops import reduce_many as rmod
+    import cuda_mpi_reductions_amd.ops.reduce_many as m
+    ts = _mixed_list(torch.float32, seed=3)
+    m._bindings.clear()
+    a = rmod(ts, "sum")
+    b = rmod(ts, "sum")
+    assert len(m._bindings) == 1 and a.data_ptr() != b.data_ptr()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    ref = torch.stack([t.double().sum() for t in ts])
+    assert torch.allclose(a, ref, rtol=1e-9, atol=1e-9)
+    ts[0].add_(1.0)  # same storage, new values: the cached binding reads them
+    c = rmod(ts, "sum")
+    assert abs(c[0].item() - (a[0].item() + ts[0].numel())) <= 1e-6 * max(1.0, abs(c[0].item()))
+
+
+@pytest.mark.gpu
+def test_reduce_inside_capture_without_reducer_raises_clearly():
+    from cuda_mpi_reductions_amd.ops import reduce
+    x = torch.ones(1000, dtype=torch.float64, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(RuntimeError, match="inside a hipGraph capture"):
+        with torch.cuda.graph(g):
+            reduce(x)
+    torch.cuda.synchronize()
+    assert reduce(x).item() == 1000.0  # eager use afterwards still works
+
+
+@pytest.mark.gpu
 def test_norm_many_matches_torch():
     ts = _mixed_list(torch.float32, seed=5)
     total, per = norm_many(ts)

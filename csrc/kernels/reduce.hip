@@ -225,6 +225,16 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     return;
   }
 
+  // ---- one workgroup (small n): it is the last arriver by construction — no partial publish,
+  //      no tickets, no second load round.
+  if (gridDim.x == 1) {
+    if (threadIdx.x < 64) {
+      if (a.xrank) v = xrank_finish<OpT, AccT>(a.xrank, v);
+      if (threadIdx.x == 0) *static_cast<AccT*>(a.out) = v;
+    }
+    return;
+  }
+
   // ---- single-pass finalisation (cdna_hip_programming.md §6 Guideline 16, sc1 form) ----
   // Ordering rests on the gfx950 code hipcc emits for these relaxed agent-scope atomics (the full
   // acq_rel form would add an L2 write-back per arrival). Generated for <SumOp,double,512,16,nt>

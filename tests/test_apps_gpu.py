@@ -243,7 +243,8 @@ def test_bench_graph_capture_failure_falls_back_on_all_ranks(tmp_path, monkeypat
     # and fall back to eager issue (never some ranks replaying graphs and others not).
     monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
     r = torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "6",
-                     "--warmup", "2", "--elements", "20000003", "--launch", "graph"], cwd=tmp_path, timeout=600)
+                     "--warmup", "2", "--elements", "20000003", "--launch", "graph", "--collective", "rccl"],
+                 cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["verified"] is True

@@ -197,3 +197,15 @@ def test_bench_vector_extras_in_headline(tmp_path):
     ex = d["reduce_c_vector"]
     for k in ("reduce_rccl", "reduce_direct", "allreduce_rccl", "allreduce_direct"):
         assert ex[k].get("verified") is True and ex[k]["gibps"] > 0, (k, ex[k])
+
+
+def test_bench_fused_corrupt_rank_fails_verification(tmp_path, monkeypatch):
+    # fault injection through the fused finish: rank 1's result is perturbed; the AND over ranks
+    # of the per-slot verification must fail the run.
+    monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    r = torchrun(2, [BENCH, "--gpus", "2", "--backend", "gloo", "--collective", "fused", "--steps", "6",
+                     "--warmup", "2", "--elements", "20000003", "--inject-fault", "corrupt@1:3"], cwd=tmp_path,
+                 timeout=600)
+    assert r.returncode != 0
+    d = _json(r)
+    assert d["verified"] is False

@@ -234,7 +234,7 @@ def _vector_extras(ctx, steps: int = 5) -> dict:
     return out
 
 
-def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int) -> dict:
+def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph: bool = True) -> dict:
     """Time K steps (after ``warmup`` eager steps); returns elapsed (MAX over ranks), the launch
     mode and how many slots the timed steps wrote (graph replays rewrite the first chunk)."""
     C = native()
@@ -262,7 +262,7 @@ def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int) -> dict:
     launch, sg = "eager", None
     capturable = dev.type == "cuda" and not args.trace and not fault.enabled and \
         (not wl.issues_collective or ctx.backend == "nccl")
-    if (args.launch == "graph" and not fault.enabled) or (args.launch == "auto" and capturable):
+    if allow_graph and ((args.launch == "graph" and not fault.enabled) or (args.launch == "auto" and capturable)):
         # Capture the K timed steps as graph replays of --graph-chunk-step chunks (all ranks agree
         # on success or all fall back to eager issue); one untimed replay uploads the graphs.
         W = warmup
@@ -388,7 +388,9 @@ def main(argv=None) -> int:
         # combine) before the next one starts (reduction.cpp:319-374 times each reduction to
         # completion). Reported next to the pipelined headline.
         slots2 = wl.new_slots(min(W, 2) + K)
-        m2 = _measure(wl, slots2, ctx, args, fault, serial=True, warmup=min(W, 2))
+        # a capture that already failed (e.g. gloo collectives on GPU tensors) is not retried
+        m2 = _measure(wl, slots2, ctx, args, fault, serial=True, warmup=min(W, 2),
+                      allow_graph=not m1["launch"].startswith("eager (graph capture failed"))
 
     verified = None
     err = wl.check()

@@ -218,9 +218,12 @@ def _vector_extras(ctx, steps: int = 5) -> dict:
     from cuda_mpi_reductions_amd.models import CONFIGS as _C, VectorReduction
     out = {"units": "GiB/s (2^30 B of total data per collective, reduce.c:93)", "dtype": "DOUBLE", "op": "SUM",
            "total_bytes": 256 * 1024 * 1024 * 8}
+    # (gloo rehearsals: its GPU-tensor reduce / all_reduce is not RCCL and crashes on 1 GiB
+    # tensors, so only the direct collective runs there)
+    impls = ("rccl", "direct") if ctx.backend == "nccl" else ("direct",)
     for collective in ("reduce", "allreduce"):
         cfg = _replace(_C["xgmi_2g_double_sum_reduce"], collective=collective)
-        for impl in ("rccl", "direct"):
+        for impl in impls:
             key = f"{collective}_{impl}"
             try:
                 wl = VectorReduction(cfg, ctx, impl=impl, direct_timeout_s=5.0).setup()

@@ -105,8 +105,9 @@ def test_bound_relaunch_and_graph_capture():
 def test_reduce_many_caches_the_binding_and_returns_fresh_tensors():
     # repeated calls on the same list reuse one binding (no per-call allocation,
     # upload or sync) and every call returns its own result tensor.
+    import importlib
     from cuda_mpi_reductions_amd.ops import reduce_many as rmod
-    import cuda_mpi_reductions_amd.ops.reduce_many as m
+    m = importlib.import_module("cuda_mpi_reductions_amd.ops.reduce_many")  # (the package re-exports the function)
     ts = _mixed_list(torch.float32, seed=3)
     m._bindings.clear()
     a = rmod(ts, "sum")

@@ -73,3 +73,24 @@ def test_direct_barrier_release_and_acquire(tmp_path):
     poll = _first(ins, r"^flat_load_dword .* sc0 sc1$", flag or 0)
     inv = _first(ins, r"^buffer_inv sc0 sc1", poll or 0)  # system-scope acquire after the wait
     assert None not in (wb, flag, poll, inv) and wb < flag < poll < inv
+
+
+def _vgpr_count(tmp_path, obj: str, symbol: str) -> int:
+    ensure_built()
+    local = tmp_path / obj
+    shutil.copy(os.path.join(ROOT, "build", "obj", "kernels", obj), local)
+    subprocess.run([OBJDUMP, "--offloading", str(local)], check=True, capture_output=True, cwd=tmp_path)
+    dev = [p for p in os.listdir(tmp_path) if p.startswith(obj) and p.endswith("gfx950")][0]
+    readelf = os.path.join(os.path.dirname(OBJDUMP), "llvm-readelf")
+    notes = subprocess.run([readelf, "--notes", str(tmp_path / dev)], check=True, capture_output=True,
+                           text=True).stdout
+    # amdhsa.kernels metadata: ".name: <sym>" followed (within the same entry) by ".vgpr_count: N"
+    m = re.search(r"\.name:\s+" + re.escape(symbol) + r"\s*\n(?:.*\n){0,40}?\s+\.vgpr_count:\s+(\d+)", notes)
+    assert m, f"no metadata for {symbol}"
+    return int(m.group(1))
+
+
+def test_headline_kernel_keeps_its_loads_in_flight(tmp_path):
+    # 512 x 16 f64 (the >= 3 GB plan): 16 independent 16-byte loads per lane need >= 64 VGPRs.
+    # A change that made hipcc re-schedule the body onto 60 VGPRs cost 30 % (7.3 -> 5.1 TB/s).
+    assert _vgpr_count(tmp_path, "reduce.o", STREAM_F64) >= 64

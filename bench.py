@@ -65,6 +65,9 @@ def parse_args(argv=None):
                    help="cross-rank combine: rccl = 1-element RCCL all-reduce after the local kernel; "
                         "fused = the kernel's last workgroup folds all ranks' partials via IPC mailboxes; "
                         "auto = fused if its self-check passes on every rank, else rccl (GPU scalar configs)")
+    p.add_argument("--tune-steps", type=int, default=20,
+                   help="--collective auto: steps of the short per-candidate measurement that picks the headline "
+                        "combine (fused 1 lane, fused 2 lanes, RCCL pipelined)")
     p.add_argument("--vector-impl", choices=["rccl", "direct"], default="rccl",
                    help="vector (reduce.c) configs: torch.distributed collective, or the one-kernel direct "
                         "peer-read collective over xGMI (GPUs)")
@@ -237,12 +240,13 @@ def _vector_extras(ctx, steps: int = 5) -> dict:
     return out
 
 
-def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph: bool = True) -> dict:
+def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph: bool = True,
+             steps: "int | None" = None) -> dict:
     """Time K steps (after ``warmup`` eager steps); returns elapsed (MAX over ranks), the launch
     mode and how many slots the timed steps wrote (graph replays rewrite the first chunk)."""
     C = native()
     dev = ctx.device
-    K = args.steps
+    K = args.steps if steps is None else steps
 
     def run(first: int, count: int):
         works = []
@@ -381,15 +385,32 @@ def main(argv=None) -> int:
     dev = ctx.device
 
     primary_serial = args.serial
+    tuning = None
+    if args.collective == "auto" and collective == "fused" and not primary_serial and not fault.enabled:
+        # Pick the headline combine by a short measurement of each candidate (same graph-replay
+        # protocol, MAX over ranks, so every rank picks the same): the in-kernel fused finish on one
+        # stream lane or two, or the RCCL all-reduce overlapped with the next local reduce.
+        T = max(4, min(K, args.tune_steps))
+        tuning = {}
+        for coll, nl in (("fused", 1), ("fused", 2), ("rccl", 1)):
+            wl.use_collective(coll, streams=nl)
+            mt = _measure(wl, wl.new_slots(2 + T), ctx, args, fault, serial=False, warmup=2, steps=T)
+            tuning[f"{coll}_{nl}lane"] = round(wl.bytes_total * T / mt["elapsed"] / 1e9, 3)
+        best = max(tuning, key=tuning.get)
+        collective, nl = best.split("_")[0], int(best.split("_")[1][0])
+        wl.use_collective(collective, streams=nl)
     slots = wl.new_slots(W + K)
     m1 = _measure(wl, slots, ctx, args, fault, serial=primary_serial, warmup=W)
+    m1_lanes = len(wl.lanes) if wl.lanes else 1
     m2 = None
     if not primary_serial and not wl.issues_collective and len(wl.lanes) <= 1:
         m2 = m1  # one kernel per step (fused finish): the pipelined run IS the serial run
     elif not primary_serial and not args.no_serial_measure:
         # The honest per-reduction number: every step completes (local reduce AND cross-rank
         # combine) before the next one starts (reduction.cpp:319-374 times each reduction to
-        # completion). Reported next to the pipelined headline.
+        # completion), on one stream lane. Reported next to the pipelined headline.
+        if len(wl.lanes) > 1:
+            wl.use_collective(wl.collective, streams=1)
         slots2 = wl.new_slots(min(W, 2) + K)
         # a capture that already failed (e.g. gloo collectives on GPU tensors) is not retried
         m2 = _measure(wl, slots2, ctx, args, fault, serial=True, warmup=min(W, 2),
@@ -418,7 +439,7 @@ def main(argv=None) -> int:
     elapsed = m1["elapsed"]
     gbps = bytes_step * K / elapsed / 1e9
     ms = elapsed / K * 1e3
-    lanes = len(wl.lanes) if wl.lanes else 1
+    lanes = m1_lanes
     if ctx.is_root:
         if wl.issues_collective:
             combine = "RCCL all-reduce of the 1-element partial (torch.distributed nccl)" \
@@ -451,6 +472,7 @@ def main(argv=None) -> int:
                 "bytes_per_step": bytes_step,
                 "op": cfg.op.upper(),
                 "collective": collective + (f" (auto; fused unavailable: {collective_note})" if collective_note else
+                                            " (auto-tuned)" if tuning is not None else
                                             " (auto)" if args.collective == "auto" else ""),
                 "cross_rank_combine": combine,
                 "overlap": "serial (each step completes before the next)" if primary_serial else
@@ -467,6 +489,9 @@ def main(argv=None) -> int:
             "verified": verified,
             "native_ext": os.path.basename(native_path()),
         }
+        if tuning is not None:
+            line["collective_tuning"] = {"steps": max(4, min(K, args.tune_steps)), "gbps": tuning,
+                                         "chosen": f"{collective}_{lanes}lane"}
         if m2 is not None:
             line["serial_gbps"] = round(bytes_step * K / m2["elapsed"] / 1e9, 3)
             line["serial_ms_per_step"] = round(m2["elapsed"] / K * 1e3, 5)

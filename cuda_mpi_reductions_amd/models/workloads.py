@@ -210,27 +210,39 @@ class ScalarReduction:
             raise RuntimeError("the fused cross-rank finish needs GPUs")
         return self
 
-    def use_collective(self, collective: str) -> None:
-        """Re-bind every lane for another cross-rank combine (e.g. fall back from ``fused`` to
-        ``rccl``), keeping the data. Collective when switching to ``fused``."""
+    def use_collective(self, collective: str, streams: Optional[int] = None) -> None:
+        """Re-bind for another cross-rank combine (e.g. fall back from ``fused`` to ``rccl``) and/or
+        another number of stream lanes, keeping the data. Collective when the result is ``fused``
+        (every rank must call it with the same arguments)."""
         if collective not in COLLECTIVES:
             raise ValueError(f"collective must be one of {COLLECTIVES}")
         if self.ctx.device.type != "cuda":
             self.collective = collective
             return
+        dev = self.ctx.device
+        torch.cuda.synchronize(dev)
+        n = self.n_streams if streams is None else max(1, int(streams))
         if collective == "fused":
             from ..parallel.xrank import open_channel
-        lanes, self.channels = [], []
-        for stream, reducer, _, _ in self.lanes:
-            ch = open_channel(self.ctx.device, timeout_s=self.xrank_timeout_s) if collective == "fused" else None
+        old = self.lanes
+        lanes, channels = [], []
+        for k in range(n):
+            if n == 1:
+                stream = torch.cuda.current_stream(dev)
+            else:
+                stream = old[k][0] if len(old) > 1 and k < len(old) else torch.cuda.Stream(dev)
+            reducer = old[k][1] if k < len(old) else Reducer(dev, config=self.kernel)
+            ch = open_channel(dev, timeout_s=self.xrank_timeout_s) if collective == "fused" else None
             bound = reducer.bind(self.x, self.cfg.op, self.acc, out=self._bound_out, xrank=ch)
             lanes.append((stream, reducer, bound, ch))
             if ch is not None:
-                self.channels.append(ch)
-        self.lanes = lanes
-        self.bound = lanes[0][2]
+                channels.append(ch)
+        self.lanes, self.channels = lanes, channels
+        self.n_streams = n
+        self._next = 0
+        self.reducer, self.bound = lanes[0][1], lanes[0][2]
         self.collective = collective
-        torch.cuda.synchronize(self.ctx.device)
+        torch.cuda.synchronize(dev)
 
     @property
     def bytes_total(self) -> int:

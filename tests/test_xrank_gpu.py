@@ -147,13 +147,17 @@ def test_bench_auto_falls_back_to_rccl_on_every_rank(tmp_path, monkeypatch):
     assert d["config"]["collective"].startswith("rccl (auto; fused unavailable"), d["config"]["collective"]
 
 
-def test_bench_auto_picks_fused(tmp_path):
+def test_bench_auto_tunes_the_combine(tmp_path):
     r = run([sys.executable, BENCH, "--steps", "6", "--warmup", "2", "--elements", "50000017"], cwd=tmp_path,
             timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
-    assert d["verified"] is True and d["config"]["collective"] == "fused (auto)"
-    assert d["serial_gbps"] == d["value"]
+    assert d["verified"] is True and d["config"]["collective"].endswith("(auto-tuned)")
+    tun = d["collective_tuning"]
+    assert set(tun["gbps"]) == {"fused_1lane", "fused_2lane", "rccl_1lane"} and all(v > 0 for v in tun["gbps"].values())
+    assert tun["chosen"] == max(tun["gbps"], key=tun["gbps"].get)
+    assert d["config"]["collective"].startswith(tun["chosen"].split("_")[0])
+    assert d["serial_gbps"] > 0 and d["serial_launch"].startswith("graph")
 
 
 # ---------------------------------------------------------------- direct collective from Python

@@ -390,12 +390,17 @@ def main(argv=None) -> int:
         # Pick the headline combine by a short measurement of each candidate (same graph-replay
         # protocol, MAX over ranks, so every rank picks the same): the in-kernel fused finish on one
         # stream lane or two, or the RCCL all-reduce overlapped with the next local reduce.
+        # Two rounds, best of each candidate: the first candidate of round 1 otherwise pays for
+        # the GPU ramping its clocks (measured: -2 % at 8 GB on an otherwise equal kernel).
         T = max(4, min(K, args.tune_steps))
         tuning = {}
-        for coll, nl in (("fused", 1), ("fused", 2), ("rccl", 1)):
-            wl.use_collective(coll, streams=nl)
-            mt = _measure(wl, wl.new_slots(2 + T), ctx, args, fault, serial=False, warmup=2, steps=T)
-            tuning[f"{coll}_{nl}lane"] = round(wl.bytes_total * T / mt["elapsed"] / 1e9, 3)
+        for _round in range(2):
+            for coll, nl in (("fused", 1), ("fused", 2), ("rccl", 1)):
+                wl.use_collective(coll, streams=nl)
+                mt = _measure(wl, wl.new_slots(2 + T), ctx, args, fault, serial=False, warmup=2, steps=T)
+                g = round(wl.bytes_total * T / mt["elapsed"] / 1e9, 3)
+                key = f"{coll}_{nl}lane"
+                tuning[key] = max(tuning.get(key, 0.0), g)
         best = max(tuning, key=tuning.get)
         collective, nl = best.split("_")[0], int(best.split("_")[1][0])
         wl.use_collective(collective, streams=nl)

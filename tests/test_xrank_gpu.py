@@ -213,3 +213,27 @@ def test_bench_fused_corrupt_rank_fails_verification(tmp_path, monkeypatch):
     assert r.returncode != 0
     d = _json(r)
     assert d["verified"] is False
+
+
+# ---------------------------------------------------------------- the N=8 shapes, rehearsed
+# Eight ranks share the one GPU of the test box: the world-8 mailbox indexing of the fused finish,
+# the W=8 instantiation of the direct kernel and bench.py's 8-rank flow (not xGMI speed).
+
+def test_bench_eight_ranks_fused_on_one_gpu(tmp_path, monkeypatch):
+    monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    r = torchrun(8, [BENCH, "--gpus", "8", "--backend", "gloo", "--collective", "fused", "--steps", "12",
+                     "--warmup", "2", "--elements", "40000003", "--graph-chunk", "6", "--no-vector-extras"],
+                 cwd=tmp_path, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r)
+    assert d["verified"] is True and d["n_gpus"] == 8 and d["config"]["parallelism"] == "dp8"
+    assert d["config"]["launch"].startswith("graph")
+
+
+def test_reduce_xgmi_direct_eight_ranks_on_one_gpu():
+    from helpers import BIN
+    r = torchrun(8, ["--no-python", os.path.join(BIN, "reduce_xgmi"), "--mode=vector", "--collective=direct",
+                     "--ints=4000037", "--doubles=2000003", "--dtypes=INT,DOUBLE", "--retries=1", "--iters=3",
+                     "--direct-grid=16", "--timeout=30", "--graph"], timeout=900)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "verification PASSED" in r.stderr

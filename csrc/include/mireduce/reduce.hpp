@@ -45,7 +45,8 @@ struct LaunchPlan {
   bool nontemporal = true;
   bool pipelined = false;
   bool single_pass = true;
-  bool flat = false;   // single-pass fan-in: flat (final arriver folds every partial) vs two-level
+  bool poll = false;   // single-pass fan-in: polled tagged slots (default, no tickets)
+  bool flat = false;   // ticketed fan-in: flat (final arriver folds every partial) vs two-level
   bool contiguous = false;  // body split: one contiguous run of tiles per workgroup vs interleaved
   uint64_t head = 0;   // scalar elements before the first 16-B aligned vector
   uint64_t nvec = 0;   // 16-byte vectors in the streaming body
@@ -68,7 +69,8 @@ class Workspace {
   void* partials() const { return partials_; }
   void* group_partials() const { return group_partials_; }
   unsigned* tickets() const { return tickets_; }
-  // Re-zero the tickets (only needed after an aborted launch).
+  uint64_t* slots() const { return slots_; }
+  // Re-zero the tickets and fan-in slots (only needed after an aborted launch).
   void reset(hipStream_t stream);
 
  private:
@@ -78,6 +80,7 @@ class Workspace {
   void* partials_ = nullptr;
   void* group_partials_ = nullptr;
   unsigned* tickets_ = nullptr;
+  uint64_t* slots_ = nullptr;  // polled fan-in: [max_grid][2] tagged words, uncached
 };
 
 constexpr int kTicketStride = 32;  // one counter per 128-byte line

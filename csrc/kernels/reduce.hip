@@ -73,7 +73,13 @@ struct Args {
   int flat;              // 1: group last-arrivers only count; the final arriver folds every partial
   int contig;            // 1: workgroup b streams one contiguous run of tiles; 0: tiles b, b+grid, ...
   const XrankDesc* xrank;  // non-null: fold the ranks' partials in-kernel before writing out (xrank.hpp)
+  uint64_t* slots;         // non-null: polled fan-in (no tickets), [gridDim.x][2] flag-tagged words
 };
+
+// Polled fan-in: a published partial is two 8-byte words (tag << 32 | 32 data bits); a cleared
+// slot is 0. The finisher clears every slot it consumed, so each launch starts from zeros.
+constexpr uint64_t kSlotTag = 0xA5C3E1F7ull << 32;
+constexpr int kPollSlots = 4;  // slots one finisher lane polls per round (grid <= 4 x BLOCK)
 
 template <class T>
 __device__ __forceinline__ uint64_t to_bits64(T v) {
@@ -241,7 +247,84 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     return;
   }
 
-  // ---- single-pass finalisation (cdna_hip_programming.md §6 Guideline 16, sc1 form) ----
+  // ---- polled fan-in (default): no tickets, no publish-then-drain wait. Every workgroup stores
+  // its partial as two tagged words (the data carries its own validity, as in the cross-rank
+  // mailbox) and exits; the last-indexed workgroup — with interleaved tiles one of the first to
+  // run out of work — polls all slots, folds them in slot order (deterministic), clears them and
+  // finishes. The finisher's path after the last partial lands is one store + one poll round,
+  // instead of store, drain, ticket (x2) and a load round. Slots live in uncached memory, so
+  // polls always see the other XCDs' stores.
+  if (a.slots) {
+    if (threadIdx.x == 0) {
+      const uint64_t bits = to_bits64(v);
+      uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(blockIdx.x);
+      __hip_atomic_store(sl, kSlotTag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sl + 1, kSlotTag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (blockIdx.x != gridDim.x - 1) return;
+    AccT t = OpT::template identity<AccT>();
+    // Bounded like every device-side wait here (all workgroups of this launch always publish, so
+    // the bound is never reached by a correct launch; it only keeps a misuse from hanging the GPU).
+    const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
+    constexpr uint64_t kBound = 1ull << 30;  // ~10 s of the 100 MHz wall clock
+    if (gridDim.x <= kPollSlots * BLOCK) {
+      // Each lane polls ALL its slots (<= kPollSlots) every round, so the finish costs one poll
+      // round trip after the last store lands, not one per slot.
+      uint64_t lo[kPollSlots], hi[kPollSlots];
+      unsigned pending = 0;
+#pragma unroll
+      for (int k = 0; k < kPollSlots; ++k)
+        if (threadIdx.x + k * BLOCK < gridDim.x) pending |= 1u << k;
+      while (pending) {
+#pragma unroll
+        for (int k = 0; k < kPollSlots; ++k) {
+          if (pending & (1u << k)) {
+            const uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(threadIdx.x + k * BLOCK);
+            lo[k] = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hi[k] = __hip_atomic_load(sl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < kPollSlots; ++k)
+          if ((pending & (1u << k)) && (lo[k] & ~0xffffffffull) == kSlotTag && (hi[k] & ~0xffffffffull) == kSlotTag)
+            pending &= ~(1u << k);
+        if (!pending || static_cast<uint64_t>(wall_clock64()) - t0 > kBound) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int k = 0; k < kPollSlots; ++k) {  // fold in slot order (deterministic), then clear
+        if (threadIdx.x + k * BLOCK < gridDim.x) {
+          t = OpT::apply(t, from_bits64<AccT>((lo[k] & 0xffffffffull) | (hi[k] << 32)));
+          uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(threadIdx.x + k * BLOCK);
+          __hip_atomic_store(sl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(sl + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    } else {  // very large grids (user --maxblocks / wg-per-cu): slot by slot
+      for (unsigned i = threadIdx.x; i < gridDim.x; i += BLOCK) {
+        uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(i);
+        uint64_t l, h;
+        for (;;) {
+          l = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          h = __hip_atomic_load(sl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((l & ~0xffffffffull) == kSlotTag && (h & ~0xffffffffull) == kSlotTag) break;
+          if (static_cast<uint64_t>(wall_clock64()) - t0 > kBound) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        t = OpT::apply(t, from_bits64<AccT>((l & 0xffffffffull) | (h << 32)));
+        __hip_atomic_store(sl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sl + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    t = block_reduce<OpT, AccT, BLOCK>(t, lds);
+    if (threadIdx.x < 64) {
+      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, t, xr_epoch, xr_err);
+      if (threadIdx.x == 0) *static_cast<AccT*>(a.out) = t;
+    }
+    return;
+  }
+
+  // ---- ticketed finalisation (MIREDUCE_FANIN=flat|tree; cdna_hip_programming.md §6 G16, sc1 form)
   // Ordering rests on the gfx950 code hipcc emits for these relaxed agent-scope atomics (the full
   // acq_rel form would add an L2 write-back per arrival). Generated for <SumOp,double,512,16,nt>
   // and pinned by tests/test_isa_ordering.py:
@@ -267,14 +350,17 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     // Flat fan-in: the group's last arriver only takes a ticket on the top counter; the last of
     // those folds all gridDim.x partials at once (one parallel sc1 load round instead of a
     // group fold + group-partial publish + second fold: two memory round trips shorter).
-    if (threadIdx.x == 0) {
-      __hip_atomic_store(&a.tickets[g * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned prev = __hip_atomic_fetch_add(&a.tickets[G * kTicketStride], 1u,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      is_last = (prev == G - 1);
+    // (One group — small grids — has no top counter: its last arriver is the finisher.)
+    if (G > 1) {
+      if (threadIdx.x == 0) {
+        __hip_atomic_store(&a.tickets[g * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned prev = __hip_atomic_fetch_add(&a.tickets[G * kTicketStride], 1u,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = (prev == G - 1);
+      }
+      __syncthreads();
+      if (!is_last) return;
     }
-    __syncthreads();
-    if (!is_last) return;
     AccT t = OpT::template identity<AccT>();
     for (unsigned i = threadIdx.x; i < gridDim.x; i += BLOCK) t = OpT::apply(t, load_sc1(&partials[i]));
     t = block_reduce<OpT, AccT, BLOCK>(t, lds);
@@ -282,7 +368,9 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, t, xr_epoch, xr_err);
       if (threadIdx.x == 0) {
         *static_cast<AccT*>(a.out) = t;
-        __hip_atomic_store(&a.tickets[G * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // reset: the top counter, or (one group) the group counter itself
+        __hip_atomic_store(&a.tickets[(G > 1 ? G : 0) * kTicketStride], 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     return;
@@ -518,16 +606,18 @@ Defaults tuned_defaults(size_t bytes, DType t) {
   return {256, 4, 3, 1, 0};
 }
 constexpr int kDefaultGroups = 8;
+constexpr int kOneGroupGrid = 64;
 
-// Fan-in shape of the single-pass finalisation; MIREDUCE_FANIN=flat|tree overrides (A/B runs).
-bool fanin_flat() {
+// Fan-in shape of the single-pass finalisation: 0 tree, 1 flat (ticketed), 2 poll (default);
+// MIREDUCE_FANIN=poll|flat|tree overrides (A/B runs).
+int fanin_mode() {
   static const int v = [] {
     const char* e = std::getenv("MIREDUCE_FANIN");
     if (e && std::strcmp(e, "tree") == 0) return 0;
     if (e && std::strcmp(e, "flat") == 0) return 1;
-    return 1;  // flat: 1 GB 139.8 vs 140.1 us, 8 MB 6.24 vs 6.80 us (profiles/r1_bench/fanin_ab.txt)
+    return 2;
   }();
-  return v == 1;
+  return v;
 }
 
 // Work split of the streaming body; MIREDUCE_SPLIT=stride|contig overrides (A/B runs; read per
@@ -596,6 +686,10 @@ Workspace::Workspace(int device, int max_grid) : max_grid_(max_grid) {
   const size_t tbytes = static_cast<size_t>(kMaxGroups + 1) * kTicketStride * sizeof(unsigned);
   MIREDUCE_HIP_THROW(hipMalloc(reinterpret_cast<void**>(&tickets_), tbytes));
   MIREDUCE_HIP_THROW(hipMemset(tickets_, 0, tbytes));
+  // polled fan-in slots: uncached, so the finisher's polls see every XCD's stores
+  MIREDUCE_HIP_THROW(hipExtMallocWithFlags(reinterpret_cast<void**>(&slots_), static_cast<size_t>(max_grid) * 16,
+                                           hipDeviceMallocUncached));
+  MIREDUCE_HIP_THROW(hipMemset(slots_, 0, static_cast<size_t>(max_grid) * 16));
   MIREDUCE_HIP_THROW(hipDeviceSynchronize());
   MIREDUCE_HIP_THROW(hipSetDevice(prev));
 }
@@ -604,11 +698,13 @@ Workspace::~Workspace() {
   (void)hipFree(partials_);
   (void)hipFree(group_partials_);
   (void)hipFree(tickets_);
+  (void)hipFree(slots_);
 }
 
 void Workspace::reset(hipStream_t stream) {
   const size_t tbytes = static_cast<size_t>(kMaxGroups + 1) * kTicketStride * sizeof(unsigned);
   MIREDUCE_HIP_THROW(hipMemsetAsync(tickets_, 0, tbytes, stream));
+  MIREDUCE_HIP_THROW(hipMemsetAsync(slots_, 0, static_cast<size_t>(max_grid_) * 16, stream));
 }
 
 LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cfg, int num_cus,
@@ -645,11 +741,14 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   if (want > static_cast<uint64_t>(max_grid)) want = max_grid;
   if (want < 1) want = 1;
   p.grid = static_cast<int>(want);
-  int groups = cfg.groups ? cfg.groups : kDefaultGroups;
+  // Arrival counters: one for small grids (<= kOneGroupGrid arrivals contend little, and the
+  // finisher then skips the second ticket round trip), kDefaultGroups shards above.
+  int groups = cfg.groups ? cfg.groups : (static_cast<int>(want) <= kOneGroupGrid ? 1 : kDefaultGroups);
   if (groups > kMaxGroups) groups = kMaxGroups;
   if (groups > p.grid) groups = p.grid;
   p.groups = p.single_pass ? groups : 0;
-  p.flat = p.single_pass && fanin_flat();
+  p.poll = p.single_pass && fanin_mode() == 2;
+  p.flat = p.single_pass && fanin_mode() == 1;
   p.contiguous = split_contiguous();
   return p;
 }
@@ -678,6 +777,7 @@ LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out
   a.out = out;
   a.groups = p.groups;
   a.flat = p.flat ? 1 : 0;
+  a.slots = p.poll ? ws.slots() : nullptr;
   a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
   const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0];
   fn(a, p.grid, stream);
@@ -708,6 +808,7 @@ BoundReduce::BoundReduce(const void* in, size_t n, DType t, Op op, DType acc, vo
   a.out = out;
   a.groups = p.groups;
   a.flat = p.flat ? 1 : 0;
+  a.slots = p.poll ? ws.slots() : nullptr;
   a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
   impl_ = new Impl{a, table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0],
                    p, op, acc};

@@ -46,6 +46,7 @@ py::dict plan_dict(const LaunchPlan& p) {
   d["pipelined"] = p.pipelined;
   d["single_pass"] = p.single_pass;
   d["flat"] = p.flat;
+  d["poll"] = p.poll;
   d["contiguous"] = p.contiguous;
   d["head"] = p.head;
   d["nvec"] = p.nvec;

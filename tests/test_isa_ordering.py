@@ -42,18 +42,40 @@ def _first(ins, pattern, start=0):
     return None
 
 
-def test_single_pass_publish_then_ticket_then_consume(tmp_path):
+def test_ticketed_fanin_publish_then_ticket_then_consume(tmp_path):
+    # MIREDUCE_FANIN=flat|tree: partial stored write-through (sc1), drained, THEN the returning
+    # ticket; after the barrier that broadcasts is_last, partials are read L1-bypassing (sc1).
     ins = _disasm(tmp_path, "reduce.o", STREAM_F64)
-    # producer: partial stored write-through (sc1), drained, THEN the ticket (returning atomic)
+    ok = False
+    for i, ln in enumerate(ins):
+        if not re.search(r"^global_store_dwordx2 .* sc1$", ln):
+            continue
+        atom = _first(ins, r"^global_atomic_add .* sc0", i)
+        if atom is None:
+            continue
+        wait = _first(ins, r"^s_waitcnt vmcnt\(0\)", i)
+        bar = _first(ins, r"^s_barrier", atom)
+        ld = _first(ins, r"^global_load_dwordx2 .* sc1$", bar or atom)
+        if wait is not None and wait < atom and bar is not None and ld is not None:
+            ok = True
+            break
+    assert ok, "no publish -> drain -> ticket -> barrier -> sc1-load sequence in the ticketed fan-in"
+
+
+def test_polled_fanin_tagged_slots(tmp_path):
+    # default fan-in: two tagged 8-byte words stored per workgroup (no drain, no ticket); the
+    # finisher polls both words of a slot (sc1 loads) with a bounded, sleeping loop and clears them.
+    ins = _disasm(tmp_path, "reduce.o", STREAM_F64)
     st = _first(ins, r"^global_store_dwordx2 .* sc1$")
-    assert st is not None, "partial publish is no longer a sc1 (write-through) store"
-    wait = _first(ins, r"^s_waitcnt vmcnt\(0\)", st)
-    atom = _first(ins, r"^global_atomic_add .* sc0", st)
-    assert wait is not None and atom is not None and wait < atom, "the publish is not drained before the ticket"
-    # consumer: after the workgroup barrier that broadcasts is_last, partials are read with sc1
-    bar = _first(ins, r"^s_barrier", atom)
-    ld = _first(ins, r"^global_load_dwordx2 .* sc1$", bar)
-    assert bar is not None and ld is not None, "the last arriver does not read partials L1-bypassing (sc1)"
+    assert st is not None and re.search(r"offset:8 sc1$", ins[st + 1] if st + 1 < len(ins) else "") or \
+        _first(ins, r"^global_store_dwordx2 .* offset:8 sc1$", st) is not None
+    poll = _first(ins, r"^global_load_dwordx2 .* sc1$", st)
+    assert poll is not None and re.search(r"^global_load_dwordx2 .* offset:8 sc1$", ins[poll + 1])
+    assert _first(ins, r"^s_sleep", poll) is not None and _first(ins, r"^s_memrealtime", st) is not None
+    # the ticketed path's atomic must come after the polled path has ended (separate branch)
+    end = _first(ins, r"^s_endpgm", poll)
+    atom = _first(ins, r"^global_atomic_add", st)
+    assert end is not None and (atom is None or atom > end)
 
 
 def test_xrank_exchange_is_system_scope(tmp_path):

@@ -48,6 +48,7 @@ struct LaunchPlan {
   bool poll = false;   // single-pass fan-in: polled tagged slots (default, no tickets)
   bool flat = false;   // ticketed fan-in: flat (final arriver folds every partial) vs two-level
   bool contiguous = false;  // body split: one contiguous run of tiles per workgroup vs interleaved
+  bool balanced = false;    // interleaved: leftover tiles split evenly over all workgroups
   uint64_t head = 0;   // scalar elements before the first 16-B aligned vector
   uint64_t nvec = 0;   // 16-byte vectors in the streaming body
   uint64_t tail = 0;   // scalar elements after the body

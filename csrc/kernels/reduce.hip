@@ -74,6 +74,8 @@ struct Args {
   int contig;            // 1: workgroup b streams one contiguous run of tiles; 0: tiles b, b+grid, ...
   const XrankDesc* xrank;  // non-null: fold the ranks' partials in-kernel before writing out (xrank.hpp)
   uint64_t* slots;         // non-null: polled fan-in (no tickets), [gridDim.x][2] flag-tagged words
+  int balance;             // 1 (interleaved split): whole rounds of tiles, then the leftover < grid
+                           // tiles split evenly over ALL workgroups (no one-tile tail on a few)
 };
 
 // Polled fan-in: a published partial is two 8-byte words (tag << 32 | 32 data bits); a cleared
@@ -180,8 +182,10 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   // This workgroup's full tiles: t0, t0 + step, ... < t1 (interleaved over the grid, or one
   // contiguous run of ntiles / grid tiles each).
   const uint64_t grid = gridDim.x;
+  const bool balanced = a.balance && !a.contig;
+  const uint64_t full = balanced ? ntiles / grid * grid : ntiles;  // tiles streamed in whole rounds
   const uint64_t t0 = a.contig ? blockIdx.x * ntiles / grid : blockIdx.x;
-  const uint64_t t1 = a.contig ? (blockIdx.x + 1) * ntiles / grid : ntiles;
+  const uint64_t t1 = a.contig ? (blockIdx.x + 1) * ntiles / grid : full;
   const uint64_t step = a.contig ? 1 : grid;
   if constexpr (PIPE) {
     if (t0 < t1) {
@@ -203,12 +207,40 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, v);
     }
   }
-  // Vectors past the last full tile, grid-strided.
-  for (uint64_t i = ntiles * kTile + static_cast<uint64_t>(blockIdx.x) * BLOCK + threadIdx.x;
-       i < a.nvec; i += static_cast<uint64_t>(gridDim.x) * BLOCK) {
-    const V v = vin[i];
+  if (balanced) {
+    // The leftover after the whole rounds (< grid tiles + the sub-tile remainder) as one even,
+    // contiguous piece per workgroup (< one tile each): every load issued unconditionally (an
+    // out-of-piece lane re-reads its piece's first vector and discards it), so no per-load branch
+    // serialises the wave (cdna_hip_programming.md §5 trap (c)).
+    const uint64_t l0 = full * kTile, left = a.nvec - l0;
+    const uint64_t s0 = l0 + left * blockIdx.x / grid, s1 = l0 + left * (blockIdx.x + 1) / grid;
+    for (uint64_t base = s0 + threadIdx.x; base < s1; base += kTile) {
+      V v[UNROLL];
+      bool ok[UNROLL];
 #pragma unroll
-    for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], OpT::pre(elem<T, AccT>(v, k)));
+      for (int u = 0; u < UNROLL; ++u) {
+        const uint64_t idx = base + static_cast<uint64_t>(u) * BLOCK;
+        ok[u] = idx < s1;
+        const V* p = vin + (ok[u] ? idx : base);
+        if constexpr (NT) v[u] = __builtin_nontemporal_load(p);
+        else v[u] = *p;
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        if (ok[u]) {
+#pragma unroll
+          for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(v[u], k)));
+        }
+      }
+    }
+  } else {
+    // Vectors past the last full tile, grid-strided.
+    for (uint64_t i = ntiles * kTile + static_cast<uint64_t>(blockIdx.x) * BLOCK + threadIdx.x;
+         i < a.nvec; i += static_cast<uint64_t>(gridDim.x) * BLOCK) {
+      const V v = vin[i];
+#pragma unroll
+      for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], OpT::pre(elem<T, AccT>(v, k)));
+    }
   }
   // Unaligned head and sub-vector tail (< N elements each), folded by the last workgroup.
   if (blockIdx.x == gridDim.x - 1) {
@@ -620,6 +652,14 @@ int fanin_mode() {
   return v;
 }
 
+// Balanced leftover: MIREDUCE_BALANCE=1 opts in (read per plan). Off by default: measured equal
+// within noise at 128 MiB - 4 GB for four plans (profiles/r2_small/balance_ab.txt) — the
+// bandwidth the idle workgroups free up already lets the few with an extra tile finish early.
+bool balance_leftover() {
+  const char* e = std::getenv("MIREDUCE_BALANCE");
+  return e && std::strcmp(e, "1") == 0;
+}
+
 // Work split of the streaming body; MIREDUCE_SPLIT=stride|contig overrides (A/B runs; read per
 // plan so one process can compare both).
 bool split_contiguous() {
@@ -750,6 +790,7 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   p.poll = p.single_pass && fanin_mode() == 2;
   p.flat = p.single_pass && fanin_mode() == 1;
   p.contiguous = split_contiguous();
+  p.balanced = !p.contiguous && balance_leftover();
   return p;
 }
 
@@ -761,6 +802,7 @@ static kern::Args make_args(const void* in, const LaunchPlan& p, DType t) {
   a.nvec = p.nvec;
   a.tail = p.tail;
   a.contig = p.contiguous ? 1 : 0;
+  a.balance = p.balanced ? 1 : 0;
   return a;
 }
 

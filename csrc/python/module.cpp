@@ -47,6 +47,7 @@ py::dict plan_dict(const LaunchPlan& p) {
   d["single_pass"] = p.single_pass;
   d["flat"] = p.flat;
   d["poll"] = p.poll;
+  d["balanced"] = p.balanced;
   d["contiguous"] = p.contiguous;
   d["head"] = p.head;
   d["nvec"] = p.nvec;

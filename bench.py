@@ -65,6 +65,8 @@ def parse_args(argv=None):
                    help="cross-rank combine: rccl = 1-element RCCL all-reduce after the local kernel; "
                         "fused = the kernel's last workgroup folds all ranks' partials via IPC mailboxes; "
                         "auto = fused if its self-check passes on every rank, else rccl (GPU scalar configs)")
+    p.add_argument("--xrank-timeout", type=float, default=30.0,
+                   help="fused finish: seconds a kernel waits for a peer's partial before flagging the channel")
     p.add_argument("--tune-steps", type=int, default=20,
                    help="--collective auto: steps of the short per-candidate measurement that picks the headline "
                         "combine (fused 1 lane, fused 2 lanes, RCCL pipelined)")
@@ -372,7 +374,7 @@ def main(argv=None) -> int:
     # The cross-rank combine is issued even on one rank (--local-only skips it): N=1 runs the
     # exact step the N-GPU job runs.
     wl = scalar_workload(cfg, ctx, kernel, streams=args.streams, collective="rccl" if collective == "auto" else collective,
-                         always_collective=not args.local_only).setup()
+                         always_collective=not args.local_only, xrank_timeout_s=args.xrank_timeout).setup()
     collective_note = None
     if collective == "auto":
         collective = "rccl"
@@ -396,11 +398,15 @@ def main(argv=None) -> int:
         tuning = {}
         for _round in range(2):
             for coll, nl in (("fused", 1), ("fused", 2), ("rccl", 1)):
+                key = f"{coll}_{nl}lane"
+                if tuning.get(key, 0.0) < 0:
+                    continue  # failed in round 1
                 wl.use_collective(coll, streams=nl)
                 mt = _measure(wl, wl.new_slots(2 + T), ctx, args, fault, serial=False, warmup=2, steps=T)
                 g = round(wl.bytes_total * T / mt["elapsed"] / 1e9, 3)
-                key = f"{coll}_{nl}lane"
-                tuning[key] = max(tuning.get(key, 0.0), g)
+                if coll == "fused" and wl.check() is not None:  # a timed-out exchange: never pick it
+                    g = -1.0
+                tuning[key] = g if g < 0 else max(tuning.get(key, 0.0), g)
         best = max(tuning, key=tuning.get)
         collective, nl = best.split("_")[0], int(best.split("_")[1][0])
         wl.use_collective(collective, streams=nl)

@@ -141,7 +141,7 @@ class ScalarReduction:
                  kernel: Optional[KernelConfig] = None, seed: int = 0x5EED,
                  acc_dtype: Optional[torch.dtype] = None, streams: int = 1,
                  collective: str = "rccl", always_collective: bool = False,
-                 xrank_timeout_s: float = 2.0):
+                 xrank_timeout_s: float = 10.0):
         if cfg.mode != "scalar":
             raise ValueError("ScalarReduction needs a scalar-mode config")
         if collective not in COLLECTIVES:

@@ -230,6 +230,19 @@ def test_bench_eight_ranks_fused_on_one_gpu(tmp_path, monkeypatch):
     assert d["config"]["launch"].startswith("graph")
 
 
+def test_bench_eight_ranks_auto_on_one_gpu(tmp_path, monkeypatch):
+    # the driver's default command at N=8 (auto-tuned combine), rehearsed with gloo on one GPU
+    monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    r = torchrun(8, [BENCH, "--gpus", "8", "--backend", "gloo", "--steps", "12", "--warmup", "2",
+                     "--elements", "40000003", "--tune-steps", "4"], cwd=tmp_path, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r)
+    assert d["verified"] is True and d["n_gpus"] == 8
+    assert "auto" in d["config"]["collective"] and "reduce_c_vector" in d
+    ex = d["reduce_c_vector"]
+    assert ex["reduce_direct"].get("verified") is True, ex
+
+
 def test_reduce_xgmi_direct_eight_ranks_on_one_gpu():
     from helpers import BIN
     r = torchrun(8, ["--no-python", os.path.join(BIN, "reduce_xgmi"), "--mode=vector", "--collective=direct",

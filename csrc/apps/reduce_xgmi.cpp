@@ -42,6 +42,7 @@
 #include "mireduce/report.hpp"
 #include "mireduce/timer.hpp"
 #include "mireduce/trace.hpp"
+#include "mireduce/xrank.hpp"
 
 using namespace mireduce;
 
@@ -132,6 +133,8 @@ void sync_stream(Ctx& c) {
 }
 
 bool is_direct(const Ctx& c) { return c.collective == "direct" || c.collective == "direct-reduce"; }
+// Collectives that need no RCCL communicator (and so may share one GPU between ranks in tests).
+bool needs_no_rccl(const Ctx& c) { return is_direct(c) || c.collective == "fused"; }
 
 // Time `iters` repetitions of `body` on the stream (optionally as one hipGraph replay).
 template <class F>
@@ -328,6 +331,19 @@ bool run_scalar(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>&
                 const std::vector<uint64_t>& counts) {
   Workspace ws(c.device);
   DeviceBuffer out(8), loc(8), oracle(8);
+  // --collective=fused: the kernel's finisher folds every rank's partial through IPC mailboxes
+  // (xrank.hpp) — one kernel per global reduction, no RCCL.
+  std::unique_ptr<XrankChannel> channel;
+  ReduceConfig step_cfg = c.kcfg;
+  if (c.collective == "fused") {
+    channel = std::make_unique<XrankChannel>(c.device, c.direct_timeout_s);
+    const IpcHandleBytes mine = channel->handle();
+    std::vector<IpcHandleBytes> all(c.env.world);
+    c.boot->allgather(mine.data(), all.data(), mine.size());
+    channel->connect(c.env.rank, c.env.world, all);
+    c.boot->barrier();  // every rank mapped every mailbox before the first launch
+    step_cfg.xrank = channel->device_desc();
+  }
   if (c.env.rank == c.root) std::printf("%s\n", gnuplot_header().c_str());
   bool ok = true;
   for (size_t k = 0; k < dtypes.size(); ++k) {
@@ -347,18 +363,20 @@ bool run_scalar(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>&
       const DType acc = default_acc(t, o);
       auto body = [&] {
         TraceRange tr("reduce_xgmi.scalar_step");
-        reduce(x.get(), count, t, o, acc, out.get(), ws, c.stream, c.kcfg);
-        c.comm->allreduce(out.get(), out.get(), 1, acc, o, c.stream);
+        reduce(x.get(), count, t, o, acc, out.get(), ws, c.stream, step_cfg);
+        if (!channel) c.comm->allreduce(out.get(), out.get(), 1, acc, o, c.stream);
       };
       for (int w = 0; w < c.warmup; ++w) {
         body();
-        c.comm->synchronize(c.stream, c.timeout_s);
+        sync_stream(c);
       }
       for (int x_ = 0; x_ < c.retries; ++x_) {
         SavedElement saved;
         if (c.fault.at(c.env.rank, c.fault_step++, "scalar step") && count) saved = corrupt_any(x.get(), 0, t, o);
         const double dt = time_iters(c, body);
         restore_element(saved);
+        if (channel && channel->error())
+          throw Error("fused: a peer's partial never arrived (device-side wait timed out after --timeout)");
         Json j;
         j.set("n_total", n).set("count_per_rank", count).set("retry", x_);
         bool vok = true;
@@ -543,8 +561,9 @@ void usage() {
   std::printf(
       "reduce_xgmi — RCCL-over-xGMI reduction benchmark (one process per GPU)\n"
       "  --mode=vector|scalar        reduce.c element-wise reduce | global array -> one value\n"
-      "  --collective=reduce|allreduce|direct|direct-reduce (vector default: reduce, like MPI_Reduce;\n"
-      "               scalar: allreduce; direct*: one-shot peer reads over xGMI via IPC, no RCCL)\n"
+      "  --collective=reduce|allreduce|direct|direct-reduce|fused (vector default: reduce, like MPI_Reduce;\n"
+      "               scalar: allreduce; direct*: one-kernel peer reads over xGMI via IPC, no RCCL;\n"
+      "               fused (scalar): the reduction kernel folds every rank's partial, no RCCL)\n"
       "  --dtypes=INT,DOUBLE  --ops=MAX,MIN,SUM  --retries=5  --warmup=1  --iters=10  --root=0\n"
       "  --ints=N --doubles=N --longs=N --floats=N   global element counts (reduce.c defaults)\n"
       "  --n=N                        global count for every dtype (scalar mode north star: 1e9)\n"
@@ -592,13 +611,15 @@ int main(int argc, char** argv) {
         throw CliError("--single-process takes --collective=allreduce|host");
       if (c.env.world != 1) throw CliError("--single-process runs without a multi-process launcher");
     } else if (c.collective != "reduce" && c.collective != "allreduce" && c.collective != "direct" &&
-               c.collective != "direct-reduce") {
-      throw CliError("--collective must be reduce|allreduce|direct|direct-reduce");
+               c.collective != "direct-reduce" && c.collective != "fused") {
+      throw CliError("--collective must be reduce|allreduce|direct|direct-reduce|fused");
     }
     if (c.mode == "scalar" && (c.collective == "direct" || c.collective == "direct-reduce"))
       throw CliError("direct collectives are vector-mode only");
-    if (c.mode == "scalar" && c.collective != "allreduce" && !(args.has("single-process") && c.collective == "host"))
-      throw CliError("scalar mode uses --collective=allreduce (or host with --single-process)");
+    if (c.mode == "scalar" && c.collective != "allreduce" && c.collective != "fused" &&
+        !(args.has("single-process") && c.collective == "host"))
+      throw CliError("scalar mode uses --collective=allreduce|fused (or host with --single-process)");
+    if (c.mode == "vector" && c.collective == "fused") throw CliError("--collective=fused is scalar-mode only");
     std::vector<std::string> list;
     if (args.get_list("dtypes", &list)) {
       dtypes.clear();
@@ -682,7 +703,7 @@ int main(int argc, char** argv) {
   bool ok = false;
   try {
     c.boot = std::make_unique<TcpBootstrap>(c.env);
-    if (!is_direct(c)) {  // the direct path needs no RCCL (and may share one GPU between ranks)
+    if (!needs_no_rccl(c)) {  // direct / fused need no RCCL (and may share one GPU between ranks)
       c.comm = std::make_unique<RcclComm>(*c.boot, c.device);
       install_comm_abort_hook(c.comm.get());
     }

@@ -32,7 +32,7 @@ def run(cmd, timeout=300, cwd=None, env=None):
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=cwd, env=e)
 
 
-def torchrun(nproc, script_args, timeout=600, cwd=None):
+def torchrun(nproc, script_args, timeout=600, cwd=None, env=None):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port())] + script_args
-    return run(cmd, timeout=timeout, cwd=cwd)
+    return run(cmd, timeout=timeout, cwd=cwd, env=env)

@@ -211,6 +211,20 @@ def test_reduce_xgmi_direct_peer_reads(collective, nproc, graph):
     assert len(rows) == 12
 
 
+@pytest.mark.parametrize("nproc", [1, 3])
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+def test_reduce_xgmi_scalar_fused(nproc, graph):
+    # scalar mode with the fused in-kernel cross-rank finish (no RCCL): every rank's result is
+    # checked against the host fold of all ranks' local results (+ the ladder oracle per rank)
+    r = torchrun(nproc, ["--no-python", os.path.join(BIN, "reduce_xgmi"), "--mode=scalar", "--collective=fused",
+                         "--doubles=30000001", "--ints=20000003", "--dtypes=INT,DOUBLE", "--retries=2", "--iters=5",
+                         "--timeout=20"] + (["--graph"] if graph else []), timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "verification PASSED" in r.stderr
+    rows = [ln for ln in r.stdout.splitlines() if re.match(rf"^(INT|DOUBLE) (MAX|MIN|SUM) {nproc} ", ln)]
+    assert len(rows) == 12
+
+
 @pytest.mark.parametrize("count", ["1", "2", "3", "5", "17", "65", "4099"])
 def test_reduce_xgmi_direct_tiny_counts(count):
     # chunks shorter than a vector, empty chunks, sub-vector tails in the last chunk

@@ -74,3 +74,25 @@ def test_example_argmax_maxloc():
     r = run([sys.executable, os.path.join(ROOT, "examples", "05_argmax_maxloc.py")], cwd=ROOT, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "match torch: True" in r.stdout and "arg_reduce agrees: True" in r.stdout
+
+
+@pytest.mark.gpu
+def test_example_xgmi_collectives_single():
+    r = run([sys.executable, os.path.join(ROOT, "examples", "06_xgmi_collectives.py")], cwd=ROOT, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    m = re.search(r"\[rank 0\] fused global sum ([0-9.]+) \(torch: ([0-9.]+), epoch 10, channel ok\)", r.stdout)
+    assert m and abs(float(m.group(1)) - float(m.group(2))) <= 1e-9 * float(m.group(2)), r.stdout
+    assert "matches the gathered sum; no timeouts" in r.stdout
+
+
+@pytest.mark.gpu
+def test_example_xgmi_collectives_three_ranks_one_gpu(tmp_path):
+    """Three ranks sharing the one GPU of the box (gloo for the host-side agreement)."""
+    r = torchrun(3, [os.path.join(ROOT, "examples", "06_xgmi_collectives.py"), "--backend", "gloo"],
+                 cwd=tmp_path, timeout=300, env={"MIREDUCE_FORCE_DEVICE": "0"})
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    sums = re.findall(r"\[rank (\d)\] fused global sum ([0-9.]+) \(torch: ([0-9.]+), epoch 10, channel ok\)", r.stdout)
+    assert len(sums) == 3, r.stdout
+    assert len({s[1] for s in sums}) == 1  # bit-identical on every rank
+    assert abs(float(sums[0][1]) - float(sums[0][2])) <= 1e-9 * float(sums[0][2])
+    assert "matches the gathered sum; no timeouts" in r.stdout

@@ -239,7 +239,51 @@ def _vector_extras(ctx, steps: int = 5) -> dict:
             except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
                 out[key] = {"error": f"{type(e).__name__}: {e}"[:200]}
             torch.cuda.empty_cache()
+    if ctx.world_size > 1:
+        out["peer_read"] = _peer_read_extra(ctx)
     return out
+
+
+def _peer_read_extra(ctx, nbytes: int = 256 << 20, steps: int = 5) -> dict:
+    """xGMI ingress roofline on this job's GPUs (bandwidth_test --peer, simpleP2P.cu:314-329): every
+    rank's one-kernel read of ``nbytes`` from each of its world-1 peers at once, all ranks together
+    (between barriers). Per-rank ingress GB/s (min / max over ranks) and the node aggregate (all
+    bytes moved / the slowest rank's time). Errors are recorded, not raised."""
+    from cuda_mpi_reductions_amd.parallel import DirectComm
+    dev, world = ctx.device, ctx.world_size
+    try:
+        comm = DirectComm(dev, nbytes, timeout_s=5.0)  # collective: fails on every rank together
+    except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
+        return {"error": f"{type(e).__name__}: {e}"[:400]}
+    err, el = None, float("inf")
+    try:
+        comm.read_peers(nbytes)  # warm-up (maps, TLB)
+        _sync(dev)
+    except Exception as e:  # noqa: BLE001
+        err = f"{type(e).__name__}: {e}"[:200]
+    pdist.barrier(ctx)  # every rank reaches every collective below, failed or not
+    if err is None:
+        try:
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                comm.read_peers(nbytes)
+            _sync(dev)
+            el = time.perf_counter() - t0
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"[:200]
+    failed = pdist.max_over_ranks(1.0 if err else 0.0, ctx) > 0.5
+    ingress = 0.0 if err else (world - 1) * nbytes * steps / el / 1e9
+    lo = -pdist.max_over_ranks(-ingress, ctx)
+    hi = pdist.max_over_ranks(ingress, ctx)
+    slowest = pdist.max_over_ranks(el if not err else 0.0, ctx)
+    del comm
+    if failed:
+        errs = [None] * world
+        torch.distributed.all_gather_object(errs, err)
+        return {"error": "; ".join(f"rank {r}: {m}" for r, m in enumerate(errs) if m)[:400]}
+    return {"bytes_per_peer": nbytes, "steps": steps, "ingress_gbps_min": round(lo, 2),
+            "ingress_gbps_max": round(hi, 2),
+            "node_gbps": round(world * (world - 1) * nbytes * steps / slowest / 1e9, 2)}
 
 
 def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph: bool = True,

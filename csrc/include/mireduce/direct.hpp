@@ -77,6 +77,10 @@ class DirectAllreduce {
   void allreduce(size_t count, DType t, Op op, hipStream_t s);
   // out[i] = op over ranks of in[i] on `root` only (reduce-scatter + gather to the root).
   void reduce(size_t count, DType t, Op op, int root, hipStream_t s);
+  // Fabric probe (no reduction): one kernel reads `bytes_each` (<= bytes()) of every peer's input
+  // buffer at once over xGMI (own buffer when world == 1) — this rank's ingress roofline next to
+  // the collectives that run on the same buffers.
+  void read_peers(size_t bytes_each, hipStream_t s);
   // Synchronous reads (after the launches have completed).
   unsigned error() const;
   unsigned epoch() const;
@@ -92,7 +96,9 @@ class DirectAllreduce {
   unsigned* sig_ = nullptr;
   unsigned* ctl_ = nullptr;
   DirectDesc* desc_ = nullptr;
+  uint32_t* sink_ = nullptr;
   std::vector<void*> opened_;
+  std::vector<const void*> peer_in_;  // peers' input buffers as mapped here
 };
 
 // Chunk r of `count` elements split over `world` ranks, aligned to 16-byte vectors.

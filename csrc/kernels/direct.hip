@@ -7,6 +7,7 @@
 
 #include "mireduce/check.hpp"
 #include "mireduce/direct.hpp"
+#include "mireduce/peer.hpp"
 #include "mireduce/ops.hpp"
 
 namespace mireduce {
@@ -261,12 +262,17 @@ DirectAllreduce::DirectAllreduce(int device, size_t bytes, int grid, double time
 }
 
 DirectAllreduce::~DirectAllreduce() {
+  DeviceGuard g(device_);
   for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
+  (void)hipFree(sink_);
   (void)hipFree(desc_);
   (void)hipFree(ctl_);
   (void)hipFree(sig_);
   (void)hipFree(out_);
   (void)hipFree(in_);
+  // An ignored failure above (e.g. closing a mapping of a peer that already exited) must not stay
+  // behind as the thread's last error: the next launch's hipGetLastError() check would report it.
+  (void)hipGetLastError();
 }
 
 std::vector<char> DirectAllreduce::handles() const {
@@ -308,6 +314,7 @@ void DirectAllreduce::connect(int rank, int world, const std::vector<std::vector
       opened_.push_back(p[k]);
     }
     d.in[r] = static_cast<const char*>(p[0]);
+    peer_in_.push_back(p[0]);
     d.out[r] = static_cast<char*>(p[1]);
     d.sig[r] = static_cast<unsigned*>(p[2]);
   }
@@ -334,6 +341,7 @@ void DirectAllreduce::launch(size_t count, DType t, Op op, int gather_rank, hipS
     case Op::Max: fn = pick_type<MaxOp>(t, world_); break;
     default: MIREDUCE_REQUIRE(false, "direct: SUM, MIN or MAX");
   }
+  (void)hipGetLastError();  // report this launch's error only
   fn(desc_, count, gather_rank, grid_, s);
   MIREDUCE_HIP_THROW(hipGetLastError());
 }
@@ -343,6 +351,19 @@ void DirectAllreduce::allreduce(size_t count, DType t, Op op, hipStream_t s) { l
 void DirectAllreduce::reduce(size_t count, DType t, Op op, int root, hipStream_t s) {
   MIREDUCE_REQUIRE(root >= 0 && root < world_, "direct: root out of range");
   launch(count, t, op, root, s);
+}
+
+void DirectAllreduce::read_peers(size_t bytes_each, hipStream_t s) {
+  MIREDUCE_REQUIRE(connected_, "direct: connect() first");
+  MIREDUCE_REQUIRE(bytes_each <= bytes_, "direct: read_peers beyond the registered buffers");
+  DeviceGuard g(device_);
+  PeerSources src{};
+  int n = 0;
+  if (peer_in_.empty()) src.p[n++] = in_;
+  for (const void* p : peer_in_) src.p[n++] = p;
+  const int grid = 128 * n;  // peer_read's default: 128 workgroups per source
+  if (!sink_) MIREDUCE_HIP_THROW(hipMalloc(reinterpret_cast<void**>(&sink_), 128 * kMaxPeerSources * sizeof(uint32_t)));
+  peer_read(src, n, bytes_each, sink_, grid, s);
 }
 
 unsigned DirectAllreduce::error() const {

@@ -40,6 +40,7 @@ void peer_read(const PeerSources& srcs, int nsrc, size_t bytes_each, uint32_t* s
   MIREDUCE_REQUIRE(nsrc >= 1 && nsrc <= kMaxPeerSources, "peer_read: 1..16 sources");
   if (grid <= 0) grid = 128 * nsrc;
   grid = (grid + nsrc - 1) / nsrc * nsrc;
+  (void)hipGetLastError();  // the check below must see this launch only, not an earlier ignored call
   hipLaunchKernelGGL(kern::peer_read_kernel, dim3(grid), dim3(kern::kPeerBlock), 0, s, srcs, nsrc,
                      static_cast<uint64_t>(bytes_each / 16), sink);
   MIREDUCE_HIP_THROW(hipGetLastError());

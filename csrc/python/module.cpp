@@ -242,6 +242,9 @@ PYBIND11_MODULE(_C, m) {
       .def("reduce", [](DirectAllreduce& d, uint64_t count, int dtype, int op, int root, uintptr_t stream) {
         d.reduce(count, static_cast<DType>(dtype), static_cast<Op>(op), root, as_stream(stream));
       }, py::arg("count"), py::arg("dtype"), py::arg("op"), py::arg("root") = 0, py::arg("stream") = 0)
+      .def("read_peers", [](DirectAllreduce& d, uint64_t bytes_each, uintptr_t stream) {
+        d.read_peers(bytes_each, as_stream(stream));
+      })
       .def("error", &DirectAllreduce::error)
       .def("epoch", &DirectAllreduce::epoch);
 

@@ -38,10 +38,12 @@ XrankChannel::XrankChannel(int device, double timeout_s) : timeout_s_(timeout_s)
 }
 
 XrankChannel::~XrankChannel() {
+  DeviceGuard g(device_);
   for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
   (void)hipFree(desc_dev_);
   (void)hipFree(counters_);
   (void)hipFree(mbox_);
+  (void)hipGetLastError();  // ignored failures above must not surface at the next launch check
 }
 
 IpcHandleBytes XrankChannel::handle() const {

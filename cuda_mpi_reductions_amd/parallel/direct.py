@@ -77,7 +77,9 @@ class DirectComm:
         if world > 1:
             errs = [None] * world
             dist.all_gather_object(errs, err, group=group)
-        bad = [f"rank {r}: {m}" for r, m in enumerate(errs) if m]
+        # the ranks that failed themselves first (the others only saw a missing peer)
+        own = [f"rank {r}: {m}" for r, m in enumerate(errs) if m and not m.startswith("a peer")]
+        bad = own + [f"rank {r}: {m}" for r, m in enumerate(errs) if m and m.startswith("a peer")]
         if bad:
             raise RuntimeError("direct collective unavailable: " + "; ".join(bad)[:500])
         self.rank, self.world = rank, world
@@ -138,6 +140,12 @@ class DirectComm:
         if self.rank == root:
             self._stage(t, False)
         return t
+
+    def read_peers(self, nbytes: Optional[int] = None) -> None:
+        """Fabric probe (no reduction): one kernel on the current stream reads ``nbytes`` (default:
+        all registered bytes) of every peer's input buffer at once over xGMI."""
+        nb = self.nbytes if nbytes is None else int(nbytes)
+        self._d.read_peers(nb, torch.cuda.current_stream(self.device).cuda_stream)
 
     def check(self) -> Optional[str]:
         """None if no device-side barrier ever timed out on any rank (collective)."""

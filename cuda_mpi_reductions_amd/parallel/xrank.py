@@ -58,7 +58,9 @@ def open_channel(device: torch.device, group=None, timeout_s: float = 2.0):
                 err = f"{type(e).__name__}: {e}"
     errs: list = [None] * world
     dist.all_gather_object(errs, err, group=group)  # also the barrier: all mailboxes mapped
-    bad = [f"rank {r}: {m}" for r, m in enumerate(errs) if m]
+    # the ranks that failed themselves first (the others only saw a missing peer)
+    own = [f"rank {r}: {m}" for r, m in enumerate(errs) if m and not m.startswith("a peer")]
+    bad = own + [f"rank {r}: {m}" for r, m in enumerate(errs) if m and m.startswith("a peer")]
     if bad:
         raise RuntimeError("fused cross-rank finish unavailable: " + "; ".join(bad)[:500])
     return ch

@@ -176,6 +176,11 @@ def test_direct_comm_world1_views_and_staging():
     comm.launch_reduce(77, torch.int32, "max", root=0)
     torch.cuda.synchronize()
     assert torch.equal(ov, iv) and comm.epoch == 2
+    comm.read_peers()  # fabric probe at world 1 reads the own buffer: no barrier, no epoch change
+    torch.cuda.synchronize()
+    assert comm.epoch == 2 and comm.check() is None
+    with pytest.raises(Exception, match="beyond the registered"):
+        comm.read_peers((1 << 20) + 4096)
 
 
 @pytest.mark.parametrize("nproc", [2, 3])
@@ -201,6 +206,7 @@ def test_bench_vector_extras_in_headline(tmp_path):
     ex = d["reduce_c_vector"]
     for k in ("reduce_rccl", "reduce_direct", "allreduce_rccl", "allreduce_direct"):
         assert ex[k].get("verified") is True and ex[k]["gibps"] > 0, (k, ex[k])
+    assert "peer_read" not in ex  # one rank: no peers to read
 
 
 def test_bench_fused_corrupt_rank_fails_verification(tmp_path, monkeypatch):
@@ -241,6 +247,8 @@ def test_bench_eight_ranks_auto_on_one_gpu(tmp_path, monkeypatch):
     assert "auto" in d["config"]["collective"] and "reduce_c_vector" in d
     ex = d["reduce_c_vector"]
     assert ex["reduce_direct"].get("verified") is True, ex
+    pr = ex["peer_read"]  # fabric probe: 8 ranks reading each other's buffers (here all on one GPU)
+    assert "error" not in pr and 0 < pr["ingress_gbps_min"] <= pr["ingress_gbps_max"] and pr["node_gbps"] > 0, pr
 
 
 def test_reduce_xgmi_direct_eight_ranks_on_one_gpu():

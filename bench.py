@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -67,9 +68,10 @@ def parse_args(argv=None):
                         "auto = fused if its self-check passes on every rank, else rccl (GPU scalar configs)")
     p.add_argument("--xrank-timeout", type=float, default=30.0,
                    help="fused finish: seconds a kernel waits for a peer's partial before flagging the channel")
-    p.add_argument("--tune-steps", type=int, default=20,
+    p.add_argument("--tune-steps", type=int, default=0,
                    help="--collective auto: steps of the short per-candidate measurement that picks the headline "
-                        "combine (fused 1 lane, fused 2 lanes, RCCL pipelined)")
+                        "combine (fused 1 lane, fused 2 lanes, RCCL pipelined); 0 = enough steps for ~30 ms of "
+                        "reduction per candidate (20..400)")
     p.add_argument("--vector-impl", choices=["rccl", "direct"], default="rccl",
                    help="vector (reduce.c) configs: torch.distributed collective, or the one-kernel direct "
                         "peer-read collective over xGMI (GPUs)")
@@ -89,9 +91,10 @@ def parse_args(argv=None):
     p.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
                    help="graph: replay the timed steps as captured hipGraphs (chunks of --graph-chunk steps); "
                         "eager: issue every step from Python; auto: graph on GPUs when capturable")
-    p.add_argument("--graph-chunk", type=int, default=128,
-                   help="steps per captured graph (each graph ends by joining its last all-reduce, so fewer, "
-                        "longer graphs leave fewer all-reduce-latency bubbles at N>1)")
+    p.add_argument("--graph-chunk", type=int, default=0,
+                   help="steps per captured graph (each graph ends by joining its lanes / last all-reduce, so "
+                        "fewer, longer graphs leave fewer bubbles); 0 = auto: every timed step in one graph "
+                        "(<= 4096) for the in-kernel fused finish, 128 when steps issue RCCL collectives")
     p.add_argument("--inject-fault", default=None,
                    help="failure-detection test: KIND[@RANK][:STEP], KIND = exit|hang|corrupt|delay=<ms> "
                         "(steps count warm-up first; forces --launch eager)")
@@ -244,6 +247,12 @@ def _vector_extras(ctx, steps: int = 5) -> dict:
     return out
 
 
+def _auto_tune_steps(bytes_per_gpu: float, target_s: float = 0.03) -> int:
+    """Tuning steps per candidate: ~``target_s`` of reduction at ~7 TB/s per GPU (20 steps of a
+    1 GB shard are 2.8 ms — within launch noise of each other), clamped to 20..400."""
+    return int(min(400, max(20, math.ceil(target_s / max(bytes_per_gpu / 7e12, 1e-9)))))
+
+
 def _peer_read_extra(ctx, nbytes: int = 256 << 20, steps: int = 5) -> dict:
     """xGMI ingress roofline on this job's GPUs (bandwidth_test --peer, simpleP2P.cu:314-329): every
     rank's one-kernel read of ``nbytes`` from each of its world-1 peers at once, all ranks together
@@ -286,6 +295,16 @@ def _peer_read_extra(ctx, nbytes: int = 256 << 20, steps: int = 5) -> dict:
             "node_gbps": round(world * (world - 1) * nbytes * steps / slowest / 1e9, 2)}
 
 
+def _graph_chunk(requested: int, steps: int, issues_collective: bool) -> int:
+    """Steps per captured graph. Auto: one graph for all the steps when they are kernels only (the
+    fused finish; measured at the 1 GB N=8 shard with 2 lanes, 1000 steps: 7.32-7.34 TB/s as one
+    graph vs 7.17-7.27 in chunks of 128, profiles/r2_shard/run4.sh), 128 when every step also
+    captures an RCCL collective."""
+    if requested > 0:
+        return requested
+    return 128 if issues_collective else max(1, min(steps, 4096))
+
+
 def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph: bool = True,
              steps: "int | None" = None) -> dict:
     """Time K steps (after ``warmup`` eager steps); returns elapsed (MAX over ranks), the launch
@@ -320,7 +339,8 @@ def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph
         # on success or all fall back to eager issue); one untimed replay uploads the graphs.
         W = warmup
         sg = StepGraph(lambda j: wl.step(slots[W + j:W + j + 1], async_op=True), K, dev,
-                       chunk=args.graph_chunk, serial=serial, fork=wl.fork, join=wl.join)
+                       chunk=_graph_chunk(args.graph_chunk, K, wl.issues_collective), serial=serial,
+                       fork=wl.fork, join=wl.join)
         if sg.capture(group_agree=ctx.world_size > 1):
             launch = f"graph (chunk {sg.chunk}, {sg.reps} replays" + (f" + 1 of {sg.rem})" if sg.rem else ")")
             for g in sg.graphs:
@@ -431,15 +451,15 @@ def main(argv=None) -> int:
     dev = ctx.device
 
     primary_serial = args.serial
-    tuning = None
+    tuning, tune_steps = None, 0
     if args.collective == "auto" and collective == "fused" and not primary_serial and not fault.enabled:
         # Pick the headline combine by a short measurement of each candidate (same graph-replay
         # protocol, MAX over ranks, so every rank picks the same): the in-kernel fused finish on one
         # stream lane or two, or the RCCL all-reduce overlapped with the next local reduce.
         # Two rounds, best of each candidate: the first candidate of round 1 otherwise pays for
         # the GPU ramping its clocks (measured: -2 % at 8 GB on an otherwise equal kernel).
-        T = max(4, min(K, args.tune_steps))
-        tuning = {}
+        T = max(4, args.tune_steps) if args.tune_steps else _auto_tune_steps(wl.bytes_total / ctx.world_size)
+        tuning, tune_steps = {}, T
         for _round in range(2):
             for coll, nl in (("fused", 1), ("fused", 2), ("rccl", 1)):
                 key = f"{coll}_{nl}lane"
@@ -545,7 +565,7 @@ def main(argv=None) -> int:
             "native_ext": os.path.basename(native_path()),
         }
         if tuning is not None:
-            line["collective_tuning"] = {"steps": max(4, min(K, args.tune_steps)), "gbps": tuning,
+            line["collective_tuning"] = {"steps": tune_steps, "gbps": tuning,
                                          "chosen": f"{collective}_{lanes}lane"}
         if m2 is not None:
             line["serial_gbps"] = round(bytes_step * K / m2["elapsed"] / 1e9, 3)

@@ -156,6 +156,7 @@ def test_bench_auto_tunes_the_combine(tmp_path):
     tun = d["collective_tuning"]
     assert set(tun["gbps"]) == {"fused_1lane", "fused_2lane", "rccl_1lane"} and all(v > 0 for v in tun["gbps"].values())
     assert tun["chosen"] == max(tun["gbps"], key=tun["gbps"].get)
+    assert tun["steps"] == 400  # auto: ~30 ms of reduction per candidate, clamped (400 MB shard)
     assert d["config"]["collective"].startswith(tun["chosen"].split("_")[0])
     assert d["serial_gbps"] > 0 and d["serial_launch"].startswith("graph")
 

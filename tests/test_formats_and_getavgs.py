@@ -63,3 +63,28 @@ def test_python_cli_grammar():
     assert cli.parse_count("1e9") == 10**9 and cli.parse_count("4k") == 4096
     with pytest.raises(cli.CliError):
         cli.parse(["method=SUM"])
+
+
+@pytest.mark.skipif(not have_ref, reason="reference data not mounted")
+def test_getavgs_averages_the_co_mode_raw_outputs():
+    """The BG/L CO-mode runs were never averaged by the reference's authors:
+    getAvgs over the concatenated `stdout-co-*` files gives the table the survey quotes."""
+    lines = []
+    for name in sorted(os.listdir(os.path.join(REF, "raw_output"))):
+        if name.startswith("stdout-co-"):
+            with open(os.path.join(REF, "raw_output", name)) as f:
+                lines += f.readlines()
+    avgs = getavgs.averages(lines)
+    expect = {  # SURVEY.md §6.3, GiB/s, 3 decimals
+        ("INT", "SUM"): {32: 10.037, 128: 40.142, 512: 160.437},
+        ("INT", "MIN"): {32: 9.743, 128: 38.967, 512: 155.720},
+        ("INT", "MAX"): {32: 9.743, 128: 38.965, 512: 155.675},
+        ("DOUBLE", "SUM"): {32: 5.396, 128: 21.515, 512: 84.944},
+        ("DOUBLE", "MIN"): {32: 2.977, 128: 11.909, 512: 48.937},
+        ("DOUBLE", "MAX"): {32: 2.978, 128: 11.937, 512: 48.685},
+    }
+    for key, by_nodes in expect.items():
+        got = {n: float(v) for n, v in avgs[key]}
+        assert set(got) == set(by_nodes), (key, got)
+        for n, v in by_nodes.items():
+            assert abs(got[n] - v) <= 1.5e-3, (key, n, got[n], v)  # survey: rounded; bc: truncated

@@ -72,7 +72,7 @@ def test_sweep_node_preset_matrix():
     for coll in ("reduce", "allreduce", "direct-reduce", "direct"):
         e = plan[names.index(f"vector-{coll}")]
         assert e[0] == "reduce_xgmi" and f"--collective={coll}" in e[3] and "--graph" in e[3]
-    for coll in ("rccl", "fused"):
+    for coll in ("allreduce", "fused"):
         e = plan[names.index(f"scalar-{coll}")]
         assert "--mode=scalar" in e[3] and f"--collective={coll}" in e[3] and "--graph" in e[3]
     assert names[-1] == "bench"

@@ -67,7 +67,7 @@ def node_preset(extra: list[str]) -> list[tuple]:
     for coll in VECTOR_COLLECTIVES:
         entries.append(("reduce_xgmi", f"vector-{coll}", "ranks",
                         ["--mode=vector", f"--collective={coll}", "--graph", "--dtypes=INT,DOUBLE"] + extra))
-    for coll in ("rccl", "fused"):  # simpleMPI's scalar combine: RCCL vs the in-kernel fused finish
+    for coll in ("allreduce", "fused"):  # simpleMPI's scalar combine: RCCL vs the in-kernel fused finish
         entries.append(("reduce_xgmi", f"scalar-{coll}", "ranks",
                         ["--mode=scalar", f"--collective={coll}", "--graph", "--dtypes=INT,DOUBLE"] + extra))
     entries.append(("bench", "bench", "ranks", ["--steps", "50", "--warmup", "10"]))

@@ -346,3 +346,21 @@ def test_bench_maxloc_config(tmp_path, launch):
     assert d["verified"] is True and d["config"]["op"] == "MAXLOC"
     assert d["config"]["launch"].startswith(launch)
     assert d["config"]["kernel_plan"]["splits"] > 1
+
+
+def test_sweep_node_preset_on_one_gpu(tmp_path):
+    """tools/sweep.py --preset node end to end at P=1: fabric probe (WAIVED on one GPU), reduce.c
+    vector mode over RCCL and direct, scalar mode over RCCL and the fused finish, the bench; every
+    point's rc file, the getAvgs results and the bench JSONL."""
+    out = tmp_path / "node"
+    r = run([sys.executable, os.path.join(ROOT, "tools", "sweep.py"), "--preset", "node", "--ranks", "1",
+             "--out", str(out), "--timeout", "300", "--", "--ints=1000003", "--doubles=1000003", "--retries=1"],
+            timeout=1200)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    for name in ("vector-reduce", "vector-allreduce", "vector-direct-reduce", "vector-direct", "scalar-allreduce",
+                 "scalar-fused", "bench"):
+        assert (out / name / f"stdout-{name}-P1.rc").read_text().strip() == "0", name
+    assert (out / "fabric" / "stdout-fabric-PNone.rc").read_text().strip() == "0"
+    assert "WAIVED" in (out / "fabric" / "stdout-fabric-PNone.txt").read_text()
+    assert (out / "scalar-fused" / "results" / "DOUBLE_SUM.txt").read_text().startswith("\nDOUBLE SUM 1 ")
+    assert "scaling efficiency" in r.stdout and (out / "bench" / "bench.jsonl").exists()

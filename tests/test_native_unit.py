@@ -1,6 +1,8 @@
 """Native C++ unit tests (host code), the TCP bootstrap under torchrun and mpirun, host
 sanitizers (ASan/UBSan on host code), and the resumable sweep orchestration."""
 import os
+import re
+import sys
 import subprocess
 
 import pytest
@@ -186,3 +188,25 @@ def test_cmake_build_and_ctest(tmp_path):
             env={"ASAN_OPTIONS": "detect_leaks=1"})
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert "tests passed" in r.stdout
+
+
+def test_prof_db_summary_and_steady_overlap(tmp_path):
+    """tools/prof_db.py on a synthetic rocpd-style SQLite file: per-kernel table, and --steady's
+    period / overlap of back-to-back kernels (two lanes overlapping vs one lane with gaps)."""
+    import sqlite3
+    db = tmp_path / "t_results.db"
+    c = sqlite3.connect(db)
+    c.execute("create table kernels (name text, start integer, end integer)")
+    # lane-overlapped run: a kernel every 100 us lasting 150 us; then idle; then a gapped run
+    rows = [("reduce_stream<x>", i * 100_000, i * 100_000 + 150_000) for i in range(20)]
+    rows += [("reduce_stream<x>", 10_000_000 + i * 200_000, 10_000_000 + i * 200_000 + 150_000) for i in range(5)]
+    rows += [("fill_kernel", 50_000_000, 50_010_000)]
+    c.executemany("insert into kernels values (?, ?, ?)", rows)
+    c.commit()
+    c.close()
+    r = run([sys.executable, os.path.join(ROOT, "tools", "prof_db.py"), str(db), "--steady", "reduce_stream"])
+    assert r.returncode == 0, r.stderr
+    assert "25 x     150.00 us" in r.stdout and "fill_kernel" in r.stdout
+    m = re.search(r"steady: 20 x 'reduce_stream' back to back: period ([0-9.]+) us per kernel, mean duration "
+                  r"150.00 us, >= 2 running ([0-9.]+) %", r.stdout)
+    assert m and abs(float(m.group(1)) - 102.5) < 0.01 and float(m.group(2)) > 40, r.stdout

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 SQLite (rocpd) output: per-kernel call count, total / mean / min / max
 duration, and (--timeline) the gaps between consecutive dispatches.
-    usage: tools/prof_db.py <results.db> [--csv out.csv] [--timeline N]
+    usage: tools/prof_db.py <results.db> [--csv out.csv] [--timeline N] [--steady SUBSTR]
+--steady: for the longest back-to-back run of kernels whose name contains SUBSTR (runs split at
+idle gaps > 1 ms), the period per kernel (first start to last end / count), the mean kernel
+duration and how much of the run had two or more of them executing at once (multi-stream overlap).
 (rocprofv3 on ROCm 7 writes <dir>/<name>_results.db unless --output-format csv is given.)"""
 import argparse
 import csv
@@ -23,6 +26,7 @@ def main(argv=None):
     ap.add_argument("db")
     ap.add_argument("--csv")
     ap.add_argument("--timeline", type=int, default=0, help="print the first N dispatches with gaps")
+    ap.add_argument("--steady", default="", help="period / overlap of the longest run of matching kernels")
     a = ap.parse_args(argv)
     ks = kernels(a.db)
     by = {}
@@ -49,7 +53,36 @@ def main(argv=None):
             gap = (s - prev) / 1e3 if prev is not None else 0.0
             print(f"  +{gap:9.2f} us gap  {(e - s) / 1e3:9.2f} us  {n[:100]}")
             prev = e
+    if a.steady:
+        print(steady(ks, a.steady))
     return 0
+
+
+def steady(ks, substr: str, idle_ns: float = 1e6) -> str:
+    ms = sorted((s, e) for n, s, e in ks if substr in n)
+    if not ms:
+        return f"steady: no kernel matches {substr!r}"
+    runs, cur = [], [ms[0]]
+    for s, e in ms[1:]:
+        if s - max(x[1] for x in cur[-4:]) > idle_ns:
+            runs.append(cur)
+            cur = []
+        cur.append((s, e))
+    runs.append(cur)
+    run = max(runs, key=len)
+    t0, t1 = run[0][0], max(e for _, e in run)
+    busy2 = 0.0  # time with >= 2 matching kernels active (sweep over start/end events)
+    ev = sorted([(s, 1) for s, _ in run] + [(e, -1) for _, e in run])
+    active, last = 0, t0
+    for t, d in ev:
+        if active >= 2:
+            busy2 += t - last
+        active += d
+        last = t
+    n = len(run)
+    dur = statistics.mean(e - s for s, e in run) / 1e3
+    return (f"steady: {n} x {substr!r} back to back: period {(t1 - t0) / n / 1e3:.2f} us per kernel, "
+            f"mean duration {dur:.2f} us, >= 2 running {100 * busy2 / (t1 - t0):.1f} % of the run")
 
 
 if __name__ == "__main__":

@@ -238,6 +238,7 @@ def _vector_extras(ctx, steps: int = 5) -> dict:
                 el, ok = _time_vector(wl, ctx, steps, 1, None, True)
                 out[key] = {"gibps": round(wl.bytes_total * steps / el / float(1 << 30), 3),
                             "ms": round(el / steps * 1e3, 4), "verified": ok}
+                wl.close()  # collective: the next registration may reuse these addresses
                 del wl
             except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
                 out[key] = {"error": f"{type(e).__name__}: {e}"[:200]}
@@ -285,7 +286,7 @@ def _peer_read_extra(ctx, nbytes: int = 256 << 20, steps: int = 5) -> dict:
     lo = -pdist.max_over_ranks(-ingress, ctx)
     hi = pdist.max_over_ranks(ingress, ctx)
     slowest = pdist.max_over_ranks(el if not err else 0.0, ctx)
-    del comm
+    comm.close()
     if failed:
         errs = [None] * world
         torch.distributed.all_gather_object(errs, err)

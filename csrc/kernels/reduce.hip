@@ -107,22 +107,43 @@ __device__ __forceinline__ T from_bits64(uint64_t b) {
 // one store round and the polls overlap. Words are (epoch << 32 | 32 data bits), written and
 // read with system-scope atomics (8-byte single-copy atomic over xGMI), so a matching epoch in
 // both words of a slot means the whole partial of this launch has landed.
-template <class OpT, class AccT>
-__device__ __forceinline__ AccT xrank_finish(const XrankDesc* d, AccT t, unsigned e, unsigned err) {
+//
+// The descriptor fields a lane needs are read by xrank_prefetch: in the polled fan-in the
+// finisher is known up front and issues these loads before it waits for the other workgroups'
+// partials, so their latency (a descriptor miss, ~0.5 us at N=1) is off the critical path.
+struct XrankLane {
+  uint64_t* peer;       // rank `lane`'s mailbox (lane < world, lane != rank)
+  const uint64_t* own;  // this rank's mailbox
+  uint64_t limit;       // wait bound in wall-clock ticks (0 after a sticky error: look once)
+  unsigned e;           // this launch's epoch
+  int world, rank;
+};
+
+__device__ __forceinline__ XrankLane xrank_prefetch(const XrankDesc* d, unsigned e, unsigned err) {
   const int lane = threadIdx.x & 63;
-  const int world = d->world;
-  const int rank = d->rank;
+  XrankLane x;
+  x.world = d->world;
+  x.rank = d->rank;
+  x.peer = d->peer_mbox[lane < kMaxXrankRanks ? lane : 0];
+  x.own = d->own_mbox;
+  x.limit = err ? 0 : d->timeout_ticks;  // a sticky error means a peer is gone: do not wait
+  x.e = e;
+  return x;
+}
+
+template <class OpT, class AccT>
+__device__ __forceinline__ AccT xrank_finish(const XrankDesc* d, const XrankLane& x, AccT t) {
+  const int lane = threadIdx.x & 63;
+  const unsigned e = x.e;
   const uint64_t parity = static_cast<uint64_t>(e & 1u) * kMaxXrankRanks;
   const uint64_t tag = static_cast<uint64_t>(e) << 32;
   const uint64_t bits = to_bits64(t);
   AccT v = OpT::template identity<AccT>();
-  if (lane < world && lane != rank) {
-    uint64_t* dst = d->peer_mbox[lane] + (parity + rank) * 2;
+  if (lane < x.world && lane != x.rank) {
+    uint64_t* dst = x.peer + (parity + x.rank) * 2;
     __hip_atomic_store(dst, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(dst + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint64_t* src = d->own_mbox + (parity + lane) * 2;
-    // A sticky error (an earlier launch timed out) means a peer is gone: look once, do not wait.
-    const uint64_t limit = err ? 0 : d->timeout_ticks;
+    const uint64_t* src = x.own + (parity + lane) * 2;
     const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
     for (;;) {
       const uint64_t lo = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -131,13 +152,13 @@ __device__ __forceinline__ AccT xrank_finish(const XrankDesc* d, AccT t, unsigne
         v = from_bits64<AccT>((lo & 0xffffffffull) | (hi << 32));
         break;
       }
-      if (static_cast<uint64_t>(wall_clock64()) - t0 > limit) {
+      if (static_cast<uint64_t>(wall_clock64()) - t0 > x.limit) {
         __hip_atomic_fetch_or(d->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
-  } else if (lane == rank) {
+  } else if (lane == x.rank) {
     v = t;  // this rank's own partial never leaves the register file
   }
   if (lane == 0) __hip_atomic_store(d->epoch, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -273,7 +294,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   //      no tickets, no second load round.
   if (gridDim.x == 1) {
     if (threadIdx.x < 64) {
-      if (a.xrank) v = xrank_finish<OpT, AccT>(a.xrank, v, xr_epoch, xr_err);
+      if (a.xrank) v = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), v);
       if (threadIdx.x == 0) *static_cast<AccT*>(a.out) = v;
     }
     return;
@@ -294,6 +315,9 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       __hip_atomic_store(sl + 1, kSlotTag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (blockIdx.x != gridDim.x - 1) return;
+    // The finisher: start the cross-rank descriptor loads now, they land while it polls.
+    XrankLane xl{};
+    if (a.xrank && threadIdx.x < 64) xl = xrank_prefetch(a.xrank, xr_epoch, xr_err);
     AccT t = OpT::template identity<AccT>();
     // Bounded like every device-side wait here (all workgroups of this launch always publish, so
     // the bound is never reached by a correct launch; it only keeps a misuse from hanging the GPU).
@@ -350,7 +374,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     }
     t = block_reduce<OpT, AccT, BLOCK>(t, lds);
     if (threadIdx.x < 64) {
-      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, t, xr_epoch, xr_err);
+      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xl, t);
       if (threadIdx.x == 0) *static_cast<AccT*>(a.out) = t;
     }
     return;
@@ -397,7 +421,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     for (unsigned i = threadIdx.x; i < gridDim.x; i += BLOCK) t = OpT::apply(t, load_sc1(&partials[i]));
     t = block_reduce<OpT, AccT, BLOCK>(t, lds);
     if (threadIdx.x < 64) {
-      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, t, xr_epoch, xr_err);
+      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), t);
       if (threadIdx.x == 0) {
         *static_cast<AccT*>(a.out) = t;
         // reset: the top counter, or (one group) the group counter itself
@@ -429,7 +453,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     const int lane = threadIdx.x;
     AccT t = lane < static_cast<int>(G) ? load_sc1(&gpart[lane]) : OpT::template identity<AccT>();
     t = wave_reduce<OpT>(t);
-    if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, t, xr_epoch, xr_err);
+    if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), t);
     if (lane == 0) {
       *static_cast<AccT*>(a.out) = t;
       __hip_atomic_store(&a.tickets[G * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -222,9 +222,12 @@ class ScalarReduction:
         dev = self.ctx.device
         torch.cuda.synchronize(dev)
         n = self.n_streams if streams is None else max(1, int(streams))
-        if collective == "fused":
-            from ..parallel.xrank import open_channel
-        old = self.lanes
+        from ..parallel.xrank import close_channels, open_channel
+        old = [(st, red) for st, red, _, _ in self.lanes]  # keep streams and workspaces
+        # Drop every reference to the old bound reductions and channels, then tear the channels
+        # down collectively (a new mailbox may reuse an old one's address; see close_channels).
+        self.lanes, self.bound = [], None
+        close_channels(self.channels, dev)
         lanes, channels = [], []
         for k in range(n):
             if n == 1:
@@ -450,6 +453,13 @@ class VectorReduction:
     def step(self, async_op: bool = False):
         self.restore()
         return self.collective(async_op=async_op)
+
+    def close(self) -> None:
+        """Collective: release the direct collective's registered buffers (``DirectComm.close``) so
+        a following registration on any rank cannot race a peer still mapping them."""
+        if self.comm is not None:
+            self.comm.close()
+            self.comm = None
 
     def verify(self) -> dict:
         """Gather every rank's input and combine on the result holders; integer SUM wraps like

@@ -161,3 +161,17 @@ class DirectComm:
     @property
     def epoch(self) -> int:
         return int(self._d.epoch())
+
+    def close(self) -> None:
+        """Collective teardown: unmap the peers' buffers, free this rank's, then wait for every rank.
+        A registration that follows (here or on a peer) may get the same addresses back, and its
+        IPC export failed while a peer still mapped the old buffer at that address (seen in the
+        bench's back-to-back registrations); after the barrier nobody does."""
+        if self._d is not None:
+            torch.cuda.synchronize(self.device)
+            self._d = None  # native destructor: close peer mappings, free own buffers
+        if self.world > 1:
+            if dist.get_backend(self.group) == "nccl":
+                dist.barrier(group=self.group, device_ids=[self.device.index])
+            else:
+                dist.barrier(group=self.group)

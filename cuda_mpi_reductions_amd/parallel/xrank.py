@@ -21,7 +21,7 @@ import torch.distributed as dist
 
 from .._native import native
 
-__all__ = ["open_channel", "check_channel"]
+__all__ = ["open_channel", "check_channel", "close_channels"]
 
 
 def open_channel(device: torch.device, group=None, timeout_s: float = 2.0):
@@ -77,3 +77,19 @@ def check_channel(channels, group=None) -> Optional[str]:
         dist.all_reduce(t, group=group)
         bad = int(t.item())
     return None if bad == 0 else f"fused cross-rank finish: {bad} channel(s) timed out waiting for a peer"
+
+
+def close_channels(channels: list, device: torch.device, group=None) -> None:
+    """Collective teardown of this rank's channels (the caller drops every other reference, e.g.
+    the bound reductions, first): the list is emptied, mappings closed, mailboxes freed, then all
+    ranks meet — a channel opened next may reuse a mailbox address, and its IPC export must not
+    race a peer that still maps the old mailbox there."""
+    had = bool(channels)
+    if had:
+        torch.cuda.synchronize(device)
+    channels.clear()
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        if dist.get_backend(group) == "nccl":
+            dist.barrier(group=group, device_ids=[device.index])
+        else:
+            dist.barrier(group=group)

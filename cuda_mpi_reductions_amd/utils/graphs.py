@@ -21,11 +21,17 @@ every rank falls back to eager issue.
 """
 from __future__ import annotations
 
+import time
 from typing import Callable, Optional
 
 import torch
 
 __all__ = ["StepGraph", "pick_chunk"]
+
+
+def _nccl_group() -> bool:
+    dist = torch.distributed
+    return dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"
 
 
 def pick_chunk(n_steps: int, max_chunk: int = 32) -> int:
@@ -68,12 +74,24 @@ class StepGraph:
                 self.join()
         return g
 
-    def capture(self, group_agree: bool = False) -> bool:
-        """Capture the chunk graph (and the remainder graph). Returns True if graphs will be used."""
+    def capture(self, group_agree: bool = False, settle_s: Optional[float] = None) -> bool:
+        """Capture the chunk graph (and the remainder graph). Returns True if graphs will be used.
+
+        ``settle_s`` (default: 0.35 s when a NCCL process group exists, else 0): wait after the
+        pre-capture synchronisation so ProcessGroupNCCL's watchdog retires every eager collective
+        first. HIP refuses a query of an event recorded on a stream that is capturing at that moment
+        (hipErrorCapturedEvent); the watchdog queries the end events of pending eager works every
+        ~100 ms and, when one such query fails during our capture — the captured collectives put
+        the NCCL stream into the capture — it aborts the whole process (seen in the tuning runs,
+        whose 128-step RCCL captures take tens of ms)."""
         ok = True
         prev = torch.cuda.current_stream(self.device)
+        if settle_s is None:
+            settle_s = 0.35 if _nccl_group() else 0.0
         try:
             torch.cuda.synchronize(self.device)
+            if settle_s > 0:
+                time.sleep(settle_s)
             self.graphs = [self._capture_one(self.chunk)]
             if self.rem:
                 self.graphs.append(self._capture_one(self.rem))

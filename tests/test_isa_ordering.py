@@ -72,10 +72,8 @@ def test_polled_fanin_tagged_slots(tmp_path):
     poll = _first(ins, r"^global_load_dwordx2 .* sc1$", st)
     assert poll is not None and re.search(r"^global_load_dwordx2 .* offset:8 sc1$", ins[poll + 1])
     assert _first(ins, r"^s_sleep", poll) is not None and _first(ins, r"^s_memrealtime", st) is not None
-    # the ticketed path's atomic must come after the polled path has ended (separate branch)
-    end = _first(ins, r"^s_endpgm", poll)
-    atom = _first(ins, r"^global_atomic_add", st)
-    assert end is not None and (atom is None or atom > end)
+    # (hipcc lays the polled and ticketed branches out in either order, so no check here compares
+    # positions across the two branches)
 
 
 def test_xrank_exchange_is_system_scope(tmp_path):

@@ -342,7 +342,8 @@ def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph
         sg = StepGraph(lambda j: wl.step(slots[W + j:W + j + 1], async_op=True), K, dev,
                        chunk=_graph_chunk(args.graph_chunk, K, wl.issues_collective), serial=serial,
                        fork=wl.fork, join=wl.join)
-        if sg.capture(group_agree=ctx.world_size > 1):
+        # (kernel-only steps keep the NCCL stream out of the capture: no watchdog settle needed)
+        if sg.capture(group_agree=ctx.world_size > 1, settle_s=None if wl.issues_collective else 0.0):
             launch = f"graph (chunk {sg.chunk}, {sg.reps} replays" + (f" + 1 of {sg.rem})" if sg.rem else ")")
             for g in sg.graphs:
                 g.replay()

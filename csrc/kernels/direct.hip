@@ -61,12 +61,21 @@ __device__ __forceinline__ uint64_t chunk_elems(uint64_t count, int world) {
   return (per + N - 1) / N * N;
 }
 
-// W > 0: exactly W ranks, every peer's load of a vector issued before any is combined.
+// Vectors per thread per loop trip in the W-rank kernel: small worlds have few peer loads per
+// vector, so each thread takes U vectors and issues all U * W loads before combining (at least
+// 4 loads in flight per lane; a 1- or 2-rank pass with one or two was latency-bound).
+template <int W>
+constexpr int direct_unroll() {
+  return W >= 4 ? 1 : (W >= 2 ? 2 : 4);
+}
+
+// W > 0: exactly W ranks, every peer's load of U vectors issued before any is combined.
 // W == 0: any world (runtime loop).
 template <class OpT, class T, int W>
 __global__ __launch_bounds__(kDirectBlock) void direct_kernel(const DirectDesc* __restrict__ d, uint64_t count,
                                                                int gather_rank) {
   constexpr int N = 16 / sizeof(T);
+  constexpr int U = W > 0 ? direct_unroll<W>() : 1;
   using V = T __attribute__((ext_vector_type(N)));
   __shared__ unsigned s_epoch, s_err;
   if (threadIdx.x == 0) {
@@ -94,27 +103,40 @@ __global__ __launch_bounds__(kDirectBlock) void direct_kernel(const DirectDesc* 
     const uint64_t nvec = (ce - cb) / N;
     const uint64_t r1 = std::min(v1, nvec);
     T* out = reinterpret_cast<T*>(d->out[rank]);
-    for (uint64_t i = v0 + threadIdx.x; i < r1; i += kDirectBlock) {
-      const uint64_t off = cb / N + i;
-      V acc;
-      if constexpr (W > 0) {
-        V v[W];
+    if constexpr (W > 0) {
+      for (uint64_t i0 = v0 + threadIdx.x; i0 < r1; i0 += U * kDirectBlock) {
+        V v[U][W];
 #pragma unroll
-        for (int p = 0; p < W; ++p) v[p] = __builtin_nontemporal_load(reinterpret_cast<const V*>(d->in[p]) + off);
-        acc = v[0];
+        for (int u = 0; u < U; ++u) {
+          const uint64_t i = i0 + static_cast<uint64_t>(u) * kDirectBlock;
+          if (i < r1)
 #pragma unroll
-        for (int p = 1; p < W; ++p)
+            for (int p = 0; p < W; ++p)
+              v[u][p] = __builtin_nontemporal_load(reinterpret_cast<const V*>(d->in[p]) + cb / N + i);
+        }
 #pragma unroll
-          for (int k = 0; k < N; ++k) acc[k] = OpT::apply(acc[k], v[p][k]);
-      } else {
-        acc = __builtin_nontemporal_load(reinterpret_cast<const V*>(d->in[0]) + off);
+        for (int u = 0; u < U; ++u) {
+          const uint64_t i = i0 + static_cast<uint64_t>(u) * kDirectBlock;
+          if (i >= r1) continue;
+          V acc = v[u][0];
+#pragma unroll
+          for (int p = 1; p < W; ++p)
+#pragma unroll
+            for (int k = 0; k < N; ++k) acc[k] = OpT::apply(acc[k], v[u][p][k]);
+          reinterpret_cast<V*>(out)[cb / N + i] = acc;
+        }
+      }
+    } else {
+      for (uint64_t i = v0 + threadIdx.x; i < r1; i += kDirectBlock) {
+        const uint64_t off = cb / N + i;
+        V acc = __builtin_nontemporal_load(reinterpret_cast<const V*>(d->in[0]) + off);
         for (int p = 1; p < world; ++p) {
           const V v = __builtin_nontemporal_load(reinterpret_cast<const V*>(d->in[p]) + off);
 #pragma unroll
           for (int k = 0; k < N; ++k) acc[k] = OpT::apply(acc[k], v[k]);
         }
+        reinterpret_cast<V*>(out)[off] = acc;
       }
-      reinterpret_cast<V*>(out)[off] = acc;
     }
     if (blockIdx.x == gridDim.x - 1) {  // sub-vector tail (last chunk only)
       for (uint64_t i = cb + nvec * N + threadIdx.x; i < ce; i += kDirectBlock) {
@@ -139,14 +161,23 @@ __global__ __launch_bounds__(kDirectBlock) void direct_kernel(const DirectDesc* 
         const uint64_t b = std::min<uint64_t>(count, p * per);
         nv[p] = p == rank ? 0 : (std::min<uint64_t>(count, b + per) - b) / N;
       }
-      for (uint64_t i = v0 + threadIdx.x; i < v1; i += kDirectBlock) {
-        V v[W];
+      for (uint64_t i0 = v0 + threadIdx.x; i0 < v1; i0 += U * kDirectBlock) {
+        V v[U][W];
 #pragma unroll
-        for (int p = 0; p < W; ++p)
-          if (i < nv[p]) v[p] = __builtin_nontemporal_load(reinterpret_cast<const V*>(d->out[p]) + p * perv + i);
+        for (int u = 0; u < U; ++u) {
+          const uint64_t i = i0 + static_cast<uint64_t>(u) * kDirectBlock;
 #pragma unroll
-        for (int p = 0; p < W; ++p)
-          if (i < nv[p]) reinterpret_cast<V*>(mine)[p * perv + i] = v[p];
+          for (int p = 0; p < W; ++p)
+            if (i < v1 && i < nv[p])
+              v[u][p] = __builtin_nontemporal_load(reinterpret_cast<const V*>(d->out[p]) + p * perv + i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint64_t i = i0 + static_cast<uint64_t>(u) * kDirectBlock;
+#pragma unroll
+          for (int p = 0; p < W; ++p)
+            if (i < v1 && i < nv[p]) reinterpret_cast<V*>(mine)[p * perv + i] = v[u][p];
+        }
       }
     } else {
       for (int p = 0; p < world; ++p) {

@@ -51,7 +51,7 @@ python: $(PYEXT)
 apps: $(APPS)
 mpi: $(MPI_APP)
 
-HEADERS := $(wildcard csrc/include/mireduce/*.hpp)
+HEADERS := $(wildcard csrc/include/mireduce/*.hpp) $(wildcard csrc/kernels/*.hpp)
 
 $(BUILD)/obj/%.o: csrc/%.hip $(HEADERS)
 	@mkdir -p $(dir $@)

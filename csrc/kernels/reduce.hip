@@ -1,521 +1,18 @@
-// Streaming reduction kernels for gfx950 (MI355X, CDNA4).
-//
-// Capability parity: the reference's block-reduction kernels sumreduce6/minreduce6/maxreduce6
-// (cuda/C/src/reduction/reduction_kernel.cu:74-253), their 20-way launch switch per (op, T)
-// (reduction_kernel.cu:263-524) and the second in-place finalisation launch
-// (reduction.cpp:344-357). Design:
-//   * one templated kernel, op functors (ops.hpp), operator identity instead of g_idata[i] (B2);
-//   * 16-byte non-temporal vector loads, UNROLL independent loads in flight per lane, grid-stride
-//     over BLOCK*UNROLL-vector tiles with 64-bit indices (B4);
-//   * wave64 butterfly (__shfl_xor over 64 lanes) instead of the 32-lane volatile tail
-//     (reduction_kernel.cu:110-122 assumes warp lockstep — wrong on CDNA), then one LDS slot per
-//     wave;
-//   * single launch: each workgroup publishes its partial write-through (sc1), drains, and takes
-//     an agent-scope ticket on one of G sharded counters; the last arriver of each group takes a
-//     ticket on the top counter and the last of those folds every partial in one parallel sc1
-//     load round (threadFenceReduction_kernel.cu:116-171 idea, but with the gfx950
-//     release/acquire forms and a sharded fan-in: one counter for 2048 arrivals costs ~25 us,
-//     eight counters ~3 us). MIREDUCE_FANIN=tree selects the older two-level fold (each group's
-//     last arriver folds and republishes its group first).
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <cstdint>
-#include <cstdlib>
-#include <cstring>
-#include <string>
-#include <vector>
-
-#include "mireduce/check.hpp"
-#include "mireduce/half.hpp"
-#include "mireduce/ops.hpp"
-#include "mireduce/vec16.hpp"
-#include "mireduce/reduce.hpp"
-#include "mireduce/xrank.hpp"
+// Streaming reduction, host side: tuned launch planner, dispatch table (filled by the
+// reduce_tab_*.hip translation units), single-/two-pass launches, bound (prepared) launches and
+// the two-pass finalize / element-wise combine kernels. The kernel templates and their design
+// notes live in reduce_kernels.hpp.
+#include "reduce_kernels.hpp"
 
 namespace mireduce {
-namespace kern {
-
-template <class OpT, class AccT>
-__device__ __forceinline__ AccT wave_reduce(AccT v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = OpT::apply(v, __shfl_xor(v, off, 64));
-  return v;
-}
-
-// Result is valid in wave 0 (all lanes). Caller must barrier before reusing `lds`.
-template <class OpT, class AccT, int BLOCK>
-__device__ __forceinline__ AccT block_reduce(AccT v, AccT* lds) {
-  constexpr int kWaves = BLOCK / 64;
-  v = wave_reduce<OpT>(v);
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  if (lane == 0) lds[wave] = v;
-  __syncthreads();
-  if (wave == 0) {
-    v = lane < kWaves ? lds[lane] : OpT::template identity<AccT>();
-    v = wave_reduce<OpT>(v);
-  }
-  return v;
-}
-
-struct Args {
-  const void* body;      // 16-byte aligned start of the vector body
-  const void* head_ptr;  // original pointer (head elements live here)
-  uint64_t head;         // scalar elements before `body`
-  uint64_t nvec;         // 16-byte vectors
-  uint64_t tail;         // scalar elements after the body
-  void* partials;        // [gridDim.x] AccT
-  void* group_partials;  // [groups] AccT
-  unsigned* tickets;     // [(groups + 1) * kTicketStride]
-  void* out;             // AccT[1]
-  int groups;            // 0: two-pass mode (write partials only)
-  int flat;              // 1: group last-arrivers only count; the final arriver folds every partial
-  int contig;            // 1: workgroup b streams one contiguous run of tiles; 0: tiles b, b+grid, ...
-  const XrankDesc* xrank;  // non-null: fold the ranks' partials in-kernel before writing out (xrank.hpp)
-  uint64_t* slots;         // non-null: polled fan-in (no tickets), [gridDim.x][2] flag-tagged words
-  int balance;             // 1 (interleaved split): whole rounds of tiles, then the leftover < grid
-                           // tiles split evenly over ALL workgroups (no one-tile tail on a few)
-};
-
-// Polled fan-in: a published partial is two 8-byte words (tag << 32 | 32 data bits); a cleared
-// slot is 0. The finisher clears every slot it consumed, so each launch starts from zeros.
-constexpr uint64_t kSlotTag = 0xA5C3E1F7ull << 32;
-constexpr int kPollSlots = 4;  // slots one finisher lane polls per round (grid <= 4 x BLOCK)
-
-template <class T>
-__device__ __forceinline__ uint64_t to_bits64(T v) {
-  if constexpr (sizeof(T) == 8) {
-    return __builtin_bit_cast(uint64_t, v);
-  } else {
-    return static_cast<uint64_t>(__builtin_bit_cast(uint32_t, v));
-  }
-}
-
-template <class T>
-__device__ __forceinline__ T from_bits64(uint64_t b) {
-  if constexpr (sizeof(T) == 8) {
-    return __builtin_bit_cast(T, b);
-  } else {
-    return __builtin_bit_cast(T, static_cast<uint32_t>(b));
-  }
-}
-
-// Cross-rank finish (xrank.hpp), run by the 64 lanes of the finishing workgroup's wave 0 with
-// this rank's partial `t` in every lane; returns the fold over all ranks in every lane.
-// Lane p pushes to rank p's mailbox and then polls slot p of its own: the world pushes leave in
-// one store round and the polls overlap. Words are (epoch << 32 | 32 data bits), written and
-// read with system-scope atomics (8-byte single-copy atomic over xGMI), so a matching epoch in
-// both words of a slot means the whole partial of this launch has landed.
-//
-// The descriptor fields a lane needs are read by xrank_prefetch: in the polled fan-in the
-// finisher is known up front and issues these loads before it waits for the other workgroups'
-// partials, so their latency (a descriptor miss, ~0.5 us at N=1) is off the critical path.
-struct XrankLane {
-  uint64_t* peer;       // rank `lane`'s mailbox (lane < world, lane != rank)
-  const uint64_t* own;  // this rank's mailbox
-  uint64_t limit;       // wait bound in wall-clock ticks (0 after a sticky error: look once)
-  unsigned e;           // this launch's epoch
-  int world, rank;
-};
-
-__device__ __forceinline__ XrankLane xrank_prefetch(const XrankDesc* d, unsigned e, unsigned err) {
-  const int lane = threadIdx.x & 63;
-  XrankLane x;
-  x.world = d->world;
-  x.rank = d->rank;
-  x.peer = d->peer_mbox[lane < kMaxXrankRanks ? lane : 0];
-  x.own = d->own_mbox;
-  x.limit = err ? 0 : d->timeout_ticks;  // a sticky error means a peer is gone: do not wait
-  x.e = e;
-  return x;
-}
-
-template <class OpT, class AccT>
-__device__ __forceinline__ AccT xrank_finish(const XrankDesc* d, const XrankLane& x, AccT t) {
-  const int lane = threadIdx.x & 63;
-  const unsigned e = x.e;
-  const uint64_t parity = static_cast<uint64_t>(e & 1u) * kMaxXrankRanks;
-  const uint64_t tag = static_cast<uint64_t>(e) << 32;
-  const uint64_t bits = to_bits64(t);
-  AccT v = OpT::template identity<AccT>();
-  if (lane < x.world && lane != x.rank) {
-    uint64_t* dst = x.peer + (parity + x.rank) * 2;
-    __hip_atomic_store(dst, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(dst + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint64_t* src = x.own + (parity + lane) * 2;
-    const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
-    for (;;) {
-      const uint64_t lo = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      const uint64_t hi = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if ((lo >> 32) == e && (hi >> 32) == e) {
-        v = from_bits64<AccT>((lo & 0xffffffffull) | (hi << 32));
-        break;
-      }
-      if (static_cast<uint64_t>(wall_clock64()) - t0 > x.limit) {
-        __hip_atomic_fetch_or(d->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  } else if (lane == x.rank) {
-    v = t;  // this rank's own partial never leaves the register file
-  }
-  if (lane == 0) __hip_atomic_store(d->epoch, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return wave_reduce<OpT>(v);
-}
-
-template <class V, int BLOCK, int UNROLL, bool NT>
-__device__ __forceinline__ void load_tile(V (&v)[UNROLL], const V* p) {
-#pragma unroll
-  for (int u = 0; u < UNROLL; ++u) {
-    if constexpr (NT) v[u] = __builtin_nontemporal_load(p + u * BLOCK);
-    else v[u] = p[u * BLOCK];
-  }
-}
-
-template <class OpT, class T, class AccT, class V, int N, int UNROLL>
-__device__ __forceinline__ void consume_tile(AccT (&acc)[UNROLL], const V (&v)[UNROLL]) {
-#pragma unroll
-  for (int u = 0; u < UNROLL; ++u) {
-#pragma unroll
-    for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(v[u], k)));
-  }
-}
-
-// PIPE: software-pipelined body — tile t+grid's loads are issued before tile t is consumed, so
-// a wave always has UNROLL loads in flight while it computes (two register sets). The loop has
-// no per-load condition (the last tile is peeled), see cdna_hip_programming.md §5 trap (c).
-template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT, bool PIPE>
-__global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
-  using V = typename Vec16<T>::type;
-  constexpr int N = Vec16<T>::N;
-  __shared__ AccT lds[BLOCK / 64];
-  __shared__ int is_last;
-
-  AccT acc[UNROLL];
-#pragma unroll
-  for (int u = 0; u < UNROLL; ++u) acc[u] = OpT::template identity<AccT>();
-
-  const V* __restrict__ vin = static_cast<const V*>(a.body);
-  constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
-  const uint64_t ntiles = a.nvec / kTile;
-  // This workgroup's full tiles: t0, t0 + step, ... < t1 (interleaved over the grid, or one
-  // contiguous run of ntiles / grid tiles each).
-  const uint64_t grid = gridDim.x;
-  const bool balanced = a.balance && !a.contig;
-  const uint64_t full = balanced ? ntiles / grid * grid : ntiles;  // tiles streamed in whole rounds
-  const uint64_t t0 = a.contig ? blockIdx.x * ntiles / grid : blockIdx.x;
-  const uint64_t t1 = a.contig ? (blockIdx.x + 1) * ntiles / grid : full;
-  const uint64_t step = a.contig ? 1 : grid;
-  if constexpr (PIPE) {
-    if (t0 < t1) {
-      V cur[UNROLL];
-      load_tile<V, BLOCK, UNROLL, NT>(cur, vin + t0 * kTile + threadIdx.x);
-      for (uint64_t tn = t0 + step; tn < t1; tn += step) {
-        V nxt[UNROLL];
-        load_tile<V, BLOCK, UNROLL, NT>(nxt, vin + tn * kTile + threadIdx.x);
-        consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, cur);
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) cur[u] = nxt[u];
-      }
-      consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, cur);
-    }
-  } else {
-    for (uint64_t t = t0; t < t1; t += step) {
-      V v[UNROLL];
-      load_tile<V, BLOCK, UNROLL, NT>(v, vin + t * kTile + threadIdx.x);
-      consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, v);
-    }
-  }
-  if (balanced) {
-    // The leftover after the whole rounds (< grid tiles + the sub-tile remainder) as one even,
-    // contiguous piece per workgroup (< one tile each): every load issued unconditionally (an
-    // out-of-piece lane re-reads its piece's first vector and discards it), so no per-load branch
-    // serialises the wave (cdna_hip_programming.md §5 trap (c)).
-    const uint64_t l0 = full * kTile, left = a.nvec - l0;
-    const uint64_t s0 = l0 + left * blockIdx.x / grid, s1 = l0 + left * (blockIdx.x + 1) / grid;
-    for (uint64_t base = s0 + threadIdx.x; base < s1; base += kTile) {
-      V v[UNROLL];
-      bool ok[UNROLL];
-#pragma unroll
-      for (int u = 0; u < UNROLL; ++u) {
-        const uint64_t idx = base + static_cast<uint64_t>(u) * BLOCK;
-        ok[u] = idx < s1;
-        const V* p = vin + (ok[u] ? idx : base);
-        if constexpr (NT) v[u] = __builtin_nontemporal_load(p);
-        else v[u] = *p;
-      }
-#pragma unroll
-      for (int u = 0; u < UNROLL; ++u) {
-        if (ok[u]) {
-#pragma unroll
-          for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(v[u], k)));
-        }
-      }
-    }
-  } else {
-    // Vectors past the last full tile, grid-strided.
-    for (uint64_t i = ntiles * kTile + static_cast<uint64_t>(blockIdx.x) * BLOCK + threadIdx.x;
-         i < a.nvec; i += static_cast<uint64_t>(gridDim.x) * BLOCK) {
-      const V v = vin[i];
-#pragma unroll
-      for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], OpT::pre(elem<T, AccT>(v, k)));
-    }
-  }
-  // Unaligned head and sub-vector tail (< N elements each), folded by the last workgroup.
-  if (blockIdx.x == gridDim.x - 1) {
-    const T* hp = static_cast<const T*>(a.head_ptr);
-    if (threadIdx.x < a.head) acc[0] = OpT::apply(acc[0], OpT::pre(static_cast<AccT>(hp[threadIdx.x])));
-    const T* tp = static_cast<const T*>(a.body) + a.nvec * N;
-    if (threadIdx.x < a.tail) acc[0] = OpT::apply(acc[0], OpT::pre(static_cast<AccT>(tp[threadIdx.x])));
-  }
-#pragma unroll
-  for (int u = 1; u < UNROLL; ++u) acc[0] = OpT::apply(acc[0], acc[u]);
-
-  // Fused cross-rank finish: this launch's epoch (counter + 1; only the finishing workgroup bumps
-  // the counter, and it runs last) and the sticky error word, loaded by every workgroup after its
-  // streaming body (not before: extra live values there change hipcc's load scheduling of the
-  // body — 76 -> 60 VGPRs and 7.3 -> 5.1 TB/s at 512 x 16) so the finisher pays no atomic round trip.
-  unsigned xr_epoch = 0, xr_err = 0;
-  if (a.xrank) {
-    xr_epoch = __hip_atomic_load(a.xrank->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    xr_err = __hip_atomic_load(a.xrank->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-
-  AccT v = block_reduce<OpT, AccT, BLOCK>(acc[0], lds);
-  AccT* partials = static_cast<AccT*>(a.partials);
-  if (a.groups == 0) {  // two-pass mode: the finalize kernel (kernel boundary) reads these
-    if (threadIdx.x == 0) partials[blockIdx.x] = v;
-    return;
-  }
-
-  // ---- one workgroup (small n): it is the last arriver by construction — no partial publish,
-  //      no tickets, no second load round.
-  if (gridDim.x == 1) {
-    if (threadIdx.x < 64) {
-      if (a.xrank) v = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), v);
-      if (threadIdx.x == 0) *static_cast<AccT*>(a.out) = v;
-    }
-    return;
-  }
-
-  // ---- polled fan-in (default): no tickets, no publish-then-drain wait. Every workgroup stores
-  // its partial as two tagged words (the data carries its own validity, as in the cross-rank
-  // mailbox) and exits; the last-indexed workgroup — with interleaved tiles one of the first to
-  // run out of work — polls all slots, folds them in slot order (deterministic), clears them and
-  // finishes. The finisher's path after the last partial lands is one store + one poll round,
-  // instead of store, drain, ticket (x2) and a load round. Slots live in uncached memory, so
-  // polls always see the other XCDs' stores.
-  if (a.slots) {
-    if (threadIdx.x == 0) {
-      const uint64_t bits = to_bits64(v);
-      uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(blockIdx.x);
-      __hip_atomic_store(sl, kSlotTag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(sl + 1, kSlotTag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (blockIdx.x != gridDim.x - 1) return;
-    // The finisher: start the cross-rank descriptor loads now, they land while it polls.
-    XrankLane xl{};
-    if (a.xrank && threadIdx.x < 64) xl = xrank_prefetch(a.xrank, xr_epoch, xr_err);
-    AccT t = OpT::template identity<AccT>();
-    // Bounded like every device-side wait here (all workgroups of this launch always publish, so
-    // the bound is never reached by a correct launch; it only keeps a misuse from hanging the GPU).
-    const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
-    constexpr uint64_t kBound = 1ull << 30;  // ~10 s of the 100 MHz wall clock
-    if (gridDim.x <= kPollSlots * BLOCK) {
-      // Each lane polls ALL its slots (<= kPollSlots) every round, so the finish costs one poll
-      // round trip after the last store lands, not one per slot.
-      uint64_t lo[kPollSlots], hi[kPollSlots];
-      unsigned pending = 0;
-#pragma unroll
-      for (int k = 0; k < kPollSlots; ++k)
-        if (threadIdx.x + k * BLOCK < gridDim.x) pending |= 1u << k;
-      while (pending) {
-#pragma unroll
-        for (int k = 0; k < kPollSlots; ++k) {
-          if (pending & (1u << k)) {
-            const uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(threadIdx.x + k * BLOCK);
-            lo[k] = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            hi[k] = __hip_atomic_load(sl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < kPollSlots; ++k)
-          if ((pending & (1u << k)) && (lo[k] & ~0xffffffffull) == kSlotTag && (hi[k] & ~0xffffffffull) == kSlotTag)
-            pending &= ~(1u << k);
-        if (!pending || static_cast<uint64_t>(wall_clock64()) - t0 > kBound) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-#pragma unroll
-      for (int k = 0; k < kPollSlots; ++k) {  // fold in slot order (deterministic), then clear
-        if (threadIdx.x + k * BLOCK < gridDim.x) {
-          t = OpT::apply(t, from_bits64<AccT>((lo[k] & 0xffffffffull) | (hi[k] << 32)));
-          uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(threadIdx.x + k * BLOCK);
-          __hip_atomic_store(sl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(sl + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    } else {  // very large grids (user --maxblocks / wg-per-cu): slot by slot
-      for (unsigned i = threadIdx.x; i < gridDim.x; i += BLOCK) {
-        uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(i);
-        uint64_t l, h;
-        for (;;) {
-          l = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          h = __hip_atomic_load(sl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((l & ~0xffffffffull) == kSlotTag && (h & ~0xffffffffull) == kSlotTag) break;
-          if (static_cast<uint64_t>(wall_clock64()) - t0 > kBound) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        t = OpT::apply(t, from_bits64<AccT>((l & 0xffffffffull) | (h << 32)));
-        __hip_atomic_store(sl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(sl + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    t = block_reduce<OpT, AccT, BLOCK>(t, lds);
-    if (threadIdx.x < 64) {
-      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xl, t);
-      if (threadIdx.x == 0) *static_cast<AccT*>(a.out) = t;
-    }
-    return;
-  }
-
-  // ---- ticketed finalisation (MIREDUCE_FANIN=flat|tree; cdna_hip_programming.md §6 G16, sc1 form)
-  // Ordering rests on the gfx950 code hipcc emits for these relaxed agent-scope atomics (the full
-  // acq_rel form would add an L2 write-back per arrival). Generated for <SumOp,double,512,16,nt>
-  // and pinned by tests/test_isa_ordering.py:
-  //   global_store_dwordx2 v4, v[2:3], s[30:31] sc1     ; partial, write-through past L2
-  //   s_waitcnt vmcnt(0)                                ; ... acknowledged before
-  //   global_atomic_add v6, v4, v6, s[34:35] sc0        ; the (returning) ticket
-  //   s_barrier                                         ; is_last broadcast
-  //   global_load_dwordx2 v[8:9], v[8:9], off sc1       ; last arriver reads partials past L1
-  const unsigned G = static_cast<unsigned>(a.groups);
-  const unsigned g = blockIdx.x % G;  // group label only; correctness is placement-independent
-  if (threadIdx.x == 0) {
-    store_sc1(&partials[blockIdx.x], v);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned members = gridDim.x / G + (g < gridDim.x % G ? 1u : 0u);
-    const unsigned prev = __hip_atomic_fetch_add(&a.tickets[g * kTicketStride], 1u,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = (prev == members - 1);
-  }
-  __syncthreads();
-  if (!is_last) return;
-
-  if (a.flat) {
-    // Flat fan-in: the group's last arriver only takes a ticket on the top counter; the last of
-    // those folds all gridDim.x partials at once (one parallel sc1 load round instead of a
-    // group fold + group-partial publish + second fold: two memory round trips shorter).
-    // (One group — small grids — has no top counter: its last arriver is the finisher.)
-    if (G > 1) {
-      if (threadIdx.x == 0) {
-        __hip_atomic_store(&a.tickets[g * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned prev = __hip_atomic_fetch_add(&a.tickets[G * kTicketStride], 1u,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        is_last = (prev == G - 1);
-      }
-      __syncthreads();
-      if (!is_last) return;
-    }
-    AccT t = OpT::template identity<AccT>();
-    for (unsigned i = threadIdx.x; i < gridDim.x; i += BLOCK) t = OpT::apply(t, load_sc1(&partials[i]));
-    t = block_reduce<OpT, AccT, BLOCK>(t, lds);
-    if (threadIdx.x < 64) {
-      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), t);
-      if (threadIdx.x == 0) {
-        *static_cast<AccT*>(a.out) = t;
-        // reset: the top counter, or (one group) the group counter itself
-        __hip_atomic_store(&a.tickets[(G > 1 ? G : 0) * kTicketStride], 0u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    return;
-  }
-
-  // Last arriver of group g: fold partials g, g+G, g+2G, ... (sc1 loads: L1 never holds them).
-  AccT s = OpT::template identity<AccT>();
-  for (unsigned i = g + threadIdx.x * G; i < gridDim.x; i += BLOCK * G)
-    s = OpT::apply(s, load_sc1(&partials[i]));
-  s = block_reduce<OpT, AccT, BLOCK>(s, lds);
-  AccT* gpart = static_cast<AccT*>(a.group_partials);
-  if (threadIdx.x == 0) {
-    store_sc1(&gpart[g], s);
-    __hip_atomic_store(&a.tickets[g * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(&a.tickets[G * kTicketStride], 1u,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = (prev == G - 1);
-  }
-  __syncthreads();
-  if (!is_last) return;
-
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    AccT t = lane < static_cast<int>(G) ? load_sc1(&gpart[lane]) : OpT::template identity<AccT>();
-    t = wave_reduce<OpT>(t);
-    if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), t);
-    if (lane == 0) {
-      *static_cast<AccT*>(a.out) = t;
-      __hip_atomic_store(&a.tickets[G * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// Second level of the two-pass path (and the on-device fold for reduce_finalize): one
-// workgroup folds `count` values. Launched after a kernel boundary, so plain loads are fine.
-template <class OpT, class AccT>
-__global__ __launch_bounds__(256) void finalize(const AccT* __restrict__ partials, uint64_t count,
-                                                AccT* __restrict__ out) {
-  __shared__ AccT lds[4];
-  AccT s = OpT::template identity<AccT>();
-  for (uint64_t i = threadIdx.x; i < count; i += 256) s = OpT::apply(s, partials[i]);
-  s = block_reduce<OpT, AccT, 256>(s, lds);
-  if (threadIdx.x == 0) *out = s;
-}
-
-template <class OpT, class T>
-__global__ __launch_bounds__(256) void combine(T* __restrict__ inout, const T* __restrict__ other,
-                                               uint64_t n) {
-  using V = typename Vec16<T>::type;
-  constexpr int N = Vec16<T>::N;
-  const uint64_t nvec = n / N;
-  V* vio = reinterpret_cast<V*>(inout);
-  const V* vo = reinterpret_cast<const V*>(other);
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; i < nvec; i += stride) {
-    V x = __builtin_nontemporal_load(vio + i);
-    const V y = __builtin_nontemporal_load(vo + i);
-#pragma unroll
-    for (int k = 0; k < N; ++k) x[k] = OpT::apply(x[k], y[k]);
-    __builtin_nontemporal_store(x, vio + i);
-  }
-  const uint64_t rem = n - nvec * N;
-  if (blockIdx.x == 0 && threadIdx.x < rem) {
-    const uint64_t i = nvec * N + threadIdx.x;
-    inout[i] = OpT::apply(inout[i], other[i]);
-  }
-}
-
-}  // namespace kern
 
 // ----------------------------------------------------------------------------------------------
 // Host-side dispatch: a table keyed by (op, dtype, acc, block, unroll, policy) replaces the
-// reference's runtime switch over 20 template instantiations per (op, T).
+// reference's runtime switch over 20 template instantiations per (op, T) (reduce_kernels.hpp).
 // ----------------------------------------------------------------------------------------------
 namespace {
 
-using LaunchFn = void (*)(const kern::Args&, int grid, hipStream_t);
-
-template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT, bool PIPE>
-void launch_stream(const kern::Args& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((kern::reduce_stream<OpT, T, AccT, BLOCK, UNROLL, NT, PIPE>), dim3(grid), dim3(BLOCK),
-                     0, s, a);
-}
-
-constexpr int kBlocks[] = {256, 512, 1024};
-constexpr int kUnrolls[] = {2, 4, 8, 16};
-constexpr int kNumBlocks = 3;
-constexpr int kNumUnrolls = 4;
+using namespace detail;
 
 int block_index(int b) { return b == 256 ? 0 : (b == 512 ? 1 : (b == 1024 ? 2 : -1)); }
 int unroll_index(int u) { return u == 2 ? 0 : (u == 4 ? 1 : (u == 8 ? 2 : (u == 16 ? 3 : -1))); }
@@ -559,74 +56,17 @@ int combo_index(Op op, DType t, DType acc) {
   }
   return -1;
 }
-constexpr int kCombos = 29;
-
-struct Table {
-  LaunchFn fn[kCombos][kNumBlocks][kNumUnrolls][2][2];  // [..][policy nt][pipelined]
-};
-
-// Pipelined variants need two register sets of UNROLL 16-byte vectors: only where the
-// per-SIMD register budget allows it (BLOCK * UNROLL <= 8192); elsewhere the plain body.
-constexpr bool pipe_ok(int b, int u) { return b * u <= 8192; }
-
-template <class OpT, class T, class AccT, int BI, int UI>
-void fill_one(Table& tb, int c) {
-  constexpr int B = kBlocks[BI];
-  constexpr int U = kUnrolls[UI];
-  constexpr bool P = pipe_ok(B, U);
-  tb.fn[c][BI][UI][0][0] = launch_stream<OpT, T, AccT, B, U, false, false>;
-  tb.fn[c][BI][UI][1][0] = launch_stream<OpT, T, AccT, B, U, true, false>;
-  tb.fn[c][BI][UI][0][1] = launch_stream<OpT, T, AccT, B, U, false, P>;
-  tb.fn[c][BI][UI][1][1] = launch_stream<OpT, T, AccT, B, U, true, P>;
-}
-
-template <class OpT, class T, class AccT, int BI>
-void fill_block(Table& tb, int c) {
-  fill_one<OpT, T, AccT, BI, 0>(tb, c);
-  fill_one<OpT, T, AccT, BI, 1>(tb, c);
-  fill_one<OpT, T, AccT, BI, 2>(tb, c);
-  fill_one<OpT, T, AccT, BI, 3>(tb, c);
-}
-
-template <class OpT, class T, class AccT>
-void fill_combo(Table& tb, int c) {
-  fill_block<OpT, T, AccT, 0>(tb, c);
-  fill_block<OpT, T, AccT, 1>(tb, c);
-  fill_block<OpT, T, AccT, 2>(tb, c);
-}
-
 const Table& table() {
   static const Table tb = [] {
     Table t{};
-    fill_combo<SumOp, int32_t, int64_t>(t, 0);
-    fill_combo<SumOp, int32_t, int32_t>(t, 1);
-    fill_combo<MinOp, int32_t, int32_t>(t, 2);
-    fill_combo<MaxOp, int32_t, int32_t>(t, 3);
-    fill_combo<SumOp, int64_t, int64_t>(t, 4);
-    fill_combo<MinOp, int64_t, int64_t>(t, 5);
-    fill_combo<MaxOp, int64_t, int64_t>(t, 6);
-    fill_combo<SumOp, float, double>(t, 7);
-    fill_combo<SumOp, float, float>(t, 8);
-    fill_combo<MinOp, float, float>(t, 9);
-    fill_combo<MaxOp, float, float>(t, 10);
-    fill_combo<SumOp, double, double>(t, 11);
-    fill_combo<MinOp, double, double>(t, 12);
-    fill_combo<MaxOp, double, double>(t, 13);
-    fill_combo<SumOp, bf16_t, float>(t, 14);
-    fill_combo<MinOp, bf16_t, float>(t, 15);
-    fill_combo<MaxOp, bf16_t, float>(t, 16);
-    fill_combo<SumOp, f16_t, float>(t, 17);
-    fill_combo<MinOp, f16_t, float>(t, 18);
-    fill_combo<MaxOp, f16_t, float>(t, 19);
-    fill_combo<SumSqOp, float, double>(t, 20);
-    fill_combo<SumSqOp, float, float>(t, 21);
-    fill_combo<SumSqOp, double, double>(t, 22);
-    fill_combo<SumSqOp, bf16_t, float>(t, 23);
-    fill_combo<SumSqOp, f16_t, float>(t, 24);
-    fill_combo<AbsMaxOp, float, float>(t, 25);
-    fill_combo<AbsMaxOp, double, double>(t, 26);
-    fill_combo<AbsMaxOp, bf16_t, float>(t, 27);
-    fill_combo<AbsMaxOp, f16_t, float>(t, 28);
+    fill_table_int32(t);
+    fill_table_int64(t);
+    fill_table_f32(t);
+    fill_table_f64(t);
+    fill_table_bf16(t);
+    fill_table_f16(t);
+    fill_table_sumsq(t);
+    fill_table_absmax(t);
     return t;
   }();
   return tb;

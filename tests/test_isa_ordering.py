@@ -45,7 +45,7 @@ def _first(ins, pattern, start=0):
 def test_ticketed_fanin_publish_then_ticket_then_consume(tmp_path):
     # MIREDUCE_FANIN=flat|tree: partial stored write-through (sc1), drained, THEN the returning
     # ticket; after the barrier that broadcasts is_last, partials are read L1-bypassing (sc1).
-    ins = _disasm(tmp_path, "reduce.o", STREAM_F64)
+    ins = _disasm(tmp_path, "reduce_tab_f64.o", STREAM_F64)
     ok = False
     for i, ln in enumerate(ins):
         if not re.search(r"^global_store_dwordx2 .* sc1$", ln):
@@ -65,7 +65,7 @@ def test_ticketed_fanin_publish_then_ticket_then_consume(tmp_path):
 def test_polled_fanin_tagged_slots(tmp_path):
     # default fan-in: two tagged 8-byte words stored per workgroup (no drain, no ticket); the
     # finisher polls both words of a slot (sc1 loads) with a bounded, sleeping loop and clears them.
-    ins = _disasm(tmp_path, "reduce.o", STREAM_F64)
+    ins = _disasm(tmp_path, "reduce_tab_f64.o", STREAM_F64)
     st = _first(ins, r"^global_store_dwordx2 .* sc1$")
     assert st is not None and re.search(r"offset:8 sc1$", ins[st + 1] if st + 1 < len(ins) else "") or \
         _first(ins, r"^global_store_dwordx2 .* offset:8 sc1$", st) is not None
@@ -77,7 +77,7 @@ def test_polled_fanin_tagged_slots(tmp_path):
 
 
 def test_xrank_exchange_is_system_scope(tmp_path):
-    ins = _disasm(tmp_path, "reduce.o", STREAM_F64)
+    ins = _disasm(tmp_path, "reduce_tab_f64.o", STREAM_F64)
     # fused cross-rank finish: mailbox words stored and polled at system scope (sc0 sc1), bounded
     st = _first(ins, r"^flat_store_dwordx2 .* sc0 sc1$")
     ld = _first(ins, r"^flat_load_dwordx2 .* sc0 sc1$", st or 0)
@@ -113,4 +113,4 @@ def _vgpr_count(tmp_path, obj: str, symbol: str) -> int:
 def test_headline_kernel_keeps_its_loads_in_flight(tmp_path):
     # 512 x 16 f64 (the >= 3 GB plan): 16 independent 16-byte loads per lane need >= 64 VGPRs.
     # A change that made hipcc re-schedule the body onto 60 VGPRs cost 30 % (7.3 -> 5.1 TB/s).
-    assert _vgpr_count(tmp_path, "reduce.o", STREAM_F64) >= 64
+    assert _vgpr_count(tmp_path, "reduce_tab_f64.o", STREAM_F64) >= 64

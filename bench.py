@@ -216,11 +216,20 @@ def run_vector(args, ctx, cfg, fault) -> int:
     return 0 if verified in (None, True) else 1
 
 
+REDUCE_C_OPS = ("max", "min", "sum")  # reduce.c's operations[] order = its output row order (reduce.c:26-28)
+
+
 def _vector_extras(ctx, steps: int = 5) -> dict:
-    """reduce.c's own measurement on this job's GPUs, next to the scalar headline: element-wise
-    DOUBLE SUM of 2 GiB of total data (NUM_DOUBLES, mpi/constants.h:2) to root 0 (MPI_Reduce,
-    reduce.c:90) and to every rank, over RCCL and over the direct one-kernel collective; RETRY_COUNT
-    (5) timed collectives each; GiB/s of total data (reduce.c:93). Errors are recorded, not raised."""
+    """reduce.c's own measurement on this job's GPUs, next to the scalar headline. Its whole table:
+    element-wise INT and DOUBLE MAX / MIN / SUM of 2 GiB of total data each (NUM_INTS / NUM_DOUBLES,
+    mpi/constants.h:1-2) to root 0 (MPI_Reduce, reduce.c:76,90), over RCCL and over the direct
+    one-kernel collective, plus DOUBLE SUM to every rank (all-reduce); RETRY_COUNT (5) timed
+    collectives each; GiB/s of total data (reduce.c:79,93).
+
+    ``reduce_<impl>`` / ``allreduce_<impl>``: DOUBLE SUM; ``table``: one entry per (dtype, op, impl)
+    in reduce.c's row order, and ``rows``: the same as reduce.c's ``"%s %s %d %10.3lf"`` output
+    lines (DATATYPE OP NODES GB/sec, reduce.c:81,95; ``impl`` selects the file in
+    tools/scaling.py's results/vector_<impl>/<DT>_<OP>.txt). Errors are recorded, not raised."""
     from dataclasses import replace as _replace
 
     from cuda_mpi_reductions_amd.models import CONFIGS as _C, VectorReduction
@@ -229,20 +238,45 @@ def _vector_extras(ctx, steps: int = 5) -> dict:
     # (gloo rehearsals: its GPU-tensor reduce / all_reduce is not RCCL and crashes on 1 GiB
     # tensors, so only the direct collective runs there)
     impls = ("rccl", "direct") if ctx.backend == "nccl" else ("direct",)
-    for collective in ("reduce", "allreduce"):
-        cfg = _replace(_C["xgmi_2g_double_sum_reduce"], collective=collective)
+    table = []
+
+    def timed(wl):
+        el, ok = _time_vector(wl, ctx, steps, 1, None, True)
+        return {"gibps": round(wl.bytes_total * steps / el / float(1 << 30), 3),
+                "ms": round(el / steps * 1e3, 4), "verified": ok}
+
+    for base, dt in (("xgmi_2g_int_sum_reduce", "INT"), ("xgmi_2g_double_sum_reduce", "DOUBLE")):
         for impl in impls:
-            key = f"{collective}_{impl}"
-            try:
-                wl = VectorReduction(cfg, ctx, impl=impl, direct_timeout_s=5.0).setup()
-                el, ok = _time_vector(wl, ctx, steps, 1, None, True)
-                out[key] = {"gibps": round(wl.bytes_total * steps / el / float(1 << 30), 3),
-                            "ms": round(el / steps * 1e3, 4), "verified": ok}
+            wl = None
+            try:  # one registration per (dtype, impl); the operator / collective only change the launch
+                wl = VectorReduction(_C[base], ctx, impl=impl, direct_timeout_s=5.0).setup()
+                for op in REDUCE_C_OPS:
+                    wl.cfg = _replace(_C[base], op=op)
+                    r = timed(wl)
+                    table.append({"dtype": dt, "op": op.upper(), "impl": impl, **r})
+                    if dt == "DOUBLE" and op == "sum":
+                        out[f"reduce_{impl}"] = r
+                if dt == "DOUBLE":
+                    wl.cfg = _replace(_C[base], collective="allreduce")
+                    out[f"allreduce_{impl}"] = timed(wl)
+            except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
+                err = {"error": f"{type(e).__name__}: {e}"[:200]}
+                done = {(t["dtype"], t["op"]) for t in table if t["impl"] == impl}
+                table += [{"dtype": dt, "op": op.upper(), "impl": impl, **err} for op in REDUCE_C_OPS
+                          if (dt, op.upper()) not in done]
+                if dt == "DOUBLE":
+                    out.setdefault(f"reduce_{impl}", err)
+                    out.setdefault(f"allreduce_{impl}", err)
+            if wl is not None:
                 wl.close()  # collective: the next registration may reuse these addresses
                 del wl
-            except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
-                out[key] = {"error": f"{type(e).__name__}: {e}"[:200]}
             torch.cuda.empty_cache()
+    out["table"] = table
+    if ctx.world_size == 1:
+        out["note"] = ("world 1: RCCL enqueues no work for a 1-rank in-place reduce (its GiB/s is the host "
+                       "round trip only); direct is one local in -> out pass; cross-GPU numbers need N > 1")
+    out["rows"] = ["%s %s %d %10.3lf" % (t["dtype"], t["op"], ctx.world_size, t["gibps"]) + f"  # {t['impl']}"
+                   for t in table if "gibps" in t]
     if ctx.world_size > 1:
         out["peer_read"] = _peer_read_extra(ctx)
     return out

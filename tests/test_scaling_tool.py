@@ -55,3 +55,27 @@ def test_cli_without_results_fails(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling.py"), str(empty),
                         "--out", str(tmp_path / "o")], capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "no bench.py results" in r.stderr
+
+
+def test_reduce_c_vector_table_becomes_results_files(tmp_path):
+    # bench.py's reduce_c_vector.table (reduce.c's INT/DOUBLE x MAX/MIN/SUM) per N -> one getAvgs-format
+    # file per (impl, DATATYPE, OP), the counterpart of the reference's mpi/results/<DT>_<OP>.txt.
+    def with_table(n, scale):
+        d = _line(n, 7300.0 * n, 8.0 / (7.3 * n))
+        d["reduce_c_vector"] = {"table": [
+            {"dtype": dt, "op": op, "impl": impl, "gibps": scale * n * (2 if impl == "direct" else 1)}
+            for dt in ("INT", "DOUBLE") for op in ("MAX", "MIN", "SUM") for impl in ("rccl", "direct")]
+            + [{"dtype": "INT", "op": "SUM", "impl": "rccl", "error": "RuntimeError: x"}]}
+        return d
+    src = tmp_path / "scale.jsonl"
+    src.write_text("\n".join(json.dumps(with_table(n, s)) for n in (1, 2, 8) for s in (100.0, 300.0)) + "\n")
+    out = tmp_path / "res"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling.py"), str(src), "--out", str(out)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    rows = (out / "vector_rccl" / "INT_SUM.txt").read_text().split("\n")
+    assert rows[0] == "" and rows[1:4] == ["INT SUM 1 200.00000", "INT SUM 2 400.00000", "INT SUM 8 1600.00000"]
+    assert (out / "vector_direct" / "DOUBLE_MAX.txt").read_text().split("\n")[3] == "DOUBLE MAX 8 3200.00000"
+    assert "| direct | DOUBLE | MIN | 2 | 800.000 | 2 |" in (out / "vector.md").read_text()
+    import plot
+    assert [n for n, _ in plot.read_results(str(out / "vector_rccl" / "DOUBLE_MIN.txt"))] == [1, 2, 8]

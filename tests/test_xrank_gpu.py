@@ -208,6 +208,12 @@ def test_bench_vector_extras_in_headline(tmp_path):
     for k in ("reduce_rccl", "reduce_direct", "allreduce_rccl", "allreduce_direct"):
         assert ex[k].get("verified") is True and ex[k]["gibps"] > 0, (k, ex[k])
     assert "peer_read" not in ex  # one rank: no peers to read
+    # reduce.c's whole table (INT / DOUBLE x MAX / MIN / SUM to root 0) over both implementations
+    tab = ex["table"]
+    assert [(t["dtype"], t["op"]) for t in tab if t["impl"] == "rccl"] == \
+        [(dt, op) for dt in ("INT", "DOUBLE") for op in ("MAX", "MIN", "SUM")]
+    assert len(tab) == 12 and all(t.get("verified") is True and t["gibps"] > 0 for t in tab), tab
+    assert ex["rows"][0].startswith("INT MAX 1 ") and len(ex["rows"]) == 12
 
 
 def test_bench_fused_corrupt_rank_fails_verification(tmp_path, monkeypatch):
@@ -248,6 +254,7 @@ def test_bench_eight_ranks_auto_on_one_gpu(tmp_path, monkeypatch):
     assert "auto" in d["config"]["collective"] and "reduce_c_vector" in d
     ex = d["reduce_c_vector"]
     assert ex["reduce_direct"].get("verified") is True, ex
+    assert len(ex["table"]) == 6 and all(t.get("verified") is True for t in ex["table"]), ex["table"]
     pr = ex["peer_read"]  # fabric probe: 8 ranks reading each other's buffers (here all on one GPU)
     assert "error" not in pr and 0 < pr["ingress_gbps_min"] <= pr["ingress_gbps_max"] and pr["node_gbps"] > 0, pr
 

@@ -10,7 +10,12 @@ or any JSON document holding such objects, e.g. the driver's scaling file), grou
 
 * ``<out>/<DT>_<OP>.txt``      rows ``DOUBLE SUM <N> <GB/s>`` (GB = 1e9 B, bench.py's unit),
                                readable by tools/plot.py and tools/makePlots.gp unchanged;
-* ``<out>/scaling.md``         N, GB/s, ms/step, speed-up over N=1 and efficiency.
+* ``<out>/scaling.md``         N, GB/s, ms/step, speed-up over N=1 and efficiency;
+* ``<out>/vector_<impl>/<DT>_<OP>.txt``  reduce.c's own table from the north-star runs'
+                               ``reduce_c_vector.table`` (INT / DOUBLE x MAX / MIN / SUM element-wise
+                               to root 0, GiB/s of total data, impl = rccl | direct), averaged per N
+                               like getAvgs.sh: the counterpart of mpi/results/<DT>_<OP>.txt, plus
+                               ``<out>/vector.md``.
 
 Efficiency = value(N) / (N * value(1)): the whole-node bandwidth of N GPUs against N copies of the
 1-GPU run (bench.py's headline is strong scaling, so this is also t(1) / (N * t(N))).
@@ -84,6 +89,38 @@ def summarise(results):
     return out
 
 
+def summarise_vector(results):
+    """{(impl, DT, OP): {N: {"gibps": mean, "runs": k}}} from every result's reduce_c_vector.table
+    (entries with an error are skipped)."""
+    acc = defaultdict(lambda: defaultdict(list))
+    for r in results:
+        for row in ((r.get("reduce_c_vector") or {}).get("table") or []):
+            if row.get("gibps") is None:
+                continue
+            acc[(row["impl"], row["dtype"], row["op"])][int(r["n_gpus"])].append(float(row["gibps"]))
+    return {k: {n: {"gibps": sum(v) / len(v), "runs": len(v)} for n, v in sorted(per_n.items())}
+            for k, per_n in acc.items()}
+
+
+def write_vector(vsummary, out_dir):
+    """results/vector_<impl>/<DT>_<OP>.txt (getAvgs.sh format) and vector.md; returns the markdown."""
+    md = ["| impl | DATATYPE | OP | N | GiB/s (total data) | runs |", "|---|---|---|---|---|---|"]
+    for (impl, dt, op), per_n in sorted(vsummary.items()):
+        d = os.path.join(out_dir, f"vector_{impl}")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"{dt}_{op}.txt"), "w") as f:
+            f.write("\n")
+            for n, v in per_n.items():
+                f.write(f"{dt} {op} {n} {v['gibps']:.5f}\n")
+        for n, v in per_n.items():
+            md.append(f"| {impl} | {dt} | {op} | {n} | {v['gibps']:.3f} | {v['runs']} |")
+    text = "\n".join(md) + "\n"
+    if vsummary:
+        with open(os.path.join(out_dir, "vector.md"), "w") as f:
+            f.write(text)
+    return text
+
+
 def efficiency(per_n):
     """{N: (speed-up over N=1, efficiency)}; None where there is no N=1 point."""
     base = per_n.get(1, {}).get("gbps")
@@ -129,6 +166,9 @@ def main(argv=None):
         print("[scaling] no bench.py results found", file=sys.stderr)
         return 1
     print(write(summarise(results), a.out), end="")
+    vs = summarise_vector(results)
+    if vs:
+        print(write_vector(vs, a.out), end="")
     return 0
 
 

@@ -4,7 +4,7 @@
 Driver contract: ``python bench.py --gpus N --steps K --warmup W`` (N>1 under
 ``torch.distributed.run``, one rank per GPU, RCCL over xGMI). One *step* is one complete global
 reduction of the 1e9-element float64 array (BASELINE.json config 4): every rank reduces its
-contiguous 1e9/N shard with the native single-pass HIP kernel (csrc/kernels/reduce.hip) into a
+contiguous 1e9/N shard with the native single-pass HIP kernel (csrc/kernels/reduce_kernels.hpp) into a
 1-element slot, then the slots are all-reduced with RCCL. The array is synthetic (on-device
 counter-based U[0,1) fill, untimed) and fixed in size as N grows -> strong scaling.
 
@@ -76,8 +76,9 @@ def parse_args(argv=None):
                    help="vector (reduce.c) configs: torch.distributed collective, or the one-kernel direct "
                         "peer-read collective over xGMI (GPUs)")
     p.add_argument("--no-vector-extras", dest="vector_extras", action="store_false",
-                   help="north-star runs also time reduce.c's element-wise 2 GiB DOUBLE SUM (reduce / allreduce, "
-                        "RCCL and direct) and report it as reduce_c_vector; this skips that")
+                   help="north-star runs also time reduce.c's element-wise table (INT / DOUBLE x MAX / MIN / SUM of "
+                        "2 GiB to root 0, plus DOUBLE SUM all-reduce; RCCL and direct) and report it as "
+                        "reduce_c_vector; this skips that")
     p.add_argument("--local-only", action="store_true",
                    help="single rank: skip the cross-rank combine (by default it is issued even at N=1)")
     p.add_argument("--streams", type=int, default=1,

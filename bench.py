@@ -262,6 +262,9 @@ def _vector_extras(ctx, steps: int = 5) -> dict:
                     out[f"allreduce_{impl}"] = timed(wl)
             except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
                 err = {"error": f"{type(e).__name__}: {e}"[:200]}
+                import traceback
+                print(f"[bench] rank {ctx.rank}: reduce.c extra {dt}/{impl} failed:\n{traceback.format_exc()}",
+                      file=sys.stderr)
                 done = {(t["dtype"], t["op"]) for t in table if t["impl"] == impl}
                 table += [{"dtype": dt, "op": op.upper(), "impl": impl, **err} for op in REDUCE_C_OPS
                           if (dt, op.upper()) not in done]
@@ -514,22 +517,27 @@ def main(argv=None) -> int:
     slots = wl.new_slots(W + K)
     m1 = _measure(wl, slots, ctx, args, fault, serial=primary_serial, warmup=W)
     m1_lanes = len(wl.lanes) if wl.lanes else 1
+    m1_issues = wl.issues_collective
+    m1_err = wl.check()  # before any re-bind below drops the headline's channels
     m2 = None
     if not primary_serial and not wl.issues_collective and len(wl.lanes) <= 1:
         m2 = m1  # one kernel per step (fused finish): the pipelined run IS the serial run
     elif not primary_serial and not args.no_serial_measure:
         # The honest per-reduction number: every step completes (local reduce AND cross-rank
         # combine) before the next one starts (reduction.cpp:319-374 times each reduction to
-        # completion), on one stream lane. Reported next to the pipelined headline.
-        if len(wl.lanes) > 1:
-            wl.use_collective(wl.collective, streams=1)
+        # completion), on one stream lane. Reported next to the pipelined headline, with the
+        # lowest-latency combine that works: the in-kernel fused finish when it passed its
+        # self-check and tuning (no second launch per step), else the RCCL all-reduce.
+        serial_coll = "fused" if tuning is not None and tuning.get("fused_1lane", -1.0) > 0 else wl.collective
+        if len(wl.lanes) > 1 or serial_coll != wl.collective:
+            wl.use_collective(serial_coll, streams=1)
         slots2 = wl.new_slots(min(W, 2) + K)
         # a capture that already failed (e.g. gloo collectives on GPU tensors) is not retried
         m2 = _measure(wl, slots2, ctx, args, fault, serial=True, warmup=min(W, 2),
                       allow_graph=not m1["launch"].startswith("eager (graph capture failed"))
 
     verified = None
-    err = wl.check()
+    err = m1_err or (wl.check() if m2 is not None and m2 is not m1 else None)
     if not args.no_verify:
         ok, ref = _verify_slots(wl, slots[:m1["written"]], ctx)
         if m2 is not None and m2 is not m1:
@@ -553,7 +561,7 @@ def main(argv=None) -> int:
     ms = elapsed / K * 1e3
     lanes = m1_lanes
     if ctx.is_root:
-        if wl.issues_collective:
+        if m1_issues:
             combine = "RCCL all-reduce of the 1-element partial (torch.distributed nccl)" \
                 if ctx.backend == "nccl" else f"{ctx.backend} all-reduce of the 1-element partial"
         elif collective == "fused":
@@ -588,7 +596,7 @@ def main(argv=None) -> int:
                                             " (auto)" if args.collective == "auto" else ""),
                 "cross_rank_combine": combine,
                 "overlap": "serial (each step completes before the next)" if primary_serial else
-                           ("pipelined (step i+1 local reduce || step i all-reduce)" if wl.issues_collective
+                           ("pipelined (step i+1 local reduce || step i all-reduce)" if m1_issues
                             else f"pipelined over {lanes} stream lanes" if lanes > 1 else
                             "serial (one kernel per step: reduce + in-kernel combine)"),
                 "streams": lanes,
@@ -608,6 +616,7 @@ def main(argv=None) -> int:
             line["serial_gbps"] = round(bytes_step * K / m2["elapsed"] / 1e9, 3)
             line["serial_ms_per_step"] = round(m2["elapsed"] / K * 1e3, 5)
             line["serial_launch"] = m2["launch"]
+            line["serial_collective"] = wl.collective
         if torch_gbps is not None:
             line["torch_gbps"] = round(torch_gbps, 3)  # same data, torch's own reduction kernels
         if extras is not None:

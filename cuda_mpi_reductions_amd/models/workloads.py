@@ -461,34 +461,45 @@ class VectorReduction:
             self.comm.close()
             self.comm = None
 
+    VERIFY_CHUNK = 1 << 25  # elements per rank per verification all-gather
+
+    def _check_chunk(self, st: torch.Tensor, y: torch.Tensor, world: int) -> bool:
+        if self.cfg.op == "sum":
+            if st.dtype.is_floating_point:
+                exp = st.double().sum(0)
+                tol = 1e-12 * world * (exp.abs() + 1.0)
+                return bool(((y.double() - exp).abs() <= tol).all())
+            bits = 8 * st.element_size()
+            exp = st.long().sum(0) if bits == 32 else st.sum(0)
+            if bits == 32:
+                exp = ((exp + 2 ** 31) % 2 ** 32 - 2 ** 31).to(st.dtype)
+            return bool(torch.equal(exp, y))
+        exp = st.min(0).values if self.cfg.op == "min" else st.max(0).values
+        return bool(torch.equal(exp, y))
+
     def verify(self) -> dict:
-        """Gather every rank's input and combine on the result holders; integer SUM wraps like
-        MPI_INT / ncclInt32 (two's complement)."""
+        """Gather every rank's input (in chunks) and combine on the result holders; integer SUM wraps
+        like MPI_INT / ncclInt32 (two's complement)."""
         self.result()
         world = self.ctx.world_size
-        gathered = [torch.empty_like(self.x) for _ in range(world)]
-        if world > 1:
-            torch.distributed.all_gather(gathered, self.x)
-        else:
-            gathered[0].copy_(self.x)
         holder = self.cfg.collective == "allreduce" or self.ctx.rank == 0
         ok = True
-        if holder:
-            st = torch.stack(gathered)
-            if self.cfg.op == "sum":
-                if st.dtype.is_floating_point:
-                    exp = st.double().sum(0)
-                    tol = 1e-12 * world * (exp.abs() + 1.0)
-                    ok = bool(((self.y.double() - exp).abs() <= tol).all())
-                else:
-                    bits = 8 * st.element_size()
-                    exp = st.long().sum(0) if bits == 32 else st.sum(0)
-                    if bits == 32:
-                        exp = ((exp + 2 ** 31) % 2 ** 32 - 2 ** 31).to(st.dtype)
-                    ok = bool(torch.equal(exp, self.y))
+        # In chunks (bounded memory on the holder: world x chunk, widened). gloo gathers host
+        # copies: its own GPU-tensor path ran out of host allocations (std::bad_alloc) in the
+        # 2-rank reduce.c INT rehearsal on one GPU and left the other rank in a mismatched collective.
+        host = world > 1 and self.ctx.backend == "gloo" and self.x.is_cuda
+        step = self.VERIFY_CHUNK
+        for a in range(0, self.x.numel(), step):
+            xs, ys = self.x[a:a + step], self.y[a:a + step]
+            if host:
+                xs, ys = xs.cpu(), ys.cpu()
+            gathered = [torch.empty_like(xs) for _ in range(world)]
+            if world > 1:
+                torch.distributed.all_gather(gathered, xs.contiguous())
             else:
-                exp = st.min(0).values if self.cfg.op == "min" else st.max(0).values
-                ok = bool(torch.equal(exp, self.y))
+                gathered[0].copy_(xs)
+            if holder and ok:
+                ok = self._check_chunk(torch.stack(gathered), ys, world)
         if self.comm is not None and self.comm.check() is not None:
             ok = False
         t = torch.tensor([1 if ok else 0], dtype=torch.int32,

@@ -90,13 +90,24 @@ def vector_case(rank, world):
             else:
                 exp = st.max(0).values.int()
             out[op] = bool(torch.equal(exp, wl.y))
+        # the workload's own chunked verification (chunk not dividing the 32768 per-rank elements)
+        wl.VERIFY_CHUNK = 1000
+        out[op + "_verify"] = wl.verify()["ok"]
+        if op == "sum":  # rank 1 contributes a wrong element 0: every rank must see the failure
+            wl.restore()
+            if rank == 1:
+                wl.corrupt()
+            wl.collective()
+            out["sum_corrupt_verify"] = wl.verify()["ok"]
     pdist.shutdown(ctx)
     return out
 
 
 def test_vector_reduce_c_semantics_two_ranks():
     out = _spawn("vector_case", 2)
-    assert out[0] == {"sum": True, "min": True, "max": True}
+    assert out[0] == {"sum": True, "min": True, "max": True, "sum_verify": True, "min_verify": True,
+                      "max_verify": True, "sum_corrupt_verify": False}
+    assert out[1]["sum_corrupt_verify"] is False and out[1]["max_verify"] is True
 
 
 def test_shard_covers_everything():

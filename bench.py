@@ -79,6 +79,9 @@ def parse_args(argv=None):
                    help="north-star runs also time reduce.c's element-wise table (INT / DOUBLE x MAX / MIN / SUM of "
                         "2 GiB to root 0, plus DOUBLE SUM all-reduce; RCCL and direct) and report it as "
                         "reduce_c_vector; this skips that")
+    p.add_argument("--extras-deadline", type=float, default=240.0,
+                   help="seconds the reduce.c extras may take after the headline; past it rank 0 prints the "
+                        "headline (extras marked as timed out) and the run ends")
     p.add_argument("--local-only", action="store_true",
                    help="single rank: skip the cross-rank combine (by default it is issued even at N=1)")
     p.add_argument("--streams", type=int, default=1,
@@ -445,6 +448,45 @@ def _verify_slots(wl, written: torch.Tensor, ctx) -> tuple:
     return ok, ref
 
 
+class _ExtrasWatchdog:
+    """Deadline for the reduce.c extras. If it passes first, rank 0 prints the finished headline
+    line (``reduce_c_vector`` = the timeout) and every rank exits with the headline's status: a
+    hung extra (e.g. one rank failing inside a collective while the others wait in it) must not
+    hold the run until the process-group timeout and lose the measured metric."""
+
+    def __init__(self, line: "dict | None", deadline_s: float, rc: int):
+        import threading
+        self._line, self._deadline, self._rc = line, deadline_s, rc
+        self._lock = threading.Lock()
+        self._done = False
+        self._timer = threading.Timer(deadline_s, self._fire)
+        self._timer.daemon = True
+        self._timer.start()
+
+    def _fire(self) -> None:
+        with self._lock:
+            if self._done:
+                return
+            self._done = True
+            if self._line is not None:
+                line = dict(self._line)
+                line["reduce_c_vector"] = {"error": f"extras did not finish within {self._deadline:.0f} s "
+                                                    "(headline measured and verified before them)"}
+                print(json.dumps(line), flush=True)
+            print(f"[bench] reduce.c extras exceeded {self._deadline:.0f} s: exiting with the headline",
+                  file=sys.stderr, flush=True)
+            os._exit(self._rc)
+
+    def finish(self) -> bool:
+        """True if the extras finished before the deadline (the caller prints the line)."""
+        with self._lock:
+            self._timer.cancel()
+            if self._done:
+                return False
+            self._done = True
+            return True
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     C = native()  # fail loudly if the HIP extension is missing
@@ -552,14 +594,12 @@ def main(argv=None) -> int:
     torch_gbps = None
     if args.compare_torch and dev.type == "cuda":
         torch_gbps = _time_torch_reduction(wl, K, W, ctx)
-    extras = None
-    if args.vector_extras and dev.type == "cuda" and cfg.name == NORTH_STAR:
-        extras = _vector_extras(ctx)
     bytes_step = wl.bytes_total
     elapsed = m1["elapsed"]
     gbps = bytes_step * K / elapsed / 1e9
     ms = elapsed / K * 1e3
     lanes = m1_lanes
+    line = None
     if ctx.is_root:
         if m1_issues:
             combine = "RCCL all-reduce of the 1-element partial (torch.distributed nccl)" \
@@ -619,12 +659,20 @@ def main(argv=None) -> int:
             line["serial_collective"] = wl.collective
         if torch_gbps is not None:
             line["torch_gbps"] = round(torch_gbps, 3)  # same data, torch's own reduction kernels
-        if extras is not None:
+    rc = 0 if verified in (None, True) else 1
+    if args.vector_extras and dev.type == "cuda" and cfg.name == NORTH_STAR:
+        # The extras run after the headline is final; a watchdog prints the headline (extras marked
+        # as timed out) and ends the process if they hang, so they can never cost the metric.
+        guard = _ExtrasWatchdog(line, args.extras_deadline, rc)
+        extras = _vector_extras(ctx)
+        if guard.finish() and line is not None:
             line["reduce_c_vector"] = extras
+            print(json.dumps(line), flush=True)
+    elif line is not None:
         print(json.dumps(line), flush=True)
     _sync(dev)
     pdist.shutdown(ctx)
-    return 0 if verified in (None, True) else 1
+    return rc
 
 
 if __name__ == "__main__":

@@ -25,3 +25,32 @@ def test_auto_tune_steps_covers_about_30ms():
     assert b._auto_tune_steps(1e9) == 210  # the N=8 shard: 143 us per step at 7 TB/s
     assert b._auto_tune_steps(8e9) == 27
     assert b._auto_tune_steps(1e6) == 400 and b._auto_tune_steps(1e12) == 20  # clamps
+
+
+def _watchdog_child(deadline, work_s, rc):
+    import subprocess
+    import sys
+    code = (
+        "import importlib.util, os, sys, time\n"
+        f"spec = importlib.util.spec_from_file_location('b', os.path.join({ROOT!r}, 'bench.py'))\n"
+        "b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)\n"
+        f"g = b._ExtrasWatchdog({{'metric': 'm', 'value': 1.0}}, {deadline}, {rc})\n"
+        f"time.sleep({work_s})\n"
+        "print('finished' if g.finish() else 'late', flush=True)\n"
+        "sys.exit(7)\n")
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+
+
+def test_extras_watchdog_prints_headline_and_exits_on_deadline():
+    import json
+    r = _watchdog_child(0.3, 30, 0)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1 and "finished" not in r.stdout, (r.stdout, r.stderr)
+    d = json.loads(lines[0])
+    assert d["value"] == 1.0 and "did not finish" in d["reduce_c_vector"]["error"]
+    assert "exceeded" in r.stderr
+
+
+def test_extras_watchdog_stays_quiet_when_extras_finish():
+    r = _watchdog_child(30, 0.1, 0)
+    assert r.returncode == 7 and r.stdout.strip() == "finished", (r.stdout, r.stderr)

@@ -266,3 +266,15 @@ def test_reduce_xgmi_direct_eight_ranks_on_one_gpu():
                      "--direct-grid=16", "--timeout=30", "--graph"], timeout=900)
     assert r.returncode == 0, r.stderr[-4000:]
     assert "verification PASSED" in r.stderr
+
+
+def test_bench_extras_deadline_keeps_the_headline(tmp_path):
+    # reduce.c extras past their deadline: the headline line is still printed (extras marked as
+    # timed out) and the run ends with the headline's status.
+    r = run([sys.executable, BENCH, "--steps", "4", "--warmup", "1", "--elements", "50000017",
+             "--extras-deadline", "0.05"], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["verified"] is True and "did not finish" in d["reduce_c_vector"]["error"]

@@ -278,3 +278,20 @@ def test_bench_extras_deadline_keeps_the_headline(tmp_path):
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["verified"] is True and "did not finish" in d["reduce_c_vector"]["error"]
+
+
+def test_bench_serial_number_takes_the_faster_combine(tmp_path):
+    # auto at N=1: when the headline is not the one-lane fused finish, the serial (per-reduction)
+    # measurement runs both the fused finish and the RCCL all-reduce and reports the faster.
+    r = run([sys.executable, BENCH, "--steps", "12", "--warmup", "2", "--elements", "50000017",
+             "--no-vector-extras"], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["verified"] is True and d["serial_gbps"] > 0
+    cands = d.get("serial_candidates_gbps")
+    if cands is None:  # the headline itself is the serial protocol (fused, one lane)
+        assert d["collective_tuning"]["chosen"] == "fused_1lane" and d["serial_collective"] == "fused"
+    else:
+        assert set(cands) == {"fused", "rccl"}
+        best = max(cands, key=cands.get)
+        assert d["serial_collective"] == best and d["serial_gbps"] == cands[best]

@@ -240,7 +240,7 @@ def test_bench_rehearsal_two_ranks_one_gpu(tmp_path):
     env_before = os.environ.get("MIREDUCE_FORCE_DEVICE")
     os.environ["MIREDUCE_FORCE_DEVICE"] = "0"
     try:
-        r = torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "5",
+        r = torchrun(2, [os.path.join(ROOT, "bench.py"), "--no-vector-extras", "--gpus", "2", "--backend", "gloo", "--steps", "5",
                          "--warmup", "1", "--elements", "20000003"], cwd=tmp_path, timeout=600)
     finally:
         if env_before is None:
@@ -268,7 +268,7 @@ def test_bench_graph_capture_failure_falls_back_on_all_ranks(tmp_path, monkeypat
 @pytest.mark.parametrize("launch", ["graph", "eager"])
 def test_bench_launch_modes(tmp_path, launch):
     # Default launch on a GPU is graph replay of the timed steps; both modes verify every slot.
-    r = run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "37", "--warmup", "3", "--elements",
+    r = run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-vector-extras", "--steps", "37", "--warmup", "3", "--elements",
              "50000017", "--launch", launch, "--graph-chunk", "16"], cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])

@@ -65,7 +65,7 @@ def test_fused_world1_matches_torch(dt, op, n):
 def test_bench_torchrun_one_rank_graphs_both_modes(tmp_path, collective):
     # the cross-rank combine is issued at world 1 and captured into graphs for both
     # the pipelined headline and the serial measurement.
-    r = torchrun(1, [BENCH, "--gpus", "1", "--steps", "8", "--warmup", "2", "--elements", "50000017",
+    r = torchrun(1, [BENCH, "--no-vector-extras", "--gpus", "1", "--steps", "8", "--warmup", "2", "--elements", "50000017",
                      "--collective", collective], cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
@@ -78,7 +78,7 @@ def test_bench_torchrun_one_rank_graphs_both_modes(tmp_path, collective):
 
 
 def test_bench_fused_two_lanes(tmp_path):
-    r = run([sys.executable, BENCH, "--steps", "24", "--warmup", "2", "--elements", "50000017", "--collective",
+    r = run([sys.executable, BENCH, "--no-vector-extras", "--steps", "24", "--warmup", "2", "--elements", "50000017", "--collective",
              "fused", "--streams", "2", "--graph-chunk", "8"], cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
@@ -91,7 +91,7 @@ def test_bench_fused_two_lanes(tmp_path):
 @pytest.mark.parametrize("nproc", [2, 4])
 def test_bench_fused_ranks_share_one_gpu(tmp_path, nproc, monkeypatch):
     monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
-    r = torchrun(nproc, [BENCH, "--gpus", str(nproc), "--backend", "gloo", "--collective", "fused", "--steps", "10",
+    r = torchrun(nproc, [BENCH, "--no-vector-extras", "--gpus", str(nproc), "--backend", "gloo", "--collective", "fused", "--steps", "10",
                          "--warmup", "2", "--elements", "20000003", "--graph-chunk", "5"], cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
@@ -139,7 +139,7 @@ def test_bench_auto_falls_back_to_rccl_on_every_rank(tmp_path, monkeypatch):
     # One rank cannot create its mailbox: every rank must agree and run the RCCL/gloo combine.
     monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
     monkeypatch.setenv("MIREDUCE_XRANK_FAIL_RANK", "1")
-    r = torchrun(2, [BENCH, "--gpus", "2", "--backend", "gloo", "--steps", "4", "--warmup", "1",
+    r = torchrun(2, [BENCH, "--no-vector-extras", "--gpus", "2", "--backend", "gloo", "--steps", "4", "--warmup", "1",
                      "--elements", "20000003"], cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
@@ -148,7 +148,7 @@ def test_bench_auto_falls_back_to_rccl_on_every_rank(tmp_path, monkeypatch):
 
 
 def test_bench_auto_tunes_the_combine(tmp_path):
-    r = run([sys.executable, BENCH, "--steps", "6", "--warmup", "2", "--elements", "50000017"], cwd=tmp_path,
+    r = run([sys.executable, BENCH, "--no-vector-extras", "--steps", "6", "--warmup", "2", "--elements", "50000017"], cwd=tmp_path,
             timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
@@ -220,7 +220,7 @@ def test_bench_fused_corrupt_rank_fails_verification(tmp_path, monkeypatch):
     # fault injection through the fused finish: rank 1's result is perturbed; the AND over ranks
     # of the per-slot verification must fail the run.
     monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
-    r = torchrun(2, [BENCH, "--gpus", "2", "--backend", "gloo", "--collective", "fused", "--steps", "6",
+    r = torchrun(2, [BENCH, "--no-vector-extras", "--gpus", "2", "--backend", "gloo", "--collective", "fused", "--steps", "6",
                      "--warmup", "2", "--elements", "20000003", "--inject-fault", "corrupt@1:3"], cwd=tmp_path,
                  timeout=600)
     assert r.returncode != 0

@@ -74,7 +74,7 @@ const Table& table() {
 
 // Tuned gfx950 defaults, measured on MI355X with tools/tune.py (interleaved rounds in one
 // process; profiles/r1_tuning/). Median read bandwidth of the chosen point:
-//   8 GB f64 sum / min  512 x 16, 1 WG/CU, nt   7.29 / 7.38 TB/s (best point for both)
+//   8 GB f64 sum / min  512 x 16, 1 WG/CU, nt   7.29 / 7.38 TB/s (round 1; round 2: 256 x 8 x 1, below)
 //   1 GB f64 sum        256 x  2, 3 WG/CU, nt   7.12 TB/s (best)
 //   8 GB i64 max        256 x  2, 3 WG/CU, nt   7.30 TB/s (best; 512 x 16 x 1 is not in the top 8)
 //   8 GB f32 sum / max  256 x  2, 3 WG/CU, nt   7.20 / 7.25 TB/s (best 7.21 / 7.25)
@@ -92,10 +92,15 @@ struct Defaults {
 };
 Defaults tuned_defaults(size_t bytes, DType t) {
   constexpr size_t MB = 1ull << 20;
-  // >= 3 GB: one 512-thread workgroup per CU (tools/tune_types.sh, profiles/r1_session3/tune_types.txt):
-  // 8-byte types 16 vectors in flight per lane (f64 7.30, i64 7.30 TB/s vs 7.16 at 256x2x3),
-  // 4-byte types 4 (f32 7.17, i32 7.19 vs 7.14).
-  if (dtype_size(t) == 8 && bytes >= 3072 * MB) return {512, 16, 1, 1, 0};
+  // >= 3 GB, 8-byte types: one 256-thread workgroup per CU, 8 vectors in flight per lane. Round 1
+  // picked 512 x 16 x 1 (f64 7.29 vs 7.23 for 256 x 8 x 1, profiles/r1_tuning/); on round 2's boxes
+  // 512 x 16 x 1 ran 0.8-2.0 % behind 256 x 8 x 1, which was first or second on every box measured
+  // for f64 SUM and int64 MAX (8 GB: 7.21 / 7.22 vs 7.07 / 7.17, profiles/r2_plan/, r2_tune/).
+  // (Its compiled body issues 4 loads then interleaves waits and adds, ~9 in flight at 86 VGPRs;
+  // forcing all 16 up front with a sched_barrier was slower still: 6.95 TB/s, r2_plan/run2.sh.)
+  // 4-byte types: one 512-thread WG per CU, 4 vectors per lane (tools/tune_types.sh,
+  // profiles/r1_session3/tune_types.txt: f32 7.17, i32 7.19 vs 7.14).
+  if (dtype_size(t) == 8 && bytes >= 3072 * MB) return {256, 8, 1, 1, 0};
   if (dtype_size(t) == 4 && bytes >= 3072 * MB) return {512, 4, 1, 1, 0};
   if (dtype_is_half(t) && bytes > 192 * MB) return {256, 4, 2, 1, 0};
   if (bytes > 192 * MB) return {256, 2, 3, 1, 0};

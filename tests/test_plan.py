@@ -42,7 +42,7 @@ def test_grid_bounds_and_groups(n):
 def test_tuned_defaults_by_size():
     C = native()
     big = C.plan(0, 10**9, F64)            # 8 GB of 8-byte elements
-    assert (big["block"], big["unroll"], big["grid"], big["nontemporal"]) == (512, 16, 256, True)
+    assert (big["block"], big["unroll"], big["grid"], big["nontemporal"]) == (256, 8, 256, True)
     mid = C.plan(0, 125_000_000, F64)      # 1 GB: the 8-GPU shard of the north star
     assert (mid["block"], mid["unroll"], mid["grid"], mid["nontemporal"]) == (256, 2, 768, True)
     l3 = C.plan(0, 1 << 25, F64)           # 256 MB: nt is fast warm and cold (plan_256mb.csv)
@@ -52,7 +52,7 @@ def test_tuned_defaults_by_size():
     f32 = C.plan(0, 2 * 10**9, 2)          # 8 GB of fp32: one 512-thread WG per CU, 4 vectors per lane
     assert (f32["block"], f32["unroll"], f32["grid"]) == (512, 4, 256)
     i64 = C.plan(0, 10**9, 1)              # 8 GB of int64: like fp64
-    assert (i64["block"], i64["unroll"], i64["grid"]) == (512, 16, 256)
+    assert (i64["block"], i64["unroll"], i64["grid"]) == (256, 8, 256)
     f32_1g = C.plan(0, 250_000_000, 2)     # 1 GB keeps the 256x2x3 plan
     assert (f32_1g["block"], f32_1g["unroll"]) == (256, 2)
 

@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import argparse
 import json
+from dataclasses import replace
 import math
 import os
 import sys
@@ -91,6 +92,9 @@ def parse_args(argv=None):
     p.add_argument("--wg-per-cu", type=int, default=0)
     p.add_argument("--groups", type=int, default=0)
     p.add_argument("--policy", choices=["auto", "nt", "default"], default="auto")
+    p.add_argument("--no-plan-tune", dest="plan_tune", action="store_false",
+                   help="--collective auto on GPUs also measures the streaming-kernel plan for the shard "
+                        "(tuned default vs the runners-up, profiles/r2_plan/); this keeps the tuned default")
     p.add_argument("--two-pass", action="store_true")
     p.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
                    help="graph: replay the timed steps as captured hipGraphs (chunks of --graph-chunk steps); "
@@ -337,6 +341,18 @@ def _peer_read_extra(ctx, nbytes: int = 256 << 20, steps: int = 5) -> dict:
             "node_gbps": round(world * (world - 1) * nbytes * steps / slowest / 1e9, 2)}
 
 
+def _plan_candidates(bytes_per_gpu: float, esize: int) -> list:
+    """Streaming-kernel plans (block, unroll, workgroups per CU) worth measuring on the node for a
+    shard of this size: (0, 0, 0) = the tuned default. The ranking of the top plans moves by 1-2 %
+    between boxes (profiles/r2_plan/), so for the headline's 8-byte shards the bench measures the
+    default against the runners-up instead of trusting one box's table."""
+    if esize == 8 and bytes_per_gpu >= 3 * (1 << 30):
+        return [(0, 0, 0), (512, 8, 1), (512, 16, 1)]
+    if esize == 8 and bytes_per_gpu >= 768 * (1 << 20):
+        return [(0, 0, 0), (256, 8, 1)]
+    return [(0, 0, 0)]
+
+
 def _graph_chunk(requested: int, steps: int, issues_collective: bool) -> int:
     """Steps per captured graph. Auto: one graph for all the steps when they are kernels only (the
     fused finish; measured at the 1 GB N=8 shard with 2 lanes, 1000 steps: 7.32-7.34 TB/s as one
@@ -503,7 +519,6 @@ def main(argv=None) -> int:
               file=sys.stderr)
     cfg = CONFIGS[args.config]
     if args.elements is not None:
-        from dataclasses import replace
         cfg = replace(cfg, n_total=args.elements)
     if cfg.mode == "vector":
         rc = run_vector(args, ctx, cfg, fault)
@@ -534,6 +549,29 @@ def main(argv=None) -> int:
 
     primary_serial = args.serial
     tuning, tune_steps = None, 0
+    plan_tuning = None
+    explicit_plan = args.block or args.unroll or args.wg_per_cu or args.two_pass or args.policy != "auto"
+    if args.collective == "auto" and not primary_serial and not fault.enabled and dev.type == "cuda" \
+            and not explicit_plan and args.plan_tune:
+        cands = _plan_candidates(wl.bytes_total / ctx.world_size, torch.empty((), dtype=cfg.dtype).element_size())
+        if len(cands) > 1:
+            # Same protocol as the combine tuning below (graph replay, MAX over ranks, two rounds,
+            # best of each), one lane, with the combine the self-check settled on.
+            T = max(4, args.tune_steps) if args.tune_steps else _auto_tune_steps(wl.bytes_total / ctx.world_size)
+            plan_tuning = {}
+            for _round in range(2):
+                for b, u, w in cands:
+                    key = "tuned default" if b == 0 else f"{b}x{u}x{w}"
+                    wl.use_kernel(replace(kernel, block=b, unroll=u, wg_per_cu=w), streams=1)
+                    mt = _measure(wl, wl.new_slots(2 + T), ctx, args, fault, serial=False, warmup=2, steps=T)
+                    g = round(wl.bytes_total * T / mt["elapsed"] / 1e9, 3)
+                    if wl.check() is not None:  # a timed-out fused exchange: discard the point
+                        g = -1.0
+                    plan_tuning[key] = g if g < 0 else max(plan_tuning.get(key, 0.0), g)
+            best = max(plan_tuning, key=plan_tuning.get)
+            b, u, w = next(c for c in cands if ("tuned default" if c[0] == 0 else f"{c[0]}x{c[1]}x{c[2]}") == best)
+            kernel = replace(kernel, block=b, unroll=u, wg_per_cu=w)
+            wl.use_kernel(kernel, streams=args.streams)
     if args.collective == "auto" and collective == "fused" and not primary_serial and not fault.enabled:
         # Pick the headline combine by a short measurement of each candidate (same graph-replay
         # protocol, MAX over ranks, so every rank picks the same): the in-kernel fused finish on one
@@ -662,6 +700,8 @@ def main(argv=None) -> int:
         if tuning is not None:
             line["collective_tuning"] = {"steps": tune_steps, "gbps": tuning,
                                          "chosen": f"{collective}_{lanes}lane"}
+        if plan_tuning is not None:
+            line["plan_tuning"] = {"gbps": plan_tuning, "chosen": max(plan_tuning, key=plan_tuning.get)}
         if m2 is not None:
             line["serial_gbps"] = round(bytes_step * K / m2["elapsed"] / 1e9, 3)
             line["serial_ms_per_step"] = round(m2["elapsed"] / K * 1e3, 5)

@@ -234,7 +234,7 @@ class ScalarReduction:
                 stream = torch.cuda.current_stream(dev)
             else:
                 stream = old[k][0] if len(old) > 1 and k < len(old) else torch.cuda.Stream(dev)
-            reducer = old[k][1] if k < len(old) else Reducer(dev, config=self.kernel)
+            reducer = old[k][1] if k < len(old) and old[k][1].config == self.kernel else Reducer(dev, config=self.kernel)
             ch = open_channel(dev, timeout_s=self.xrank_timeout_s) if collective == "fused" else None
             bound = reducer.bind(self.x, self.cfg.op, self.acc, out=self._bound_out, xrank=ch)
             lanes.append((stream, reducer, bound, ch))
@@ -246,6 +246,12 @@ class ScalarReduction:
         self.reducer, self.bound = lanes[0][1], lanes[0][2]
         self.collective = collective
         torch.cuda.synchronize(dev)
+
+    def use_kernel(self, kernel: KernelConfig, streams: Optional[int] = None) -> None:
+        """Re-bind every lane with another streaming-kernel plan (fresh reducers; same data and
+        combine). Collective when the combine is ``fused``."""
+        self.kernel = kernel
+        self.use_collective(self.collective, streams=streams)
 
     @property
     def bytes_total(self) -> int:

@@ -54,3 +54,12 @@ def test_extras_watchdog_prints_headline_and_exits_on_deadline():
 def test_extras_watchdog_stays_quiet_when_extras_finish():
     r = _watchdog_child(30, 0.1, 0)
     assert r.returncode == 7 and r.stdout.strip() == "finished", (r.stdout, r.stderr)
+
+
+def test_plan_candidates_only_for_the_headline_shards():
+    b = _bench()
+    GB = 1 << 30
+    assert b._plan_candidates(8e9, 8) == [(0, 0, 0), (512, 8, 1), (512, 16, 1)]  # N=1 / N=2 shards
+    assert b._plan_candidates(1e9, 8) == [(0, 0, 0), (256, 8, 1)]                # N=8 shard
+    assert b._plan_candidates(0.5 * GB, 8) == [(0, 0, 0)]
+    assert b._plan_candidates(8e9, 4) == [(0, 0, 0)] and b._plan_candidates(8e9, 2) == [(0, 0, 0)]

@@ -295,3 +295,17 @@ def test_bench_serial_number_takes_the_faster_combine(tmp_path):
         assert set(cands) == {"fused", "rccl"}
         best = max(cands, key=cands.get)
         assert d["serial_collective"] == best and d["serial_gbps"] == cands[best]
+
+
+def test_bench_plan_tuning_at_the_eight_gpu_shard(tmp_path):
+    # auto at the 1 GB shard: the tuned default plan is measured against 256x8x1 and the faster
+    # is the one the headline runs.
+    r = run([sys.executable, BENCH, "--steps", "8", "--warmup", "2", "--elements", "125000000",
+             "--no-vector-extras", "--tune-steps", "8"], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["verified"] is True
+    pt = d["plan_tuning"]
+    assert set(pt["gbps"]) == {"tuned default", "256x8x1"} and pt["chosen"] == max(pt["gbps"], key=pt["gbps"].get)
+    plan = d["config"]["kernel_plan"]
+    assert (plan["block"], plan["unroll"]) == ((256, 8) if pt["chosen"] == "256x8x1" else (256, 2))

@@ -552,7 +552,7 @@ def main(argv=None) -> int:
     plan_tuning = None
     explicit_plan = args.block or args.unroll or args.wg_per_cu or args.two_pass or args.policy != "auto"
     if args.collective == "auto" and not primary_serial and not fault.enabled and dev.type == "cuda" \
-            and not explicit_plan and args.plan_tune:
+            and not explicit_plan and args.plan_tune and hasattr(wl, "use_kernel"):
         cands = _plan_candidates(wl.bytes_total / ctx.world_size, torch.empty((), dtype=cfg.dtype).element_size())
         if len(cands) > 1:
             # Same protocol as the combine tuning below (graph replay, MAX over ranks, two rounds,

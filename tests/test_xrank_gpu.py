@@ -309,3 +309,12 @@ def test_bench_plan_tuning_at_the_eight_gpu_shard(tmp_path):
     assert set(pt["gbps"]) == {"tuned default", "256x8x1"} and pt["chosen"] == max(pt["gbps"], key=pt["gbps"].get)
     plan = d["config"]["kernel_plan"]
     assert (plan["block"], plan["unroll"]) == ((256, 8) if pt["chosen"] == "256x8x1" else (256, 2))
+
+
+def test_bench_maxloc_config_skips_plan_tuning(tmp_path):
+    # MAXLOC runs the arg-reduction kernel (no streaming plan to re-bind): auto must not plan-tune it.
+    r = run([sys.executable, BENCH, "--config", "xgmi_1b_double_maxloc", "--steps", "4", "--warmup", "1",
+             "--elements", "125000000", "--no-vector-extras"], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["verified"] is True and "plan_tuning" not in d

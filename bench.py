@@ -608,9 +608,9 @@ def main(argv=None) -> int:
         # completion), on one stream lane. Reported next to the pipelined headline, with the
         # faster combine for that protocol: when the fused finish passed its self-check both it
         # (one kernel per step) and the RCCL all-reduce are measured, else the headline's combine.
-        # (The headline's slots are verified first: every re-bind keeps the data but a candidate's
-        # slots are checked before the next one runs.)
-        ok_head = _verify_slots(wl, slots[:m1["written"]], ctx)[0] if not args.no_verify else None
+        # (Every slot is verified after all measurements — the torch reference pass between two
+        # timed runs cost the following one ~6 % — while a candidate's channel errors are read
+        # before the next re-bind drops its channels.)
         fused_ok_here = tuning is not None and tuning.get("fused_1lane", -1.0) > 0
         for c in (["fused", "rccl"] if fused_ok_here else [wl.collective]):
             if len(wl.lanes) > 1 or c != wl.collective:
@@ -619,8 +619,7 @@ def main(argv=None) -> int:
             # a capture that already failed (e.g. gloo collectives on GPU tensors) is not retried
             m = _measure(wl, s2, ctx, args, fault, serial=True, warmup=min(W, 2),
                          allow_graph=not m1["launch"].startswith("eager (graph capture failed"))
-            m["collective"] = c
-            m["ok"] = _verify_slots(wl, s2[:m["written"]], ctx)[0] if not args.no_verify else None
+            m["collective"], m["slots"] = c, s2
             m["err"] = wl.check()  # before the next re-bind drops this candidate's channels
             serial_runs[c] = m
         m2 = min(serial_runs.values(), key=lambda m: m["elapsed"])
@@ -628,11 +627,9 @@ def main(argv=None) -> int:
     verified = None
     err = m1_err or next((m["err"] for m in serial_runs.values() if m["err"]), None)
     if not args.no_verify:
-        if serial_runs:
-            ok, ref = ok_head, None
-            ok = ok and all(m["ok"] for m in serial_runs.values())
-        else:
-            ok, ref = _verify_slots(wl, slots[:m1["written"]], ctx)
+        ok, ref = _verify_slots(wl, slots[:m1["written"]], ctx)
+        for m in serial_runs.values():
+            ok = _verify_slots(wl, m["slots"][:m["written"]], ctx)[0] and ok
         verified = ok and err is None
         if not verified and ctx.is_root:
             print(f"[bench] VERIFICATION FAILED: {ref or ''} {err or ''}", file=sys.stderr)

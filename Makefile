@@ -18,7 +18,7 @@ BUILD     ?= build
 
 OPT       := $(if $(DEBUG),-O0 -g,-O3)
 CXXSTD    := -std=c++17
-INCLUDES  := -Icsrc/include -I$(ROCM)/include
+INCLUDES  := -Icsrc/include -I$(BUILD)/gen -I$(ROCM)/include
 WARN      := -Wall -Wno-unused-result
 COMMON    := $(CXXSTD) $(OPT) $(WARN) -fPIC $(INCLUDES)
 HIPFLAGS  := $(COMMON) -x hip --offload-arch=$(ARCH) -munsafe-fp-atomics $(if $(SAVE_TEMPS),-save-temps=obj,)
@@ -61,6 +61,17 @@ $(BUILD)/obj/%.o: csrc/%.cpp $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HOSTCXX) $(HOSTFLAGS) -c $< -o $@
 
+# Build provenance (csrc/include/mireduce/version.hpp): the source hash header is regenerated on
+# every make but replaced only when the hash changed, so version.o (and the links) rebuild exactly
+# when some csrc file did.
+SRC_HASH_H := $(BUILD)/gen/mireduce_source_hash.h
+.PHONY: FORCE
+FORCE:
+$(SRC_HASH_H): FORCE
+	@mkdir -p $(dir $@)
+	@$(PYTHON) tools/source_hash.py --header > $@.tmp && { cmp -s $@.tmp $@ || mv $@.tmp $@; }; rm -f $@.tmp
+$(BUILD)/obj/runtime/version.o: $(SRC_HASH_H)
+
 # core: kernels + host runtime (no RCCL: the python extension shares a process with torch's RCCL)
 $(LIB): $(KERNEL_OBJ) $(RUNTIME_OBJ)
 	@mkdir -p $(dir $@)
@@ -86,10 +97,10 @@ $(BUILD)/bin/%: csrc/apps/%.cpp $(LIB) $(COMMLIB) $(HEADERS)
 	    -L$(ROCM)/lib -lrccl $(LDLIBS) -o $@
 
 # reduce.c parity app: plain C++ against MPICH (CPU buffers only; no HIP needed).
-MPI_SRCS := csrc/apps/reduce_mpi.cpp csrc/runtime/fault.cpp csrc/runtime/mt19937.cpp csrc/runtime/cli.cpp csrc/runtime/report.cpp csrc/runtime/timer.cpp csrc/runtime/types.cpp
-$(MPI_APP): $(MPI_SRCS) $(HEADERS)
+MPI_SRCS := csrc/apps/reduce_mpi.cpp csrc/runtime/fault.cpp csrc/runtime/mt19937.cpp csrc/runtime/cli.cpp csrc/runtime/report.cpp csrc/runtime/timer.cpp csrc/runtime/types.cpp csrc/runtime/version.cpp
+$(MPI_APP): $(MPI_SRCS) $(HEADERS) $(SRC_HASH_H)
 	@mkdir -p $(dir $@)
-	g++ $(CXXSTD) -O3 -Wall -Icsrc/include -DMIREDUCE_NO_HIP -I$(MPI_HOME)/include \
+	g++ $(CXXSTD) -O3 -Wall -Icsrc/include -I$(BUILD)/gen -DMIREDUCE_NO_HIP -I$(MPI_HOME)/include \
 	    $(MPI_SRCS) -static-libstdc++ -static-libgcc $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,$(MPI_HOME)/lib -o $@
 
 # Diagnostic: per-workgroup timeline of streaming-body variants (docs/TUNING.md).
@@ -110,7 +121,7 @@ unit: $(UNIT)
 
 $(BUILD)/bin/host_unit: tests/native/host_unit.cpp $(filter-out csrc/apps/reduce_mpi.cpp,$(MPI_SRCS)) $(HEADERS)
 	@mkdir -p $(dir $@)
-	g++ $(CXXSTD) -O2 -Wall -Icsrc/include -DMIREDUCE_NO_HIP tests/native/host_unit.cpp \
+	g++ $(CXXSTD) -O2 -Wall -Icsrc/include -I$(BUILD)/gen -DMIREDUCE_NO_HIP tests/native/host_unit.cpp \
 	    $(filter-out csrc/apps/reduce_mpi.cpp,$(MPI_SRCS)) -o $@
 
 $(BUILD)/bin/bootstrap_test: tests/native/bootstrap_test.cpp $(COMMLIB) $(LIB) $(HEADERS)
@@ -121,10 +132,10 @@ $(BUILD)/bin/bootstrap_test: tests/native/bootstrap_test.cpp $(COMMLIB) $(LIB) $
 # Host sanitizers: CPU-only code paths under ASan+UBSan.
 asan: csrc/apps/reduce_mpi.cpp
 	@mkdir -p $(BUILD)/asan
-	g++ $(CXXSTD) -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -Icsrc/include -DMIREDUCE_NO_HIP \
+	g++ $(CXXSTD) -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -Icsrc/include -I$(BUILD)/gen -DMIREDUCE_NO_HIP \
 	    -I$(MPI_HOME)/include $(MPI_SRCS) -static-libstdc++ -static-libgcc $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,$(MPI_HOME)/lib \
 	    -o $(BUILD)/asan/reduce_mpi
-	g++ $(CXXSTD) -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -Icsrc/include -DMIREDUCE_NO_HIP \
+	g++ $(CXXSTD) -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -Icsrc/include -I$(BUILD)/gen -DMIREDUCE_NO_HIP \
 	    tests/native/host_unit.cpp $(filter-out csrc/apps/reduce_mpi.cpp,$(MPI_SRCS)) -o $(BUILD)/asan/host_unit
 
 clean:

@@ -12,21 +12,24 @@ Timing: W untimed warm-up steps; then barrier + synchronize, K timed steps, sync
 MAX elapsed time over ranks defines the measurement. Value = total bytes reduced per step x K /
 elapsed / 1e9 (GB = 1e9 B, the CUDA sample's unit, reduction.cpp:744-745).
 
-Cross-rank combine (``--collective``): ``rccl`` = a 1-element RCCL all-reduce after the local
-kernel (on RCCL's stream); ``fused`` = the local kernel's last workgroup exchanges the partials
-through IPC-mapped mailboxes over xGMI and folds them itself (csrc/include/mireduce/xrank.hpp),
-one kernel per step. The combine is issued even at N=1 (``--local-only`` skips it), so the 1-GPU
-run executes exactly the N-GPU step.
+Cross-rank combine (``--collective``): ``fused`` = the local kernel's last workgroup exchanges the
+partials through IPC-mapped mailboxes over xGMI and folds them itself (csrc/include/mireduce/xrank.hpp),
+one kernel per step, every device wait bounded; ``rccl`` = a 1-element RCCL all-reduce after the
+local kernel (on RCCL's stream); ``auto`` (default) = fused if its self-check passes on every rank,
+else rccl. The combine is issued even at N=1 (``--local-only`` skips it), so the 1-GPU run executes
+exactly the N-GPU step (at world 1 it exchanges nothing).
 
-Two measurements per run: the headline ``value`` is pipelined (independent steps: step i+1's
-local reduce overlaps step i's all-reduce, which runs on its own stream); ``serial_gbps`` /
-``serial_ms_per_step`` time each step to completion before the next starts (the reference's
-per-reduction timing, reduction.cpp:319-374). ``--serial`` makes the serial number the headline.
-Both are replayed from captured hipGraphs by default (``--launch``; chunks of up to 128 steps,
-captured after eager warm-up steps and replayed once untimed): eager Python issue of the RCCL
-all-reduce leaves ~22 us GPU gaps per step, which at N=8 (0.14 ms per step) would cost ~15 %.
-Every step's result is checked after timing against torch's own fp64 reduction of the shards
-(AND over ranks).
+Headline = the per-reduction time (reduction.cpp:319-374, mpi/reduce.c:75-79): ONE stream lane,
+every step — local reduce AND cross-rank combine — completes before the next starts, replayed from
+captured hipGraphs (``--launch``; captured after eager warm-up steps and replayed once untimed:
+eager Python issue leaves ~22 us GPU gaps per step). The headline phase runs under a deadline
+(``--headline-deadline``): past it rank 0 prints a diagnostic JSON line and every rank exits
+non-zero instead of waiting out the process-group timeout. Only after the line is final do the
+extras run (pipelined / 2-lane / RCCL candidates, reduce.c's element-wise table, the xGMI peer-read
+probe), under their own watchdog (``--extras-deadline``): a hung extra still leaves the printed,
+verified headline. Every step's result is checked after timing against torch's own fp64 reduction
+of the shards (AND over ranks), and every device-side error word (polled fan-in, fused finish) is
+read and agreed over ranks.
 
 Reference number: 92.7729 GB/s (CUDA DOUBLE SUM, mpi/CUdata.txt:2).
 """
@@ -59,10 +62,16 @@ def parse_args(argv=None):
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default=NORTH_STAR, choices=sorted(CONFIGS))
     p.add_argument("--elements", type=int, default=None, help="override the global element count")
-    p.add_argument("--serial", action="store_true",
-                   help="headline with no overlap between consecutive steps (default: pipelined headline, "
-                        "serial reported as serial_gbps)")
-    p.add_argument("--no-serial-measure", action="store_true", help="skip the second (serial) measurement")
+    p.add_argument("--pipelined", action="store_true",
+                   help="experiment: a pipelined headline (independent steps overlap: step i+1's local reduce "
+                        "with step i's combine, or over --streams lanes) instead of the per-reduction time")
+    p.add_argument("--serial", action="store_true", help="(default; kept for old command lines)")
+    p.add_argument("--headline-deadline", type=float, default=180.0,
+                   help="seconds the headline phase (setup, self-check, plan tuning, timed steps, verification) "
+                        "may take; past it rank 0 prints a diagnostic JSON line and every rank exits with 2")
+    p.add_argument("--no-candidates", dest="candidates", action="store_false",
+                   help="skip the after-headline candidate measurements (pipelined 2-lane fused finish, RCCL "
+                        "serial / pipelined)")
     p.add_argument("--collective", choices=["auto", "rccl", "fused"], default="auto",
                    help="cross-rank combine: rccl = 1-element RCCL all-reduce after the local kernel; "
                         "fused = the kernel's last workgroup folds all ranks' partials via IPC mailboxes; "
@@ -70,9 +79,8 @@ def parse_args(argv=None):
     p.add_argument("--xrank-timeout", type=float, default=30.0,
                    help="fused finish: seconds a kernel waits for a peer's partial before flagging the channel")
     p.add_argument("--tune-steps", type=int, default=0,
-                   help="--collective auto: steps of the short per-candidate measurement that picks the headline "
-                        "combine (fused 1 lane, fused 2 lanes, RCCL pipelined); 0 = enough steps for ~30 ms of "
-                        "reduction per candidate (20..400)")
+                   help="--collective auto: steps of the short per-plan measurement that picks the streaming-kernel "
+                        "plan (fused finish only); 0 = enough steps for ~30 ms of reduction per plan (20..400)")
     p.add_argument("--vector-impl", choices=["rccl", "direct"], default="rccl",
                    help="vector (reduce.c) configs: torch.distributed collective, or the one-kernel direct "
                         "peer-read collective over xGMI (GPUs)")
@@ -86,7 +94,8 @@ def parse_args(argv=None):
     p.add_argument("--local-only", action="store_true",
                    help="single rank: skip the cross-rank combine (by default it is issued even at N=1)")
     p.add_argument("--streams", type=int, default=1,
-                   help="alternate independent steps over this many HIP streams (each with its own workspace)")
+                   help="with --pipelined: alternate independent steps over this many HIP streams (each with its "
+                        "own workspace); the per-reduction headline always runs one lane")
     p.add_argument("--block", type=int, default=0)
     p.add_argument("--unroll", type=int, default=0)
     p.add_argument("--wg-per-cu", type=int, default=0)
@@ -104,8 +113,9 @@ def parse_args(argv=None):
                         "fewer, longer graphs leave fewer bubbles); 0 = auto: every timed step in one graph "
                         "(<= 4096) for the in-kernel fused finish, 128 when steps issue RCCL collectives")
     p.add_argument("--inject-fault", default=None,
-                   help="failure-detection test: KIND[@RANK][:STEP], KIND = exit|hang|corrupt|delay=<ms> "
-                        "(steps count warm-up first; forces --launch eager)")
+                   help="failure-detection test: KIND[@RANK][:STEP][/SITE], KIND = exit|hang|corrupt|delay=<ms>|"
+                        "mailbox, SITE = step (headline; steps count warm-up first; forces eager issue) | extras "
+                        "(the after-headline candidates)")
     p.add_argument("--pg-timeout", type=float, default=600.0, help="process-group collective timeout (s)")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--compare-torch", action="store_true",
@@ -172,14 +182,14 @@ def _time_vector(wl, ctx, K: int, W: int, fault, verify: bool) -> tuple:
     dev = ctx.device
     for i in range(W):
         wl.restore()
-        if fault is not None and fault.enabled and fault.at(ctx.rank, i, "bench step"):
+        if fault is not None and fault.at(ctx.rank, i, "step", "bench step"):
             wl.corrupt()
         wl.collective()
     times, checks = [], []
     holder = wl.cfg.collective == "allreduce" or ctx.rank == 0
     for i in range(W, W + K):
         wl.restore()
-        if fault is not None and fault.enabled and fault.at(ctx.rank, i, "bench step"):
+        if fault is not None and fault.at(ctx.rank, i, "step", "bench step"):
             wl.corrupt()  # this rank contributes a wrong element: verification must fail
         _sync(dev)
         pdist.barrier(ctx)
@@ -225,69 +235,111 @@ def run_vector(args, ctx, cfg, fault) -> int:
 
 
 REDUCE_C_OPS = ("max", "min", "sum")  # reduce.c's operations[] order = its output row order (reduce.c:26-28)
+REDUCE_C_DTYPES = (("INT", "xgmi_2g_int_sum_reduce"), ("DOUBLE", "xgmi_2g_double_sum_reduce"))  # reduce.c:73-97
+REDUCE_C_RETRIES = 5  # RETRY_COUNT (mpi/constants.h:5)
+REDUCE_C_HEADER = "# DATATYPE OP NODES GB/sec"  # reduce.c:68
+WORLD1_RCCL = ("world 1: a 1-rank in-place RCCL reduce enqueues no work (torch.distributed.reduce is in-place), "
+               "so there is no number to report; the cross-GPU table needs N > 1")
 
 
-def _vector_extras(ctx, steps: int = 5) -> dict:
-    """reduce.c's own measurement on this job's GPUs, next to the scalar headline. Its whole table:
-    element-wise INT and DOUBLE MAX / MIN / SUM of 2 GiB of total data each (NUM_INTS / NUM_DOUBLES,
-    mpi/constants.h:1-2) to root 0 (MPI_Reduce, reduce.c:76,90), over RCCL and over the direct
-    one-kernel collective, plus DOUBLE SUM to every rank (all-reduce); RETRY_COUNT (5) timed
-    collectives each; GiB/s of total data (reduce.c:79,93).
+def _one_collective(wl, ctx) -> float:
+    """One timed element-wise collective, as reduce.c times one MPI_Reduce (reduce.c:74-79): the
+    receive side is restored outside the clock, then barrier, collective, synchronize; MAX over ranks
+    (reduce.c timed on rank 0 only and without a barrier)."""
+    wl.restore()
+    _sync(ctx.device)
+    pdist.barrier(ctx)
+    t0 = time.perf_counter()
+    wl.collective()
+    _sync(ctx.device)
+    return pdist.max_over_ranks(time.perf_counter() - t0, ctx)
 
-    ``reduce_<impl>`` / ``allreduce_<impl>``: DOUBLE SUM; ``table``: one entry per (dtype, op, impl)
-    in reduce.c's row order, and ``rows``: the same as reduce.c's ``"%s %s %d %10.3lf"`` output
-    lines (DATATYPE OP NODES GB/sec, reduce.c:81,95; ``impl`` selects the file in
-    tools/scaling.py's results/vector_<impl>/<DT>_<OP>.txt). Errors are recorded, not raised."""
-    from dataclasses import replace as _replace
 
+def _checksum(wl, holder: bool) -> float:
+    return float(wl.result().to(torch.float64).sum().item()) if holder else 0.0
+
+
+def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES) -> dict:
+    """reduce.c's own measurement on this job's GPUs, next to the scalar headline, in reduce.c's
+    shape: element-wise INT and DOUBLE MAX / MIN / SUM of 2 GiB of total data each (NUM_INTS /
+    NUM_DOUBLES, mpi/constants.h:1-2) to root 0 (MPI_Reduce, reduce.c:76,90), one warm-up SUM per
+    dtype (reduce.c:61-64), then ``retries`` rounds of the six collectives in reduce.c's row order,
+    each timed on its own (retry-major, reduce.c:71-97); GiB/s of total data (reduce.c:79,93). Over
+    RCCL (torch.distributed, in place: the receive buffer is restored outside the clock like
+    reduce.c's bzero) and over the direct one-kernel collective (send buffer -> separate receive
+    buffer, like reduce.c's random_* -> reduced_*, reduce.c:46-49).
+
+    ``table``: one entry per timed collective (retry, dtype, op, impl); ``rows``: per impl, exactly
+    reduce.c's stdout (header + ``"%s %s %d %10.3lf"`` lines, reduce.c:68,81,95), ready for
+    utils/getavgs.py; ``reduce_<impl>`` / ``allreduce_<impl>``: DOUBLE SUM to root / to every rank.
+    At world 1 RCCL rows are null (its 1-rank in-place reduce does no work). Every (dtype, op) is
+    verified against the gathered inputs on its first retry and later retries must reproduce its
+    checksum. Errors are recorded, not raised."""
     from cuda_mpi_reductions_amd.models import CONFIGS as _C, VectorReduction
-    out = {"units": "GiB/s (2^30 B of total data per collective, reduce.c:93)", "dtype": "DOUBLE", "op": "SUM",
-           "total_bytes": 256 * 1024 * 1024 * 8}
+    out = {"units": "GiB/s (2^30 B of total data per collective, reduce.c:93)", "retries": retries,
+           "order": "retry-major: per retry INT MAX, INT MIN, INT SUM, DOUBLE MAX, DOUBLE MIN, DOUBLE SUM "
+                    "(reduce.c:71-97)", "total_bytes": 256 * 1024 * 1024 * 8}
     # (gloo rehearsals: its GPU-tensor reduce / all_reduce is not RCCL and crashes on 1 GiB
     # tensors, so only the direct collective runs there)
     impls = ("rccl", "direct") if ctx.backend == "nccl" else ("direct",)
-    table = []
-
-    def timed(wl):
-        el, ok = _time_vector(wl, ctx, steps, 1, None, True)
-        return {"gibps": round(wl.bytes_total * steps / el / float(1 << 30), 3),
-                "ms": round(el / steps * 1e3, 4), "verified": ok}
-
-    for base, dt in (("xgmi_2g_int_sum_reduce", "INT"), ("xgmi_2g_double_sum_reduce", "DOUBLE")):
-        for impl in impls:
-            wl = None
-            try:  # one registration per (dtype, impl); the operator / collective only change the launch
-                wl = VectorReduction(_C[base], ctx, impl=impl, direct_timeout_s=5.0).setup()
-                for op in REDUCE_C_OPS:
-                    wl.cfg = _replace(_C[base], op=op)
-                    r = timed(wl)
-                    table.append({"dtype": dt, "op": op.upper(), "impl": impl, **r})
-                    if dt == "DOUBLE" and op == "sum":
-                        out[f"reduce_{impl}"] = r
-                if dt == "DOUBLE":
-                    wl.cfg = _replace(_C[base], collective="allreduce")
-                    out[f"allreduce_{impl}"] = timed(wl)
-            except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
-                err = {"error": f"{type(e).__name__}: {e}"[:200]}
-                import traceback
-                print(f"[bench] rank {ctx.rank}: reduce.c extra {dt}/{impl} failed:\n{traceback.format_exc()}",
-                      file=sys.stderr)
-                done = {(t["dtype"], t["op"]) for t in table if t["impl"] == impl}
-                table += [{"dtype": dt, "op": op.upper(), "impl": impl, **err} for op in REDUCE_C_OPS
-                          if (dt, op.upper()) not in done]
-                if dt == "DOUBLE":
-                    out.setdefault(f"reduce_{impl}", err)
-                    out.setdefault(f"allreduce_{impl}", err)
-            if wl is not None:
-                wl.close()  # collective: the next registration may reuse these addresses
-                del wl
-            torch.cuda.empty_cache()
+    table, rows = [], {}
+    holder = ctx.rank == 0
+    for impl in impls:
+        if impl == "rccl" and ctx.world_size == 1:
+            table += [{"dtype": dt, "op": op.upper(), "impl": impl, "gibps": None, "note": WORLD1_RCCL}
+                      for dt, _ in REDUCE_C_DTYPES for op in REDUCE_C_OPS]
+            out["reduce_rccl"] = out["allreduce_rccl"] = {"gibps": None, "note": WORLD1_RCCL}
+            continue
+        wls = {}
+        lines = [REDUCE_C_HEADER]
+        try:
+            for dt, base in REDUCE_C_DTYPES:  # both registered up front: the rounds interleave dtypes
+                wls[dt] = VectorReduction(_C[base], ctx, impl=impl, direct_timeout_s=5.0).setup()
+            for dt, base in REDUCE_C_DTYPES:  # warm-up SUM per dtype (reduce.c:61-64)
+                wls[dt].cfg = replace(_C[base], op="sum")
+                _one_collective(wls[dt], ctx)
+            first = {}
+            for x in range(retries):
+                for dt, base in REDUCE_C_DTYPES:
+                    wl = wls[dt]
+                    for op in REDUCE_C_OPS:
+                        wl.cfg = replace(_C[base], op=op)
+                        el = _one_collective(wl, ctx)
+                        gib = wl.bytes_total / el / float(1 << 30)
+                        if x == 0:  # full check against the gathered inputs, and the reference checksum
+                            ok = wl.verify()["ok"]
+                            first[(dt, op)] = _checksum(wl, holder)
+                        else:
+                            same = _checksum(wl, holder) == first[(dt, op)]
+                            ok = -pdist.max_over_ranks(-float(same), ctx) > 0.5  # AND over ranks
+                        table.append({"retry": x, "dtype": dt, "op": op.upper(), "impl": impl,
+                                      "gibps": round(gib, 3), "ms": round(el * 1e3, 4), "verified": ok})
+                        lines.append("%s %s %d %10.3lf" % (dt, op.upper(), ctx.world_size, gib))
+            for kind, coll in (("reduce", "reduce"), ("allreduce", "allreduce")):  # DOUBLE SUM summaries
+                wl = wls["DOUBLE"]
+                wl.cfg = replace(_C["xgmi_2g_double_sum_reduce"], op="sum", collective=coll)
+                els = [_one_collective(wl, ctx) for _ in range(retries)]
+                ok = wl.verify()["ok"]
+                out[f"{kind}_{impl}"] = {"gibps": round(wl.bytes_total * retries / sum(els) / float(1 << 30), 3),
+                                         "ms": round(sum(els) / retries * 1e3, 4), "verified": ok}
+        except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
+            import traceback
+            err = {"error": f"{type(e).__name__}: {e}"[:200]}
+            print(f"[bench] rank {ctx.rank}: reduce.c extra ({impl}) failed:\n{traceback.format_exc()}",
+                  file=sys.stderr)
+            table.append({"impl": impl, **err})
+            out.setdefault(f"reduce_{impl}", err)
+            out.setdefault(f"allreduce_{impl}", err)
+        for wl in wls.values():
+            wl.close()  # collective: the next registration may reuse these addresses
+        wls.clear()
+        torch.cuda.empty_cache()
+        rows[impl] = lines
     out["table"] = table
+    out["rows"] = rows
     if ctx.world_size == 1:
-        out["note"] = ("world 1: RCCL enqueues no work for a 1-rank in-place reduce (its GiB/s is the host "
-                       "round trip only); direct is one local in -> out pass; cross-GPU numbers need N > 1")
-    out["rows"] = ["%s %s %d %10.3lf" % (t["dtype"], t["op"], ctx.world_size, t["gibps"]) + f"  # {t['impl']}"
-                   for t in table if "gibps" in t]
+        out["note"] = ("world 1: RCCL rows are null (no work); direct is one local send -> receive pass (what "
+                       "MPI_Reduce does on one rank); tools/scaling.py keeps N=1 out of the results files")
     if ctx.world_size > 1:
         out["peer_read"] = _peer_read_extra(ctx)
     return out
@@ -364,9 +416,10 @@ def _graph_chunk(requested: int, steps: int, issues_collective: bool) -> int:
 
 
 def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph: bool = True,
-             steps: "int | None" = None) -> dict:
+             steps: "int | None" = None, site: str = "step") -> dict:
     """Time K steps (after ``warmup`` eager steps); returns elapsed (MAX over ranks), the launch
-    mode and how many slots the timed steps wrote (graph replays rewrite the first chunk)."""
+    mode and how many slots the timed steps wrote (graph replays rewrite the first chunk). ``site``:
+    the fault-injection site of these steps (``step`` = the headline, ``extras`` = a candidate)."""
     C = native()
     dev = ctx.device
     K = args.steps if steps is None else steps
@@ -376,7 +429,7 @@ def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph
         wl.fork()
         for i in range(first, first + count):
             C.trace_push("bench.step")
-            corrupt = fault.at(ctx.rank, i, "bench step") if fault.enabled else False
+            corrupt = fault.at(ctx.rank, i, site, f"bench {site}")
             w = wl.step(slots[i:i + 1], async_op=True, corrupt=corrupt)
             C.trace_pop()
             if w is not None:
@@ -390,9 +443,10 @@ def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph
 
     run(0, warmup)
     launch, sg = "eager", None
-    capturable = dev.type == "cuda" and not args.trace and not fault.enabled and \
+    armed = fault.on(site)
+    capturable = dev.type == "cuda" and not args.trace and not armed and \
         (not wl.issues_collective or ctx.backend == "nccl")
-    if allow_graph and ((args.launch == "graph" and not fault.enabled) or (args.launch == "auto" and capturable)):
+    if allow_graph and ((args.launch == "graph" and not armed) or (args.launch == "auto" and capturable)):
         # Capture the K timed steps as graph replays of --graph-chunk-step chunks (all ranks agree
         # on success or all fall back to eager issue); one untimed replay uploads the graphs.
         W = warmup
@@ -429,12 +483,12 @@ def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph
 
 def _try_fused(wl, ctx) -> "str | None":
     """Switch the workload to the fused in-kernel finish and check it on every rank: 3 steps, no
-    channel timeout, results equal to torch's reference. On any failure (agreed over ranks) switch
-    back to RCCL and return the reason."""
+    channel timeout or fan-in error, results equal to torch's reference. On any failure (agreed over
+    ranks) switch back to RCCL and return the reason."""
     try:
-        wl.use_collective("fused")  # collective; raises on every rank if any rank cannot map
+        wl.use_collective("fused", streams=1)  # collective; raises on every rank if any rank cannot map
     except Exception as e:  # noqa: BLE001
-        wl.use_collective("rccl")
+        wl.use_collective("rccl", streams=1)
         return f"setup: {e}"[:300]
     slots = wl.new_slots(3)
     for i in range(3):
@@ -446,7 +500,7 @@ def _try_fused(wl, ctx) -> "str | None":
         if not ok:
             err = f"self-check mismatch: {ref}"
     if err is not None:
-        wl.use_collective("rccl")
+        wl.use_collective("rccl", streams=1)
     return err
 
 
@@ -464,15 +518,14 @@ def _verify_slots(wl, written: torch.Tensor, ctx) -> tuple:
     return ok, ref
 
 
-class _ExtrasWatchdog:
-    """Deadline for the reduce.c extras. If it passes first, rank 0 prints the finished headline
-    line (``reduce_c_vector`` = the timeout) and every rank exits with the headline's status: a
-    hung extra (e.g. one rank failing inside a collective while the others wait in it) must not
-    hold the run until the process-group timeout and lose the measured metric."""
+class _PhaseWatchdog:
+    """Deadline for one phase of the run. If it passes first, rank 0 prints ``make_line()`` (when
+    not None) and every rank exits with ``rc``: a phase hung in a collective (e.g. one rank failing
+    inside it while the others wait) must not hold the run until the process-group timeout."""
 
-    def __init__(self, line: "dict | None", deadline_s: float, rc: int):
+    def __init__(self, what: str, deadline_s: float, rc: int, make_line):
         import threading
-        self._line, self._deadline, self._rc = line, deadline_s, rc
+        self._what, self._deadline, self._rc, self._make_line = what, deadline_s, rc, make_line
         self._lock = threading.Lock()
         self._done = False
         self._timer = threading.Timer(deadline_s, self._fire)
@@ -484,23 +537,103 @@ class _ExtrasWatchdog:
             if self._done:
                 return
             self._done = True
-            if self._line is not None:
-                line = dict(self._line)
-                line["reduce_c_vector"] = {"error": f"extras did not finish within {self._deadline:.0f} s "
-                                                    "(headline measured and verified before them)"}
+            line = self._make_line()
+            if line is not None:
                 print(json.dumps(line), flush=True)
-            print(f"[bench] reduce.c extras exceeded {self._deadline:.0f} s: exiting with the headline",
+            print(f"[bench] {self._what} exceeded {self._deadline:.0f} s: exiting with {self._rc}",
                   file=sys.stderr, flush=True)
             os._exit(self._rc)
 
     def finish(self) -> bool:
-        """True if the extras finished before the deadline (the caller prints the line)."""
+        """True if the phase finished before the deadline (the caller goes on)."""
         with self._lock:
             self._timer.cancel()
             if self._done:
                 return False
             self._done = True
             return True
+
+
+class _ExtrasWatchdog(_PhaseWatchdog):
+    """The after-headline extras' deadline: on expiry the finished headline ``line`` is printed
+    (extras marked as timed out) and every rank exits with the headline's status."""
+
+    def __init__(self, line: "dict | None", deadline_s: float, rc: int):
+        def make():
+            if line is None:
+                return None
+            out = dict(line)
+            msg = f"extras did not finish within {deadline_s:.0f} s (headline measured and verified before them)"
+            out["extras_error"] = msg
+            out["reduce_c_vector"] = {"error": msg}
+            return out
+        super().__init__("after-headline extras", deadline_s, rc, make)
+
+
+def _gbps(wl, K: int, elapsed: float) -> float:
+    return wl.bytes_total * K / elapsed / 1e9
+
+
+def _candidates(wl, ctx, args, fault, fused_ok: bool) -> dict:
+    """After-headline measurements of the other step protocols (extras; never the headline):
+
+    * ``fused_2lane_pipelined``: the fused finish over two stream lanes, consecutive independent
+      reductions overlapping (one step's tail with the next one's body);
+    * ``rccl_serial`` / ``rccl_pipelined``: the 1-element RCCL all-reduce combine, each step to
+      completion / the all-reduce of step i overlapping the local reduce of step i+1 (N > 1 only:
+      at world 1 the all-reduce enqueues no kernel).
+
+    Each is verified and its error words read; a failure is recorded, never raised. Fault site
+    ``extras`` injects into these steps."""
+    K, W = args.steps, min(args.warmup, 2)
+    todo = []
+    if fused_ok:
+        todo.append(("fused_2lane_pipelined", "fused", 2, False))
+    if ctx.world_size > 1:
+        todo += [("rccl_serial", "rccl", 1, True), ("rccl_pipelined", "rccl", 1, False)]
+    out = {}
+    for name, coll, lanes, serial in todo:
+        try:
+            wl.use_collective(coll, streams=lanes)
+            slots = wl.new_slots(W + K)
+            m = _measure(wl, slots, ctx, args, fault, serial=serial, warmup=W, site="extras")
+            err = wl.check()
+            ok = _verify_slots(wl, slots[:m["written"]], ctx)[0] and err is None
+            out[name] = {"gbps": round(_gbps(wl, K, m["elapsed"]), 3),
+                         "ms_per_step": round(m["elapsed"] / K * 1e3, 5), "launch": m["launch"], "verified": ok}
+            if err:
+                out[name]["error"] = err
+        except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
+            out[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
+            print(f"[bench] rank {ctx.rank}: candidate {name} failed: {e}", file=sys.stderr)
+    if ctx.world_size == 1:
+        out["rccl_serial"] = out["rccl_pipelined"] = {"gbps": None, "note": "world 1: a 1-rank RCCL all-reduce "
+                                                      "enqueues no kernel, so there is no combine to measure"}
+    return out
+
+
+def _tune_plan(wl, ctx, args, fault, kernel, cands) -> "tuple[KernelConfig, dict]":
+    """Streaming-kernel plan for this shard: the tuned default against the runners-up
+    (profiles/r2_plan/), each measured with the headline protocol (one lane, fused finish, serial,
+    graph replay, MAX over ranks) in two rounds, best of each (the first candidate of round 1 pays
+    for the GPU ramping its clocks). A candidate whose fused exchange or fan-in flagged an error is
+    out for good (-1, sticky)."""
+    T = max(4, args.tune_steps) if args.tune_steps else _auto_tune_steps(wl.bytes_total / ctx.world_size)
+    res = {}
+    for _round in range(2):
+        for b, u, w in cands:
+            key = "tuned default" if b == 0 else f"{b}x{u}x{w}"
+            if res.get(key, 0.0) < 0:
+                continue
+            wl.use_kernel(replace(kernel, block=b, unroll=u, wg_per_cu=w), streams=1)
+            mt = _measure(wl, wl.new_slots(2 + T), ctx, args, fault, serial=True, warmup=2, steps=T)
+            g = round(_gbps(wl, T, mt["elapsed"]), 3)
+            res[key] = -1.0 if wl.check() is not None else max(res.get(key, 0.0), g)
+    best = max(res, key=res.get)
+    b, u, w = next(c for c in cands if ("tuned default" if c[0] == 0 else f"{c[0]}x{c[1]}x{c[2]}") == best)
+    kernel = replace(kernel, block=b, unroll=u, wg_per_cu=w)
+    wl.use_kernel(kernel, streams=1)
+    return kernel, {"steps": T, "gbps": res, "chosen": best}
 
 
 def main(argv=None) -> int:
@@ -524,137 +657,92 @@ def main(argv=None) -> int:
         rc = run_vector(args, ctx, cfg, fault)
         pdist.shutdown(ctx)
         return rc
+    K, W = args.steps, args.warmup
+    dev = ctx.device
+    metric = METRIC if cfg.name == NORTH_STAR else f"reduction bandwidth (GB/s), {cfg.name}"
+
+    # ------------------------------------------------------------------ headline phase (deadline)
+    stage = {"now": "setup"}
+
+    def diag():
+        if not ctx.is_root:
+            return None
+        return {"metric": metric, "value": None, "unit": "GB/s", "n_gpus": ctx.world_size, "steps": K,
+                "warmup": W, "higher_is_better": True, "scaling": "strong", "verified": None,
+                "error": f"headline phase did not finish within {args.headline_deadline:.0f} s "
+                         f"(stage: {stage['now']}); no measurement", "native_source_hash": C.source_hash()}
+    watch = _PhaseWatchdog("headline phase", args.headline_deadline, 2, diag)
+
     kernel = KernelConfig(block=args.block, unroll=args.unroll, wg_per_cu=args.wg_per_cu,
                           groups=args.groups,
                           nontemporal=None if args.policy == "auto" else args.policy == "nt",
                           single_pass=not args.two_pass)
     collective = args.collective
-    fused_ok = ctx.device.type == "cuda" and not args.two_pass and cfg.op not in LOC_OPS and not args.local_only
+    fused_ok = dev.type == "cuda" and not args.two_pass and cfg.op not in LOC_OPS and not args.local_only
     if collective == "fused" and not fused_ok:
         raise SystemExit("--collective fused needs GPUs, the single-pass kernel and a non-LOC operator")
+    lanes = max(1, args.streams) if args.pipelined else 1
     # The cross-rank combine is issued even on one rank (--local-only skips it): N=1 runs the
     # exact step the N-GPU job runs.
-    wl = scalar_workload(cfg, ctx, kernel, streams=args.streams, collective="rccl" if collective == "auto" else collective,
-                         always_collective=not args.local_only, xrank_timeout_s=args.xrank_timeout).setup()
+    wl = scalar_workload(cfg, ctx, kernel, streams=lanes, collective="rccl" if collective == "auto" else collective,
+                         always_collective=not args.local_only, xrank_timeout_s=args.xrank_timeout,
+                         fault=fault).setup()
     collective_note = None
     if collective == "auto":
         collective = "rccl"
         if fused_ok:
+            stage["now"] = "fused self-check"
             collective_note = _try_fused(wl, ctx)
             collective = "fused" if collective_note is None else "rccl"
             if collective_note and ctx.is_root:
                 print(f"[bench] fused finish unavailable, using RCCL: {collective_note}", file=sys.stderr)
-    K, W = args.steps, args.warmup
-    dev = ctx.device
+            if lanes > 1:
+                wl.use_collective(collective, streams=lanes)
 
-    primary_serial = args.serial
-    tuning, tune_steps = None, 0
     plan_tuning = None
     explicit_plan = args.block or args.unroll or args.wg_per_cu or args.two_pass or args.policy != "auto"
-    if args.collective == "auto" and not primary_serial and not fault.enabled and dev.type == "cuda" \
-            and not explicit_plan and args.plan_tune and hasattr(wl, "use_kernel"):
+    if args.collective == "auto" and collective == "fused" and lanes == 1 and not fault.on("step") \
+            and dev.type == "cuda" and not explicit_plan and args.plan_tune and hasattr(wl, "use_kernel"):
         cands = _plan_candidates(wl.bytes_total / ctx.world_size, torch.empty((), dtype=cfg.dtype).element_size())
         if len(cands) > 1:
-            # Same protocol as the combine tuning below (graph replay, MAX over ranks, two rounds,
-            # best of each), one lane, with the combine the self-check settled on.
-            T = max(4, args.tune_steps) if args.tune_steps else _auto_tune_steps(wl.bytes_total / ctx.world_size)
-            plan_tuning = {}
-            for _round in range(2):
-                for b, u, w in cands:
-                    key = "tuned default" if b == 0 else f"{b}x{u}x{w}"
-                    wl.use_kernel(replace(kernel, block=b, unroll=u, wg_per_cu=w), streams=1)
-                    mt = _measure(wl, wl.new_slots(2 + T), ctx, args, fault, serial=False, warmup=2, steps=T)
-                    g = round(wl.bytes_total * T / mt["elapsed"] / 1e9, 3)
-                    if wl.check() is not None:  # a timed-out fused exchange: discard the point
-                        g = -1.0
-                    plan_tuning[key] = g if g < 0 else max(plan_tuning.get(key, 0.0), g)
-            best = max(plan_tuning, key=plan_tuning.get)
-            b, u, w = next(c for c in cands if ("tuned default" if c[0] == 0 else f"{c[0]}x{c[1]}x{c[2]}") == best)
-            kernel = replace(kernel, block=b, unroll=u, wg_per_cu=w)
-            wl.use_kernel(kernel, streams=args.streams)
-    if args.collective == "auto" and collective == "fused" and not primary_serial and not fault.enabled:
-        # Pick the headline combine by a short measurement of each candidate (same graph-replay
-        # protocol, MAX over ranks, so every rank picks the same): the in-kernel fused finish on one
-        # stream lane or two, or the RCCL all-reduce overlapped with the next local reduce.
-        # Two rounds, best of each candidate: the first candidate of round 1 otherwise pays for
-        # the GPU ramping its clocks (measured: -2 % at 8 GB on an otherwise equal kernel).
-        T = max(4, args.tune_steps) if args.tune_steps else _auto_tune_steps(wl.bytes_total / ctx.world_size)
-        tuning, tune_steps = {}, T
-        for _round in range(2):
-            for coll, nl in (("fused", 1), ("fused", 2), ("rccl", 1)):
-                key = f"{coll}_{nl}lane"
-                if tuning.get(key, 0.0) < 0:
-                    continue  # failed in round 1
-                wl.use_collective(coll, streams=nl)
-                mt = _measure(wl, wl.new_slots(2 + T), ctx, args, fault, serial=False, warmup=2, steps=T)
-                g = round(wl.bytes_total * T / mt["elapsed"] / 1e9, 3)
-                if coll == "fused" and wl.check() is not None:  # a timed-out exchange: never pick it
-                    g = -1.0
-                tuning[key] = g if g < 0 else max(tuning.get(key, 0.0), g)
-        best = max(tuning, key=tuning.get)
-        collective, nl = best.split("_")[0], int(best.split("_")[1][0])
-        wl.use_collective(collective, streams=nl)
-    slots = wl.new_slots(W + K)
-    m1 = _measure(wl, slots, ctx, args, fault, serial=primary_serial, warmup=W)
-    m1_lanes = len(wl.lanes) if wl.lanes else 1
-    m1_issues = wl.issues_collective
-    m1_err = wl.check()  # before any re-bind below drops the headline's channels
-    m2, serial_runs = None, {}
-    if not primary_serial and not wl.issues_collective and len(wl.lanes) <= 1:
-        m2 = m1  # one kernel per step (fused finish): the pipelined run IS the serial run
-    elif not primary_serial and not args.no_serial_measure:
-        # The honest per-reduction number: every step completes (local reduce AND cross-rank
-        # combine) before the next one starts (reduction.cpp:319-374 times each reduction to
-        # completion), on one stream lane. Reported next to the pipelined headline, with the
-        # faster combine for that protocol: when the fused finish passed its self-check both it
-        # (one kernel per step) and the RCCL all-reduce are measured, else the headline's combine.
-        # (Every slot is verified after all measurements — the torch reference pass between two
-        # timed runs cost the following one ~6 % — while a candidate's channel errors are read
-        # before the next re-bind drops its channels.)
-        fused_ok_here = tuning is not None and tuning.get("fused_1lane", -1.0) > 0
-        for c in (["fused", "rccl"] if fused_ok_here else [wl.collective]):
-            if len(wl.lanes) > 1 or c != wl.collective:
-                wl.use_collective(c, streams=1)
-            s2 = wl.new_slots(min(W, 2) + K)
-            # a capture that already failed (e.g. gloo collectives on GPU tensors) is not retried
-            m = _measure(wl, s2, ctx, args, fault, serial=True, warmup=min(W, 2),
-                         allow_graph=not m1["launch"].startswith("eager (graph capture failed"))
-            m["collective"], m["slots"] = c, s2
-            m["err"] = wl.check()  # before the next re-bind drops this candidate's channels
-            serial_runs[c] = m
-        m2 = min(serial_runs.values(), key=lambda m: m["elapsed"])
+            # kernel-only steps with bounded device waits: this cannot hang on a collective
+            stage["now"] = "plan tuning"
+            kernel, plan_tuning = _tune_plan(wl, ctx, args, fault, kernel, cands)
 
+    stage["now"] = "timed steps"
+    slots = wl.new_slots(W + K)
+    m = _measure(wl, slots, ctx, args, fault, serial=not args.pipelined, warmup=W)
+    m_lanes = len(wl.lanes) if wl.lanes else 1
+    m_issues = wl.issues_collective
+    err = wl.check()  # device error words (fan-in, fused finish), agreed over ranks
+    stage["now"] = "verification"
     verified = None
-    err = m1_err or next((m["err"] for m in serial_runs.values() if m["err"]), None)
     if not args.no_verify:
-        ok, ref = _verify_slots(wl, slots[:m1["written"]], ctx)
-        for m in serial_runs.values():
-            ok = _verify_slots(wl, m["slots"][:m["written"]], ctx)[0] and ok
+        ok, ref = _verify_slots(wl, slots[:m["written"]], ctx)
         verified = ok and err is None
         if not verified and ctx.is_root:
             print(f"[bench] VERIFICATION FAILED: {ref or ''} {err or ''}", file=sys.stderr)
     elif err is not None:
         verified = False
+    if err is not None and ctx.is_root:
+        print(f"[bench] device error: {err}", file=sys.stderr)
 
-    torch_gbps = None
-    if args.compare_torch and dev.type == "cuda":
-        torch_gbps = _time_torch_reduction(wl, K, W, ctx)
-    bytes_step = wl.bytes_total
-    elapsed = m1["elapsed"]
-    gbps = bytes_step * K / elapsed / 1e9
-    ms = elapsed / K * 1e3
-    lanes = m1_lanes
+    gbps = _gbps(wl, K, m["elapsed"])
+    ms = m["elapsed"] / K * 1e3
     line = None
     if ctx.is_root:
-        if m1_issues:
-            combine = "RCCL all-reduce of the 1-element partial (torch.distributed nccl)" \
-                if ctx.backend == "nccl" else f"{ctx.backend} all-reduce of the 1-element partial"
+        world1 = ctx.world_size == 1
+        if m_issues:
+            combine = ("none at world 1 (a 1-rank RCCL all-reduce is issued but enqueues no kernel)" if world1 else
+                       "RCCL all-reduce of the 1-element partial (torch.distributed nccl)" if ctx.backend == "nccl"
+                       else f"{ctx.backend} all-reduce of the 1-element partial")
         elif collective == "fused":
-            combine = "fused in-kernel cross-rank finish (IPC mailboxes over xGMI, csrc/include/mireduce/xrank.hpp)"
+            combine = ("none at world 1 (the fused finish is bound, exchanges nothing)" if world1 else
+                       "fused in-kernel cross-rank finish (IPC mailboxes over xGMI, csrc/include/mireduce/xrank.hpp)")
         else:
             combine = "none (--local-only)"
         line = {
-            "metric": METRIC if cfg.name == NORTH_STAR else f"reduction bandwidth (GB/s), {cfg.name}",
+            "metric": metric,
             "value": round(gbps, 3),
             "unit": "GB/s",
             "n_gpus": ctx.world_size,
@@ -674,18 +762,20 @@ def main(argv=None) -> int:
                 "parallelism": f"dp{ctx.world_size}",
                 "backend": ctx.backend,
                 "n_total_elements": wl.n_total,
-                "bytes_per_step": bytes_step,
+                "bytes_per_step": wl.bytes_total,
                 "op": cfg.op.upper(),
-                "collective": collective + (f" (auto; fused unavailable: {collective_note})" if collective_note else
-                                            " (auto-tuned)" if tuning is not None else
-                                            " (auto)" if args.collective == "auto" else ""),
+                "collective": collective,
+                "collective_choice": ("auto: fused finish passed its self-check on every rank"
+                                      if args.collective == "auto" and collective == "fused" else
+                                      f"auto; fused unavailable: {collective_note}" if collective_note else
+                                      "auto" if args.collective == "auto" else "explicit (--collective)"),
                 "cross_rank_combine": combine,
-                "overlap": "serial (each step completes before the next)" if primary_serial else
-                           ("pipelined (step i+1 local reduce || step i all-reduce)" if m1_issues
-                            else f"pipelined over {lanes} stream lanes" if lanes > 1 else
-                            "serial (one kernel per step: reduce + in-kernel combine)"),
-                "streams": lanes,
-                "launch": m1["launch"],
+                "overlap": ("serial: one stream lane, each global reduction (local reduce + combine) completes "
+                            "before the next starts (reduction.cpp:319-374)") if not args.pipelined else
+                           ("pipelined (step i+1 local reduce || step i all-reduce)" if m_issues
+                            else f"pipelined over {m_lanes} stream lanes"),
+                "streams": m_lanes,
+                "launch": m["launch"],
                 "kernel_plan": wl.reducer.last_plan if getattr(wl, "reducer", None) else getattr(wl, "plan", None),
             },
             "per_gpu_gbps": round(gbps / ctx.world_size, 3),
@@ -693,33 +783,43 @@ def main(argv=None) -> int:
             "baseline_source": cfg.baseline_source,
             "verified": verified,
             "native_ext": os.path.basename(native_path()),
+            "native_source_hash": C.source_hash(),
         }
-        if tuning is not None:
-            line["collective_tuning"] = {"steps": tune_steps, "gbps": tuning,
-                                         "chosen": f"{collective}_{lanes}lane"}
+        if err is not None:
+            line["device_error"] = err
+        if not args.pipelined:
+            line["serial_gbps"] = line["value"]
+            line["serial_ms_per_step"] = line["ms_per_step"]
+            line["serial_launch"] = m["launch"]
+            line["serial_collective"] = collective
         if plan_tuning is not None:
-            line["plan_tuning"] = {"gbps": plan_tuning, "chosen": max(plan_tuning, key=plan_tuning.get)}
-        if m2 is not None:
-            line["serial_gbps"] = round(bytes_step * K / m2["elapsed"] / 1e9, 3)
-            line["serial_ms_per_step"] = round(m2["elapsed"] / K * 1e3, 5)
-            line["serial_launch"] = m2["launch"]
-            line["serial_collective"] = m2.get("collective", collective)
-            if len(serial_runs) > 1:
-                line["serial_candidates_gbps"] = {c: round(bytes_step * K / m["elapsed"] / 1e9, 3)
-                                                  for c, m in serial_runs.items()}
-        if torch_gbps is not None:
-            line["torch_gbps"] = round(torch_gbps, 3)  # same data, torch's own reduction kernels
+            line["plan_tuning"] = plan_tuning
     rc = 0 if verified in (None, True) else 1
+    if not watch.finish():
+        return 2  # (unreachable: the watchdog ended the process)
+
+    # ------------------------------------------------------------------ extras (watchdog; never the headline)
+    guard = _ExtrasWatchdog(line, args.extras_deadline, rc)
+    extras = {}
+    if args.candidates and dev.type == "cuda" and hasattr(wl, "use_collective") and not args.pipelined:
+        extras["candidates"] = _candidates(wl, ctx, args, fault, collective == "fused")
+    if args.compare_torch and dev.type == "cuda":
+        extras["torch_gbps"] = round(_time_torch_reduction(wl, K, W, ctx), 3)
     if args.vector_extras and dev.type == "cuda" and cfg.name == NORTH_STAR:
-        # The extras run after the headline is final; a watchdog prints the headline (extras marked
-        # as timed out) and ends the process if they hang, so they can never cost the metric.
-        guard = _ExtrasWatchdog(line, args.extras_deadline, rc)
-        extras = _vector_extras(ctx)
-        if guard.finish() and line is not None:
-            line["reduce_c_vector"] = extras
-            print(json.dumps(line), flush=True)
-    elif line is not None:
+        extras["reduce_c_vector"] = _vector_extras(ctx)
+    if guard.finish() and line is not None:
+        cands = extras.get("candidates")
+        if cands is not None:
+            line["candidates"] = cands
+            pipe = [v["gbps"] for k, v in cands.items() if k.endswith("pipelined") and v.get("gbps")]
+            line["pipelined_gbps"] = max(pipe) if pipe else None
+            line["rccl_serial_gbps"] = cands.get("rccl_serial", {}).get("gbps")
+        for k in ("torch_gbps", "reduce_c_vector"):
+            if k in extras:
+                line[k] = extras[k]
         print(json.dumps(line), flush=True)
+    elif line is not None:  # the watchdog printed it
+        pass
     _sync(dev)
     pdist.shutdown(ctx)
     return rc

@@ -20,6 +20,7 @@
 #include <string>
 #include <vector>
 
+#include "mireduce/version.hpp"
 #include "mireduce/check.hpp"
 #include "mireduce/cli.hpp"
 #include "mireduce/device.hpp"
@@ -172,6 +173,10 @@ int main(int argc, char** argv) {
   } catch (const CliError& e) {
     std::fprintf(stderr, "%s\n", e.what());
     return EXIT_FAILURE;
+  }
+  if (args.has("version")) {  // build provenance (version.hpp)
+    std::printf("bandwidth_test (mireduce) native source %s\n", mireduce::source_hash());
+    return 0;
   }
   if (args.has("help")) {
     std::printf("bandwidth_test [--size=BYTES (default 2G)] [--iters=20] [--device=0] [--host] [--json=PATH]\n"

@@ -29,6 +29,7 @@
 #include <vector>
 #include <cmath>
 
+#include "mireduce/version.hpp"
 #include "mireduce/cli.hpp"
 #include "mireduce/fault.hpp"
 #include "mireduce/mt19937.hpp"
@@ -197,13 +198,17 @@ int main(int argc, char** argv) {
     MPI_Finalize();
     return EXIT_FAILURE;
   }
+  if (args.has("version")) {  // build provenance (version.hpp)
+    std::printf("reduce_mpi (mireduce) native source %s\n", mireduce::source_hash());
+    return 0;
+  }
   if (args.has("help")) {
     if (rank == 0) usage();
     MPI_Finalize();
     return EXIT_SUCCESS;
   }
   const std::set<std::string> known = {"ints", "doubles", "longs", "floats", "dtypes", "ops", "retries", "warmup",
-                                       "root", "collective", "timing", "verify", "json", "help", "inject-fault"};
+                                       "root", "collective", "timing", "verify", "json", "help", "version", "inject-fault"};
   for (const auto& u : args.unknown(known))
     if (rank == 0) std::fprintf(stderr, "warning: unknown flag --%s ignored\n", u.c_str());
 

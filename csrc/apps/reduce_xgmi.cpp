@@ -29,6 +29,7 @@
 #include <string>
 #include <vector>
 
+#include "mireduce/version.hpp"
 #include "mireduce/check.hpp"
 #include "mireduce/cli.hpp"
 #include "mireduce/comm.hpp"
@@ -53,7 +54,7 @@ constexpr uint64_t kNumDoubles = 256ull * 1024 * 1024;  // mpi/constants.h:2
 
 const std::set<std::string> kKnown = {"mode", "collective", "dtypes", "ops", "ints", "doubles", "longs", "floats",
                                       "n", "retries", "warmup", "iters", "root", "json", "graph", "mt19937",
-                                      "noverify", "seed", "help", "unroll", "block", "wg-per-cu", "policy",
+                                      "noverify", "seed", "help", "version", "unroll", "block", "wg-per-cu", "policy",
                                       "units", "timeout", "trace", "single-process", "inject-fault",
                                       "direct-grid"};
 
@@ -377,6 +378,8 @@ bool run_scalar(Ctx& c, const std::vector<DType>& dtypes, const std::vector<Op>&
         restore_element(saved);
         if (channel && channel->error())
           throw Error("fused: a peer's partial never arrived (device-side wait timed out after --timeout)");
+        if (ws.error())  // polled fan-in reached its wait bound: the results are poisoned
+          throw Error("polled fan-in: a launch reached its wait bound (device-side error word set)");
         Json j;
         j.set("n_total", n).set("count_per_rank", count).set("retry", x_);
         bool vok = true;
@@ -543,6 +546,7 @@ bool run_single_process(Ctx& c, const std::vector<DType>& dtypes, const std::vec
           } else {
             vok = std::memcmp(got, expect, as) == 0;
           }
+          for (int i = 0; i < ndev; ++i) vok = vok && d[i].ws->error() == 0;  // fan-in error words
           ok = ok && vok;
           j.set("verified", vok);
         }
@@ -589,6 +593,10 @@ int main(int argc, char** argv) {
   } catch (const CliError& e) {
     std::fprintf(stderr, "%s\n", e.what());
     return EXIT_FAILURE;
+  }
+  if (args.has("version")) {  // build provenance (version.hpp)
+    std::printf("reduce_xgmi (mireduce) native source %s\n", mireduce::source_hash());
+    return 0;
   }
   if (args.has("help")) {
     usage();

@@ -31,6 +31,7 @@
 #include <thread>
 #include <vector>
 
+#include "mireduce/version.hpp"
 #include "mireduce/arg_reduce.hpp"
 #include "mireduce/check.hpp"
 #include "mireduce/cli.hpp"
@@ -77,7 +78,7 @@ struct Options {
 
 const std::set<std::string> kKnown = {
     "method", "type", "n", "threads", "kernel", "maxblocks", "cpufinal", "cputhresh", "shmoo",
-    "device", "qatest", "noprompt", "prompt", "help", "quiet", "iterations", "acc", "unroll",
+    "device", "qatest", "noprompt", "prompt", "help", "version", "quiet", "iterations", "acc", "unroll",
     "wg-per-cu", "policy", "pattern", "seed", "fill", "noverify", "json", "log", "master-log",
     "countdown", "shmoo-max", "trace", "timing", "cold", "arg"};
 
@@ -132,8 +133,19 @@ struct Buffers {
   DeviceBuffer flush;                      // --cold: cache-eviction scratch
   std::vector<unsigned char> host;  // input copy (for CPU verification)
   void* pinned = nullptr;           // --cpufinal partials landing zone
+  size_t pinned_bytes = 0;
   ~Buffers() {
     if (pinned) (void)hipHostFree(pinned);
+  }
+  // Grow the landing zone to hold `bytes` (stream-synchronised by the caller first). The ladder's
+  // first pass leaves as many partials as it launches blocks, and kernels 0..5 have no --maxblocks
+  // cap: e.g. --kernel=0 --threads=64 --cpufinal leaves n/64 partials.
+  void ensure_pinned(size_t bytes) {
+    if (bytes <= pinned_bytes) return;
+    if (pinned) HIP_CHECK(hipHostFree(pinned));
+    pinned = nullptr;
+    HIP_CHECK(hipHostMalloc(&pinned, bytes, hipHostMallocDefault));
+    pinned_bytes = bytes;
   }
 };
 
@@ -164,7 +176,12 @@ struct Runner {
 
   // The reference's host fold of what the relaunch loop left (reduction.cpp:332,362-370).
   bool host_fold_partials(const void* partials, uint64_t left, unsigned char* host_out) {
-    HIP_CHECK(hipMemcpyAsync(b.pinned, partials, left * dtype_size(o.acc), hipMemcpyDeviceToHost, s));
+    const size_t bytes = left * dtype_size(o.acc);
+    if (bytes > b.pinned_bytes) {  // (only the warm-up call can grow it: same n, same plan after)
+      HIP_CHECK(hipStreamSynchronize(s));
+      b.ensure_pinned(bytes);
+    }
+    HIP_CHECK(hipMemcpyAsync(b.pinned, partials, bytes, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     cpu_fold(b.pinned, left, o.acc, o.op, host_out);
     host_folded = left;
@@ -358,7 +375,7 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
   b.in.allocate(std::max<uint64_t>(o.n, 1) * es);
   b.out.allocate(8);
   b.partials.allocate(2 * static_cast<size_t>(std::max(ws.max_grid(), 1 << 16)) * 8);  // ping-pong passes
-  HIP_CHECK(hipHostMalloc(&b.pinned, static_cast<size_t>(std::max(ws.max_grid(), 1 << 16)) * 8, hipHostMallocDefault));
+  b.ensure_pinned(static_cast<size_t>(std::max(ws.max_grid(), 1 << 16)) * 8);
 
   FillSpec fs;
   fs.pattern = o.pattern;
@@ -379,12 +396,19 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
   L.log(kLogBoth, "%d blocks\n\n", r.plan.grid);
 
   Timing t = time_iterations(r, o.n, o.iterations);
+  // device-side error word of the polled fan-in (a finisher reached its wait bound: results poisoned)
+  const unsigned fan_err = ws.error();
+  if (fan_err) {
+    L.log(kLogBoth, "FAN-IN ERROR: a launch reached the polled fan-in's wait bound (result poisoned)\n");
+    ws.reset(s);
+    HIP_CHECK(hipStreamSynchronize(s));
+  }
   const double secs = t.avg_ms * 1e-3;
   const double bytes = static_cast<double>(o.n) * es;
   L.log(kLogBoth | kLogMaster, "%s\n", throughput_line(secs > 0 ? 1.0e-9 * bytes / secs : 0.0, secs, o.n, 1,
                                                        static_cast<unsigned>(r.plan.block)).c_str());
 
-  bool ok = true;
+  bool ok = fan_err == 0;
   unsigned char cpu[8] = {0};
   double tol = 0;
   bool checked = false;
@@ -398,9 +422,9 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
       const bool summed = o.op == Op::Sum || o.op == Op::SumSq;
       const double abs_sum = o.op == Op::SumSq ? std::fabs(c) : (summed ? cpu_abs_sum(b.host.data(), o.n, o.dtype) : 0.0);
       tol = summed ? sum_tolerance(o.dtype, o.acc, o.n, abs_sum) : 0.0;
-      ok = summed ? std::fabs(g - c) <= tol : g == c;
+      ok = ok && (summed ? std::fabs(g - c) <= tol : g == c);
     } else {
-      ok = acc_as_int64(t.result, o.acc) == acc_as_int64(cpu, o.acc);
+      ok = ok && acc_as_int64(t.result, o.acc) == acc_as_int64(cpu, o.acc);
     }
   } else if (o.verify) {
     // Huge device-filled arrays (no host copy), independent oracles:
@@ -414,9 +438,9 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
       if (summed_f && o.acc == DType::Float32) {
         const double g = acc_as_double(t.result, o.acc), c = acc_as_double(cpu, o.acc);
         tol = sum_tolerance(o.dtype, o.acc, o.n, std::fabs(c));
-        ok = std::fabs(g - c) <= tol;
+        ok = ok && std::fabs(g - c) <= tol;
       } else {
-        ok = std::memcmp(t.result, cpu, dtype_size(o.acc)) == 0;  // exact: integer-valued terms
+        ok = ok && std::memcmp(t.result, cpu, dtype_size(o.acc)) == 0;  // exact: integer-valued terms
       }
     } else {
       Options o2 = o;
@@ -434,9 +458,9 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
       if (summed_f) {
         const double g = acc_as_double(t.result, o.acc), c = acc_as_double(cpu, o.acc);
         tol = 1e-9 * std::fabs(c) + 1e-12;
-        ok = std::fabs(g - c) <= tol;
+        ok = ok && std::fabs(g - c) <= tol;
       } else {
-        ok = std::memcmp(t.result, cpu, dtype_size(o.acc)) == 0;
+        ok = ok && std::memcmp(t.result, cpu, dtype_size(o.acc)) == 0;
       }
     }
   }
@@ -456,10 +480,11 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
         .set("iterations", o.iterations).set("cold", o.cold).set("timing", o.batch_timing && !o.cold ? "batch" : "per-iter").set("avg_ms", t.avg_ms).set("median_ms", st.median).set("min_ms", st.min)
         .set("max_ms", st.max).set("std_ms", st.stddev).set("gb_per_s", secs > 0 ? bytes / secs / kGB : 0.0)
         .set("gib_per_s", secs > 0 ? bytes / secs / kGiB : 0.0).set("bytes_per_GB", kGB)
-        .set("gpu_result", acc_as_double(t.result, o.acc)).set("verified", checked ? ok : true)
+        .set("gpu_result", acc_as_double(t.result, o.acc)).set("verified", checked ? ok : fan_err == 0)
         .set("tolerance", tol).set("device", di.name).set("arch", di.arch).set("cus", di.cus)
         .set("passes", r.passes).set("host_folded", r.host_folded).set("cputhresh", o.cputhresh)
-        .set("oracle", checked ? oracle : std::string("none")).set("iteration_ms", t.ms);
+        .set("oracle", checked ? oracle : std::string("none")).set("fanin_error", static_cast<int64_t>(fan_err))
+        .set("iteration_ms", t.ms);
     j.write_file(o.json);
   }
   return ok;
@@ -509,6 +534,10 @@ int main(int argc, char** argv) {
   } catch (const CliError& e) {
     std::fprintf(stderr, "%s\n", e.what());
     return EXIT_FAILURE;
+  }
+  if (args.has("version")) {  // build provenance (version.hpp)
+    std::printf("reduction (mireduce) native source %s\n", mireduce::source_hash());
+    return 0;
   }
   if (args.has("help")) {
     usage();

@@ -34,6 +34,13 @@ struct ReduceConfig {
   // Fused cross-rank finish: XrankChannel::device_desc() (xrank.hpp). The launch then writes the
   // fold over every rank's partial into out (single-pass only).
   const void* xrank = nullptr;
+  // Polled fan-in wait bound in wall-clock ticks (0: ~10.7 s). Reaching it sets the workspace's
+  // sticky error and poisons the result (Workspace::error()).
+  uint64_t fanin_bound_ticks = 0;
+  // Test hook (failure-path tests only): workgroup `debug_delay_wg` sleeps `debug_delay_ticks`
+  // wall-clock ticks before publishing its partial (-1: none).
+  int debug_delay_wg = -1;
+  uint64_t debug_delay_ticks = 0;
 };
 
 // What the planner chose (printed by the apps, recorded in JSON sidecars).
@@ -54,9 +61,10 @@ struct LaunchPlan {
   uint64_t tail = 0;   // scalar elements after the body
 };
 
-// Device scratch for one reduction stream: per-workgroup partials, per-group partials and the
-// arrival tickets (zeroed once; the last arriver of each launch resets them). One Workspace
-// must not be used by two concurrently running reductions.
+// Device scratch for one reduction stream: per-workgroup partials, per-group partials, the
+// arrival tickets (zeroed once; the last arriver of each launch resets them), the polled fan-in's
+// epoch-tagged slots and its state words (epoch, sticky error). One Workspace must not be used by
+// two concurrently running reductions.
 class Workspace {
  public:
   explicit Workspace(int device = -1, int max_grid = 16384);
@@ -71,7 +79,13 @@ class Workspace {
   void* group_partials() const { return group_partials_; }
   unsigned* tickets() const { return tickets_; }
   uint64_t* slots() const { return slots_; }
-  // Re-zero the tickets and fan-in slots (only needed after an aborted launch).
+  unsigned* fan() const { return fan_; }
+  // Sticky error of the polled fan-in (synchronous read: call after the launches completed).
+  // Non-zero: some launch's finisher reached its wait bound; that launch and every later one
+  // wrote a poisoned result (NaN, or the identity for integers) until reset().
+  unsigned error() const;
+  // Re-zero the tickets, fan-in slots and the sticky error (after an error or an aborted launch;
+  // stream-ordered: no launch on this workspace may be running on another stream).
   void reset(hipStream_t stream);
 
  private:
@@ -82,6 +96,7 @@ class Workspace {
   void* group_partials_ = nullptr;
   unsigned* tickets_ = nullptr;
   uint64_t* slots_ = nullptr;  // polled fan-in: [max_grid][2] tagged words, uncached
+  unsigned* fan_ = nullptr;    // polled fan-in: [0] epoch, [1] sticky error, uncached
 };
 
 constexpr int kTicketStride = 32;  // one counter per 128-byte line
@@ -110,6 +125,8 @@ class BoundReduce {
   // `out` (optional) redirects the result to another accumulator slot for this launch.
   void launch(hipStream_t stream, void* out = nullptr) const;
   const LaunchPlan& plan() const;
+  // The bound workspace's sticky fan-in error (Workspace::error()).
+  unsigned error() const;
 
  private:
   struct Impl;

@@ -199,6 +199,8 @@ Workspace::Workspace(int device, int max_grid) : max_grid_(max_grid) {
   MIREDUCE_HIP_THROW(hipExtMallocWithFlags(reinterpret_cast<void**>(&slots_), static_cast<size_t>(max_grid) * 16,
                                            hipDeviceMallocUncached));
   MIREDUCE_HIP_THROW(hipMemset(slots_, 0, static_cast<size_t>(max_grid) * 16));
+  MIREDUCE_HIP_THROW(hipExtMallocWithFlags(reinterpret_cast<void**>(&fan_), 256, hipDeviceMallocUncached));
+  MIREDUCE_HIP_THROW(hipMemset(fan_, 0, 256));
   MIREDUCE_HIP_THROW(hipDeviceSynchronize());
   MIREDUCE_HIP_THROW(hipSetDevice(prev));
 }
@@ -208,12 +210,26 @@ Workspace::~Workspace() {
   (void)hipFree(group_partials_);
   (void)hipFree(tickets_);
   (void)hipFree(slots_);
+  (void)hipFree(fan_);
+}
+
+unsigned Workspace::error() const {
+  unsigned v = 0;
+  int prev = 0;
+  MIREDUCE_HIP_THROW(hipGetDevice(&prev));
+  MIREDUCE_HIP_THROW(hipSetDevice(device_));
+  const hipError_t e = hipMemcpy(&v, fan_ + 1, sizeof v, hipMemcpyDeviceToHost);
+  (void)hipSetDevice(prev);
+  MIREDUCE_HIP_THROW(e);
+  return v;
 }
 
 void Workspace::reset(hipStream_t stream) {
   const size_t tbytes = static_cast<size_t>(kMaxGroups + 1) * kTicketStride * sizeof(unsigned);
   MIREDUCE_HIP_THROW(hipMemsetAsync(tickets_, 0, tbytes, stream));
   MIREDUCE_HIP_THROW(hipMemsetAsync(slots_, 0, static_cast<size_t>(max_grid_) * 16, stream));
+  // the epoch may stay: every slot is 0 now, and epochs start at 1
+  MIREDUCE_HIP_THROW(hipMemsetAsync(fan_ + 1, 0, sizeof(unsigned), stream));
 }
 
 LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cfg, int num_cus,
@@ -263,8 +279,11 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   return p;
 }
 
-static kern::Args make_args(const void* in, const LaunchPlan& p, DType t) {
+static kern::Args make_args(const void* in, const LaunchPlan& p, DType t, const ReduceConfig& cfg) {
   kern::Args a{};
+  a.fan_bound = cfg.fanin_bound_ticks ? cfg.fanin_bound_ticks : kern::kFanBoundTicks;
+  a.delay_wg = cfg.debug_delay_wg;
+  a.delay_ticks = cfg.debug_delay_ticks;
   a.head_ptr = in;
   a.body = static_cast<const char*>(in) + p.head * dtype_size(t);
   a.head = p.head;
@@ -281,7 +300,7 @@ LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out
   MIREDUCE_REQUIRE(c >= 0, "unsupported (dtype, op, accumulator) combination");
   MIREDUCE_REQUIRE(out != nullptr, "output pointer is null");
   LaunchPlan p = plan_reduce(in, n, t, cfg, ws.num_cus(), ws.max_grid());
-  kern::Args a = make_args(in, p, t);
+  kern::Args a = make_args(in, p, t, cfg);
   a.partials = ws.partials();
   a.group_partials = ws.group_partials();
   a.tickets = ws.tickets();
@@ -289,6 +308,7 @@ LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out
   a.groups = p.groups;
   a.flat = p.flat ? 1 : 0;
   a.slots = p.poll ? ws.slots() : nullptr;
+  a.fan = ws.fan();
   a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
   const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0];
   fn(a, p.grid, stream);
@@ -303,6 +323,7 @@ struct BoundReduce::Impl {
   LaunchPlan plan;
   Op op;
   DType acc;
+  const Workspace* ws;
 };
 
 BoundReduce::BoundReduce(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
@@ -312,7 +333,7 @@ BoundReduce::BoundReduce(const void* in, size_t n, DType t, Op op, DType acc, vo
   MIREDUCE_REQUIRE(c >= 0, "unsupported (dtype, op, accumulator) combination");
   MIREDUCE_REQUIRE(out != nullptr, "output pointer is null");
   const LaunchPlan p = plan_reduce(in, n, t, cfg, ws.num_cus(), ws.max_grid());
-  kern::Args a = make_args(in, p, t);
+  kern::Args a = make_args(in, p, t, cfg);
   a.partials = ws.partials();
   a.group_partials = ws.group_partials();
   a.tickets = ws.tickets();
@@ -320,9 +341,10 @@ BoundReduce::BoundReduce(const void* in, size_t n, DType t, Op op, DType acc, vo
   a.groups = p.groups;
   a.flat = p.flat ? 1 : 0;
   a.slots = p.poll ? ws.slots() : nullptr;
+  a.fan = ws.fan();
   a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
   impl_ = new Impl{a, table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0],
-                   p, op, acc};
+                   p, op, acc, &ws};
 }
 
 BoundReduce::~BoundReduce() { delete impl_; }
@@ -337,6 +359,8 @@ void BoundReduce::launch(hipStream_t stream, void* out) const {
 
 const LaunchPlan& BoundReduce::plan() const { return impl_->plan; }
 
+unsigned BoundReduce::error() const { return impl_->ws->error(); }
+
 LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, void* partials,
                            int max_grid, int num_cus, hipStream_t stream, const ReduceConfig& cfg) {
   const int c = combo_index(op, t, acc);
@@ -345,7 +369,7 @@ LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, 
   c2.single_pass = false;
   c2.xrank = nullptr;
   LaunchPlan p = plan_reduce(in, n, t, c2, num_cus, max_grid);
-  kern::Args a = make_args(in, p, t);
+  kern::Args a = make_args(in, p, t, c2);
   a.partials = partials;
   a.groups = 0;
   const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0];

@@ -29,6 +29,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "mireduce/check.hpp"
@@ -78,15 +79,29 @@ struct Args {
   int flat;              // 1: group last-arrivers only count; the final arriver folds every partial
   int contig;            // 1: workgroup b streams one contiguous run of tiles; 0: tiles b, b+grid, ...
   const XrankDesc* xrank;  // non-null: fold the ranks' partials in-kernel before writing out (xrank.hpp)
-  uint64_t* slots;         // non-null: polled fan-in (no tickets), [gridDim.x][2] flag-tagged words
+  uint64_t* slots;         // non-null: polled fan-in (no tickets), [gridDim.x][2] epoch-tagged words
+  unsigned* fan;           // polled fan-in state (Workspace): [0] epoch = finished launches, [1] sticky error
+  uint64_t fan_bound;      // polled fan-in: finisher's wait bound in wall-clock ticks
   int balance;             // 1 (interleaved split): whole rounds of tiles, then the leftover < grid
                            // tiles split evenly over ALL workgroups (no one-tile tail on a few)
+  int delay_wg;            // test hook (ReduceConfig::debug_delay_wg): this workgroup sleeps
+  uint64_t delay_ticks;    // delay_ticks before publishing its partial; -1 = none
 };
 
-// Polled fan-in: a published partial is two 8-byte words (tag << 32 | 32 data bits); a cleared
-// slot is 0. The finisher clears every slot it consumed, so each launch starts from zeros.
-constexpr uint64_t kSlotTag = 0xA5C3E1F7ull << 32;
+// Polled fan-in: a published partial is two 8-byte words (epoch << 32 | 32 data bits), where the
+// epoch is this launch's number (Workspace fan[0] + 1, read by every workgroup at its start and
+// advanced by the finisher after it has consumed every slot): a slot is valid for exactly one
+// launch, so nothing needs clearing, and a late store from an earlier (timed-out) launch never
+// matches. Reaching the bound sets the sticky error fan[1] and poisons the result (NaN / identity)
+// instead of folding unpublished slots; Workspace::error() reports it, Workspace::reset() clears it.
 constexpr int kPollSlots = 4;  // slots one finisher lane polls per round (grid <= 4 x BLOCK)
+constexpr uint64_t kFanBoundTicks = 1ull << 30;  // ~10.7 s of the 100 MHz wall clock
+
+template <class AccT>
+__device__ __forceinline__ AccT poisoned() {
+  if constexpr (std::is_floating_point_v<AccT>) return __builtin_nan("");
+  else return AccT(0);
+}
 
 template <class T>
 __device__ __forceinline__ uint64_t to_bits64(T v) {
@@ -202,6 +217,13 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) acc[u] = OpT::template identity<AccT>();
 
+  // Polled fan-in epoch of this launch: the load is issued before the streaming body and its value
+  // first used after it, so its latency hides under the body's first loads (one VGPR; the ISA test
+  // pins that no wait sits between it and the body). Every workgroup reads it before the finisher
+  // can advance it: the finisher advances fan[0] only after every slot holds this epoch.
+  const bool polled = a.slots && gridDim.x > 1;
+  const unsigned fan_raw = polled ? __hip_atomic_load(a.fan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+
   const V* __restrict__ vin = static_cast<const V*>(a.body);
   constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
   const uint64_t ntiles = a.nvec / kTile;
@@ -313,21 +335,32 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   // instead of store, drain, ticket (x2) and a load round. Slots live in uncached memory, so
   // polls always see the other XCDs' stores.
   if (a.slots) {
+    unsigned fan_e = __builtin_amdgcn_readfirstlane(fan_raw) + 1u;
+    if (fan_e == 0) fan_e = 1;  // 0 is the tag of a zeroed slot
+    const uint64_t tag = static_cast<uint64_t>(fan_e) << 32;
     if (threadIdx.x == 0) {
+      if (static_cast<int>(blockIdx.x) == a.delay_wg) {  // test hook: a slow workgroup
+        const uint64_t d0 = static_cast<uint64_t>(wall_clock64());
+        while (static_cast<uint64_t>(wall_clock64()) - d0 < a.delay_ticks) __builtin_amdgcn_s_sleep(127);
+      }
       const uint64_t bits = to_bits64(v);
       uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(blockIdx.x);
-      __hip_atomic_store(sl, kSlotTag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(sl + 1, kSlotTag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sl, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sl + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (blockIdx.x != gridDim.x - 1) return;
-    // The finisher: start the cross-rank descriptor loads now, they land while it polls.
+    // The finisher: start the cross-rank descriptor loads and the sticky-error load now, they land
+    // while it polls.
     XrankLane xl{};
     if (a.xrank && threadIdx.x < 64) xl = xrank_prefetch(a.xrank, xr_epoch, xr_err);
+    const unsigned fan_err = __hip_atomic_load(a.fan + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     AccT t = OpT::template identity<AccT>();
     // Bounded like every device-side wait here (all workgroups of this launch always publish, so
-    // the bound is never reached by a correct launch; it only keeps a misuse from hanging the GPU).
+    // a correct launch never reaches the bound; it keeps a stalled or misused launch from hanging
+    // the GPU, and reaching it is reported, never folded into a plausible-looking result).
     const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
-    constexpr uint64_t kBound = 1ull << 30;  // ~10 s of the 100 MHz wall clock
+    const uint64_t kBound = a.fan_bound;
+    bool late = false;
     if (gridDim.x <= kPollSlots * BLOCK) {
       // Each lane polls ALL its slots (<= kPollSlots) every round, so the finish costs one poll
       // round trip after the last store lands, not one per slot.
@@ -347,40 +380,47 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
         }
 #pragma unroll
         for (int k = 0; k < kPollSlots; ++k)
-          if ((pending & (1u << k)) && (lo[k] & ~0xffffffffull) == kSlotTag && (hi[k] & ~0xffffffffull) == kSlotTag)
+          if ((pending & (1u << k)) && (lo[k] & ~0xffffffffull) == tag && (hi[k] & ~0xffffffffull) == tag)
             pending &= ~(1u << k);
-        if (!pending || static_cast<uint64_t>(wall_clock64()) - t0 > kBound) break;
+        if (!pending) break;
+        if (static_cast<uint64_t>(wall_clock64()) - t0 > kBound) {
+          late = true;
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
       }
 #pragma unroll
-      for (int k = 0; k < kPollSlots; ++k) {  // fold in slot order (deterministic), then clear
-        if (threadIdx.x + k * BLOCK < gridDim.x) {
+      for (int k = 0; k < kPollSlots; ++k)  // fold in slot order (deterministic)
+        if (threadIdx.x + k * BLOCK < gridDim.x)
           t = OpT::apply(t, from_bits64<AccT>((lo[k] & 0xffffffffull) | (hi[k] << 32)));
-          uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(threadIdx.x + k * BLOCK);
-          __hip_atomic_store(sl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(sl + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
     } else {  // very large grids (user --maxblocks / wg-per-cu): slot by slot
       for (unsigned i = threadIdx.x; i < gridDim.x; i += BLOCK) {
-        uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(i);
+        const uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(i);
         uint64_t l, h;
         for (;;) {
           l = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           h = __hip_atomic_load(sl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((l & ~0xffffffffull) == kSlotTag && (h & ~0xffffffffull) == kSlotTag) break;
-          if (static_cast<uint64_t>(wall_clock64()) - t0 > kBound) break;
+          if ((l & ~0xffffffffull) == tag && (h & ~0xffffffffull) == tag) break;
+          if (late || static_cast<uint64_t>(wall_clock64()) - t0 > kBound) {
+            late = true;
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
         }
         t = OpT::apply(t, from_bits64<AccT>((l & 0xffffffffull) | (h << 32)));
-        __hip_atomic_store(sl, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(sl + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+    // Any lane past the bound (or an earlier launch's sticky error) poisons this launch's result.
+    const bool bad = __syncthreads_or(late) || fan_err != 0;
     t = block_reduce<OpT, AccT, BLOCK>(t, lds);
     if (threadIdx.x < 64) {
-      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xl, t);
-      if (threadIdx.x == 0) *static_cast<AccT*>(a.out) = t;
+      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xl, bad ? poisoned<AccT>() : t);
+      if (threadIdx.x == 0) {
+        *static_cast<AccT*>(a.out) = bad ? poisoned<AccT>() : t;
+        if (bad) __hip_atomic_fetch_or(a.fan + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // every slot of this launch has been read (or abandoned): the next launch's epoch
+        __hip_atomic_store(a.fan, fan_e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     return;
   }

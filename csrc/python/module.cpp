@@ -24,6 +24,7 @@
 #include "mireduce/reduce_many.hpp"
 #include "mireduce/trace.hpp"
 #include "mireduce/types.hpp"
+#include "mireduce/version.hpp"
 #include "mireduce/xrank.hpp"
 
 namespace py = pybind11;
@@ -97,6 +98,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("OP_SUMSQ") = static_cast<int>(Op::SumSq);
   m.attr("OP_AMAX") = static_cast<int>(Op::AbsMax);
   m.attr("TICKET_STRIDE") = kTicketStride;
+  // Build provenance: hash of the csrc tree this module was built from (tools/source_hash.py).
+  m.def("source_hash", [] { return std::string(source_hash()); });
 
   // Read and clear the calling thread's sticky HIP error (e.g. left behind by an aborted
   // stream capture, which would otherwise fail the next unrelated kernel-launch check).
@@ -162,7 +165,9 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("num_cus", &Workspace::num_cus)
       .def_property_readonly("max_grid", &Workspace::max_grid)
       .def_property_readonly("partials_ptr", [](const Workspace& w) { return reinterpret_cast<uintptr_t>(w.partials()); })
-      .def("reset", [](Workspace& w, uintptr_t stream) { w.reset(as_stream(stream)); }, py::arg("stream") = 0);
+      .def("reset", [](Workspace& w, uintptr_t stream) { w.reset(as_stream(stream)); }, py::arg("stream") = 0)
+      .def("error", &Workspace::error)
+      .def_property_readonly("fan_ptr", [](const Workspace& w) { return reinterpret_cast<uintptr_t>(w.fan()); });
 
   // Prepared launch for per-step loops: launch(stream) is one positional-argument call.
   py::class_<BoundReduce>(m, "BoundReduce")
@@ -180,7 +185,8 @@ PYBIND11_MODULE(_C, m) {
            py::arg("single_pass") = true, py::arg("pipeline") = -1, py::arg("xrank") = 0, py::keep_alive<1, 2>())
       .def("launch", [](const BoundReduce& b, uintptr_t stream, uintptr_t out) { b.launch(as_stream(stream), as_ptr<void>(out)); },
            py::arg("stream"), py::arg("out_ptr") = 0)
-      .def_property_readonly("plan", [](const BoundReduce& b) { return plan_dict(b.plan()); });
+      .def_property_readonly("plan", [](const BoundReduce& b) { return plan_dict(b.plan()); })
+      .def("error", &BoundReduce::error);
 
   // Fused cross-rank finish (xrank.hpp): exchange handle() bytes with every rank, connect(), then
   // pass desc_ptr as BoundReduce(..., xrank=desc_ptr).
@@ -252,19 +258,23 @@ PYBIND11_MODULE(_C, m) {
       "reduce",
       [](Workspace& ws, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out,
          uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks, int groups,
-         int policy, bool single_pass, int pipeline) {
+         int policy, bool single_pass, int pipeline, uint64_t fanin_bound_ticks, int debug_delay_wg,
+         uint64_t debug_delay_ticks) {
+        ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline);
+        cfg.fanin_bound_ticks = fanin_bound_ticks;
+        cfg.debug_delay_wg = debug_delay_wg;
+        cfg.debug_delay_ticks = debug_delay_ticks;
         const LaunchPlan p = reduce(as_ptr<const void>(in), n, static_cast<DType>(dtype),
                                     static_cast<Op>(op), static_cast<DType>(acc),
-                                    as_ptr<void>(out), ws, as_stream(stream),
-                                    make_cfg(block, unroll, wg_per_cu, max_blocks, groups,
-                                             policy, single_pass, pipeline));
+                                    as_ptr<void>(out), ws, as_stream(stream), cfg);
         return plan_dict(p);
       },
       py::arg("ws"), py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"),
       py::arg("acc"), py::arg("out_ptr"), py::arg("stream") = 0, py::arg("block") = 0,
       py::arg("unroll") = 0, py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0,
       py::arg("groups") = 0, py::arg("policy") = -1, py::arg("single_pass") = true,
-      py::arg("pipeline") = -1);
+      py::arg("pipeline") = -1, py::arg("fanin_bound_ticks") = 0, py::arg("debug_delay_wg") = -1,
+      py::arg("debug_delay_ticks") = 0);
 
   m.def(
       "plan",

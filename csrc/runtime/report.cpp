@@ -1,5 +1,6 @@
 // Output formats and statistics; see report.hpp.
 #include "mireduce/report.hpp"
+#include "mireduce/version.hpp"
 
 #include <algorithm>
 #include <cinttypes>
@@ -97,7 +98,16 @@ std::string Json::str() const {
 bool Json::write_file(const std::string& path) const {
   std::ofstream f(path, std::ios::app);
   if (!f) return false;
-  f << str() << "\n";
+  // every sidecar record carries the build provenance (version.hpp)
+  bool has_hash = false;
+  for (const auto& kv : kv_) has_hash = has_hash || kv.first == "native_source_hash";
+  if (has_hash) {
+    f << str() << "\n";
+  } else {
+    Json j = *this;
+    j.set("native_source_hash", std::string(source_hash()));
+    f << j.str() << "\n";
+  }
   return static_cast<bool>(f);
 }
 

@@ -141,7 +141,7 @@ class ScalarReduction:
                  kernel: Optional[KernelConfig] = None, seed: int = 0x5EED,
                  acc_dtype: Optional[torch.dtype] = None, streams: int = 1,
                  collective: str = "rccl", always_collective: bool = False,
-                 xrank_timeout_s: float = 10.0):
+                 xrank_timeout_s: float = 10.0, fault=None):
         if cfg.mode != "scalar":
             raise ValueError("ScalarReduction needs a scalar-mode config")
         if collective not in COLLECTIVES:
@@ -154,6 +154,7 @@ class ScalarReduction:
         self.collective = collective
         self.always_collective = bool(always_collective)
         self.xrank_timeout_s = xrank_timeout_s
+        self.fault = fault  # FaultInjector: a "mailbox" fault fails this rank's channel creation
         self.x: Optional[torch.Tensor] = None
         self.offset = 0
         self.count = 0
@@ -199,7 +200,8 @@ class ScalarReduction:
             for k in range(self.n_streams):
                 stream = torch.cuda.current_stream(dev) if self.n_streams == 1 else torch.cuda.Stream(dev)
                 reducer = Reducer(dev, config=self.kernel)
-                ch = open_channel(dev, timeout_s=self.xrank_timeout_s) if self.collective == "fused" else None
+                ch = open_channel(dev, timeout_s=self.xrank_timeout_s, fault=self.fault) \
+                    if self.collective == "fused" else None
                 bound = reducer.bind(self.x, self.cfg.op, self.acc, out=self._bound_out, xrank=ch)
                 self.lanes.append((stream, reducer, bound, ch))
                 if ch is not None:
@@ -235,7 +237,7 @@ class ScalarReduction:
             else:
                 stream = old[k][0] if len(old) > 1 and k < len(old) else torch.cuda.Stream(dev)
             reducer = old[k][1] if k < len(old) and old[k][1].config == self.kernel else Reducer(dev, config=self.kernel)
-            ch = open_channel(dev, timeout_s=self.xrank_timeout_s) if collective == "fused" else None
+            ch = open_channel(dev, timeout_s=self.xrank_timeout_s, fault=self.fault) if collective == "fused" else None
             bound = reducer.bind(self.x, self.cfg.op, self.acc, out=self._bound_out, xrank=ch)
             lanes.append((stream, reducer, bound, ch))
             if ch is not None:
@@ -310,11 +312,33 @@ class ScalarReduction:
         return None
 
     def check(self) -> Optional[str]:
-        """None, or the fused finish's error (a peer's partial never arrived). Collective."""
-        if not self.channels:
+        """None, or what went wrong in the launches so far, agreed over ranks (collective when a
+        process group spans several ranks; call after the launches):
+
+        * the polled fan-in's sticky error (a launch's finisher reached its wait bound: that launch
+          and every later one on the workspace wrote a poisoned result; the workspaces are reset);
+        * the fused finish's error (a peer's partial never arrived)."""
+        if self.ctx.device.type != "cuda":
             return None
-        from ..parallel.xrank import check_channel
-        return check_channel(self.channels)
+        dev = self.ctx.device
+        torch.cuda.synchronize(dev)
+        fan = sum(int(red.ws.error() != 0) for _, red, _, _ in self.lanes)
+        xr = sum(int(ch.error() != 0) for ch in self.channels)
+        if self.ctx.world_size > 1:
+            t = torch.tensor([fan, xr], dtype=torch.int64,
+                             device=dev if self.ctx.backend == "nccl" else "cpu")
+            torch.distributed.all_reduce(t)
+            fan, xr = (int(v) for v in t.tolist())
+        if fan:
+            for _, red, _, _ in self.lanes:
+                red.ws.reset(_current_stream_handle(dev))
+            torch.cuda.synchronize(dev)
+        msgs = []
+        if fan:
+            msgs.append(f"polled fan-in: {fan} workspace(s) reached the wait bound (results poisoned; reset)")
+        if xr:
+            msgs.append(f"fused cross-rank finish: {xr} channel(s) timed out waiting for a peer")
+        return "; ".join(msgs) or None
 
     # ------------------------------------------------------------------ verify
     def reference(self, chunk: int = 1 << 28):

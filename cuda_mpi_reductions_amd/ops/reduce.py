@@ -123,6 +123,18 @@ class Reducer:
     def num_cus(self) -> int:
         return self.ws.num_cus
 
+    def check(self, stream: Optional[torch.cuda.Stream] = None) -> Optional[str]:
+        """None, or the polled fan-in's sticky error: some launch's finisher reached its wait bound
+        (a workgroup never published), so that launch and every later one on this workspace wrote a
+        poisoned result (NaN, or the identity for integers) instead of a wrong-but-plausible one.
+        Synchronises the device; after an error the workspace is reset, so the next launch is good."""
+        torch.cuda.synchronize(self.device)
+        if self.ws.error() == 0:
+            return None
+        self.ws.reset(_stream_handle(self.device, stream))
+        torch.cuda.synchronize(self.device)
+        return "polled fan-in: a launch reached its wait bound (results poisoned since; workspace reset)"
+
     def __call__(
         self,
         x: torch.Tensor,

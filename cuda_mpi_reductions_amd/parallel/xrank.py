@@ -13,7 +13,6 @@ allocates a mailbox, the IPC handles are all-gathered, every peer's mailbox is m
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -24,8 +23,10 @@ from .._native import native
 __all__ = ["open_channel", "check_channel", "close_channels"]
 
 
-def open_channel(device: torch.device, group=None, timeout_s: float = 2.0):
-    """Create and connect this rank's :class:`_C.XrankChannel` (collective)."""
+def open_channel(device: torch.device, group=None, timeout_s: float = 2.0, fault=None):
+    """Create and connect this rank's :class:`_C.XrankChannel` (collective). ``fault`` (a
+    :class:`utils.fault.FaultInjector`, kind ``mailbox``) makes one rank fail to create its mailbox:
+    the failure-path test of the collective agreement below."""
     C = native()
     idx = device.index if device.index is not None else torch.cuda.current_device()
     if not (dist.is_available() and dist.is_initialized()):
@@ -40,8 +41,8 @@ def open_channel(device: torch.device, group=None, timeout_s: float = 2.0):
     # so one rank's failure to allocate or map cannot leave the others blocked in a collective.
     err, ch, handle = None, None, b""
     try:
-        if os.environ.get("MIREDUCE_XRANK_FAIL_RANK") == str(rank):  # failure-path test hook
-            raise RuntimeError("injected mailbox failure (MIREDUCE_XRANK_FAIL_RANK)")
+        if fault is not None and fault.mailbox(rank):
+            raise RuntimeError("injected mailbox failure (--inject-fault mailbox)")
         ch = C.XrankChannel(idx, timeout_s)
         handle = ch.handle()
     except Exception as e:  # noqa: BLE001 - reported collectively below

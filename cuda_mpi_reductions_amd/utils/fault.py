@@ -5,8 +5,14 @@ rank stalls until the SLURM walltime, mpi/submit_all.sh:4). Here every cross-ran
 deadline (process-group timeout, bootstrap deadline, RCCL async-error polling) and results are
 verified; ``--inject-fault`` provokes the failures those mechanisms exist for.
 
-Spec: ``KIND[@RANK][:STEP]`` with KIND = exit | hang | corrupt | delay=<ms>; RANK defaults to 1,
-STEP to 0 (also read from ``MIREDUCE_INJECT_FAULT``).
+Spec: ``KIND[@RANK][:STEP][/SITE]`` with KIND = exit | hang | corrupt | delay=<ms> | mailbox;
+RANK defaults to 1, STEP to 0, SITE to ``step`` (also read from ``MIREDUCE_INJECT_FAULT``).
+
+* SITE ``step``: the measured steps of the headline (bench.py counts warm-up steps first);
+  ``extras``: the steps of bench.py's after-headline candidates (pipelined / RCCL measurements) —
+  a hang there must still leave a printed, verified headline (the extras watchdog).
+* KIND ``mailbox``: rank RANK fails to create its fused-finish mailbox
+  (:func:`parallel.xrank.open_channel`); every rank must then agree on the RCCL fallback.
 """
 from __future__ import annotations
 
@@ -18,7 +24,8 @@ from typing import Optional
 
 __all__ = ["FaultSpec", "FaultInjector", "parse_fault_spec"]
 
-KINDS = ("none", "exit", "hang", "corrupt", "delay")
+KINDS = ("none", "exit", "hang", "corrupt", "delay", "mailbox")
+SITES = ("step", "extras")
 
 
 @dataclass(frozen=True)
@@ -27,6 +34,7 @@ class FaultSpec:
     rank: int = 1
     step: int = 0
     delay_ms: int = 0
+    site: str = "step"
 
 
 def _count(s: str, spec: str) -> int:
@@ -38,7 +46,11 @@ def _count(s: str, spec: str) -> int:
 def parse_fault_spec(spec: Optional[str]) -> FaultSpec:
     if not spec or spec == "none":
         return FaultSpec()
-    kind, step, rank = spec, None, None
+    kind, step, rank, site = spec, None, None, "step"
+    if "/" in kind:
+        kind, site = kind.split("/", 1)
+        if site not in SITES:
+            raise ValueError(f"bad fault spec {spec!r}: site must be one of {', '.join(SITES)}")
     if ":" in kind:
         kind, step = kind.split(":", 1)
     if "@" in kind:
@@ -48,8 +60,9 @@ def parse_fault_spec(spec: Optional[str]) -> FaultSpec:
         delay = _count(kind[len("delay="):], spec)
         kind = "delay"
     if kind not in KINDS[1:]:
-        raise ValueError(f"bad fault spec {spec!r}: kind must be exit, hang, corrupt or delay=<ms>")
-    return FaultSpec(kind, 1 if rank is None else _count(rank, spec), 0 if step is None else _count(step, spec), delay)
+        raise ValueError(f"bad fault spec {spec!r}: kind must be exit, hang, corrupt, delay=<ms> or mailbox")
+    return FaultSpec(kind, 1 if rank is None else _count(rank, spec), 0 if step is None else _count(step, spec), delay,
+                     site)
 
 
 class FaultInjector:
@@ -65,13 +78,22 @@ class FaultInjector:
     def enabled(self) -> bool:
         return self.spec.kind != "none"
 
-    def at(self, rank: int, step: int, site: str = "step") -> bool:
-        """Fire once at (rank, step). Returns True iff the caller must corrupt its local result."""
+    def on(self, site: str = "step") -> bool:
+        """Whether a step fault is armed at ``site`` (the bench issues such steps eagerly)."""
+        return self.spec.kind not in ("none", "mailbox") and self.spec.site == site
+
+    def mailbox(self, rank: int) -> bool:
+        """Whether ``rank`` must fail to create its fused-finish mailbox (every attempt)."""
+        return self.spec.kind == "mailbox" and rank == self.spec.rank
+
+    def at(self, rank: int, step: int, site: str = "step", label: str = "") -> bool:
+        """Fire once at (rank, step) of ``site``. Returns True iff the caller must corrupt its local
+        result."""
         s = self.spec
-        if self.fired or s.kind == "none" or rank != s.rank or step != s.step:
+        if self.fired or not self.on(site) or rank != s.rank or step != s.step:
             return False
         self.fired = True
-        print(f"[fault] rank {rank} {s.kind} at {site} {step}", file=sys.stderr, flush=True)
+        print(f"[fault] rank {rank} {s.kind} at {label or site} {step}", file=sys.stderr, flush=True)
         if s.kind == "exit":
             sys.stdout.flush()
             os._exit(3)

@@ -236,6 +236,18 @@ def test_reduce_xgmi_direct_tiny_counts(count):
     assert "verification PASSED" in r.stderr
 
 
+@pytest.mark.parametrize("args", [["--kernel=0", "--threads=64"], ["--kernel=3", "--n=1e8"]])
+def test_reduction_cpufinal_more_partials_than_the_pinned_default(tmp_path, args):
+    # kernels 0..5 have no --maxblocks cap, so --cpufinal can leave more partials
+    # than the default 64 Ki-entry pinned landing zone; it must grow, not overflow the host heap.
+    js = tmp_path / "cf.json"
+    r = reduction(tmp_path, "--method=SUM", "--type=double", "--cpufinal", "--iterations=2", f"--json={js}", *args)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(js.read_text().splitlines()[-1])
+    assert d["verified"] is True and d["passes"] == 1 and d["host_folded"] > 65536, d
+    assert d["fanin_error"] == 0 and d["native_source_hash"] != "unknown"
+
+
 def test_bench_rehearsal_two_ranks_one_gpu(tmp_path):
     env_before = os.environ.get("MIREDUCE_FORCE_DEVICE")
     os.environ["MIREDUCE_FORCE_DEVICE"] = "0"

@@ -62,16 +62,29 @@ def test_ticketed_fanin_publish_then_ticket_then_consume(tmp_path):
     assert ok, "no publish -> drain -> ticket -> barrier -> sc1-load sequence in the ticketed fan-in"
 
 
-def test_polled_fanin_tagged_slots(tmp_path):
-    # default fan-in: two tagged 8-byte words stored per workgroup (no drain, no ticket); the
-    # finisher polls both words of a slot (sc1 loads) with a bounded, sleeping loop and clears them.
+def test_polled_fanin_epoch_tagged_slots(tmp_path):
+    # default fan-in: the launch's epoch (Workspace fan[0]) is loaded L2-bypassing
+    # in the prologue and NOT waited for before the streaming body issues its first loads (its
+    # latency hides under them); every workgroup stores two epoch-tagged 8-byte words (no drain, no
+    # ticket); the finisher reads the sticky-error word (fan[1], offset:4), polls both words of a
+    # slot (sc1 loads) with a bounded, sleeping loop, and finally stores the new epoch (a dword sc1
+    # store back to fan[0]) — no slot is cleared.
     ins = _disasm(tmp_path, "reduce_tab_f64.o", STREAM_F64)
+    ep = _first(ins, r"^global_load_dword v\d+, v\d+, (s\[\d+:\d+\]) sc1$")
+    assert ep is not None and ep < 60, "epoch load is not in the prologue"
+    fan = re.search(r"(s\[\d+:\d+\]) sc1$", ins[ep]).group(1)
+    body = _first(ins, r"^global_load_dwordx4 .* nt$", ep)
+    wait0 = _first(ins, r"^s_waitcnt vmcnt\(0\)", ep)
+    assert body is not None and (wait0 is None or body < wait0), "a wait separates the epoch load from the body"
     st = _first(ins, r"^global_store_dwordx2 .* sc1$")
-    assert st is not None and re.search(r"offset:8 sc1$", ins[st + 1] if st + 1 < len(ins) else "") or \
-        _first(ins, r"^global_store_dwordx2 .* offset:8 sc1$", st) is not None
+    assert st is not None and _first(ins, r"^global_store_dwordx2 .* offset:8 sc1$", st) is not None
+    err = _first(ins, r"^global_load_dword v\d+, v\d+, " + re.escape(fan) + r" offset:4 sc1$", st)
+    assert err is not None, "finisher does not read the sticky error word"
     poll = _first(ins, r"^global_load_dwordx2 .* sc1$", st)
     assert poll is not None and re.search(r"^global_load_dwordx2 .* offset:8 sc1$", ins[poll + 1])
     assert _first(ins, r"^s_sleep", poll) is not None and _first(ins, r"^s_memrealtime", st) is not None
+    assert _first(ins, r"^global_store_dword v\d+, v\d+, " + re.escape(fan) + r" sc1$", poll) is not None, \
+        "finisher does not advance the epoch"
     # (hipcc lays the polled and ticketed branches out in either order, so no check here compares
     # positions across the two branches)
 

@@ -74,8 +74,57 @@ def test_reduce_c_vector_table_becomes_results_files(tmp_path):
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     rows = (out / "vector_rccl" / "INT_SUM.txt").read_text().split("\n")
-    assert rows[0] == "" and rows[1:4] == ["INT SUM 1 200.00000", "INT SUM 2 400.00000", "INT SUM 8 1600.00000"]
-    assert (out / "vector_direct" / "DOUBLE_MAX.txt").read_text().split("\n")[3] == "DOUBLE MAX 8 3200.00000"
+    # N=1 is left out (one rank has no cross-rank reduction to report)
+    assert rows[0] == "" and rows[1:3] == ["INT SUM 2 400.00000", "INT SUM 8 1600.00000"] and rows[3] == ""
+    assert (out / "vector_direct" / "DOUBLE_MAX.txt").read_text().split("\n")[2] == "DOUBLE MAX 8 3200.00000"
     assert "| direct | DOUBLE | MIN | 2 | 800.000 | 2 |" in (out / "vector.md").read_text()
+    assert "| 1 |" not in (out / "vector.md").read_text()
     import plot
-    assert [n for n, _ in plot.read_results(str(out / "vector_rccl" / "DOUBLE_MIN.txt"))] == [1, 2, 8]
+    assert [n for n, _ in plot.read_results(str(out / "vector_rccl" / "DOUBLE_MIN.txt"))] == [2, 8]
+
+
+def test_bench_reduce_c_rows_through_getavgs_match_the_reference_shape(tmp_path):
+    # bench.py's reduce_c_vector.rows[impl] are reduce.c's own stdout (header +
+    # RETRY_COUNT retry-major rounds of INT/DOUBLE x MAX/MIN/SUM, "%s %s %d %10.3lf"); tools/scaling.py
+    # concatenates the N > 1 runs into collected.txt and utils/getavgs.py (getAvgs.sh) turns that into
+    # results/<DT>_<OP>.txt with exactly the shape of the reference's mpi/results/*.txt.
+    import re
+    from cuda_mpi_reductions_amd.utils import getavgs
+
+    def bench_line(n):
+        d = _line(n, 7300.0 * n, 8.0 / (7.3 * n))
+        lines, table = ["# DATATYPE OP NODES GB/sec"], []
+        for x in range(5):
+            for dt in ("INT", "DOUBLE"):
+                for op in ("MAX", "MIN", "SUM"):
+                    g = 100.0 * n + x + (0.5 if dt == "DOUBLE" else 0.0)
+                    lines.append("%s %s %d %10.3lf" % (dt, op, n, g))
+                    table.append({"retry": x, "dtype": dt, "op": op, "impl": "direct", "gibps": g})
+        d["reduce_c_vector"] = {"table": table, "rows": {"direct": lines}}
+        return d
+    src = tmp_path / "scale.jsonl"
+    src.write_text("\n".join(json.dumps(bench_line(n)) for n in (1, 2, 4, 8)) + "\n")
+    out = tmp_path / "res"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling.py"), str(src), "--out", str(out)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    collected = out / "vector_direct" / "collected.txt"
+    text = collected.read_text().splitlines()
+    assert text.count("# DATATYPE OP NODES GB/sec") == 3  # the N = 2, 4, 8 runs; N = 1 left out
+    assert len(text) == 3 * 31 and not [ln for ln in text if ln.startswith("INT MAX 1 ")]
+    res = tmp_path / "results"
+    getavgs.write_results(str(collected), str(res))
+    ref_dir = "/root/reference/mpi/results"
+    line_rx = re.compile(r"^(INT|DOUBLE) (SUM|MIN|MAX) \d+ \d+\.\d{5}$")
+    for dt in ("INT", "DOUBLE"):
+        for op in ("SUM", "MIN", "MAX"):
+            got = (res / f"{dt}_{op}.txt").read_text().split("\n")
+            assert got[0] == "" and got[-1] == "" and len(got) == 5, got  # blank line + N = 2, 4, 8
+            assert all(line_rx.match(ln) for ln in got[1:-1]), got
+            assert sorted(int(ln.split()[2]) for ln in got[1:-1]) == [2, 4, 8]
+            mean8 = float([ln for ln in got[1:-1] if ln.split()[2] == "8"][0].split()[3])
+            assert abs(mean8 - (800.0 + 2.0 + (0.5 if dt == "DOUBLE" else 0.0))) < 1e-4  # mean of retries 0..4
+            ref_path = os.path.join(ref_dir, f"{dt}_{op}.txt")
+            if os.path.exists(ref_path):  # the reference's own file has the same shape
+                ref = open(ref_path).read().split("\n")
+                assert ref[0] == "" and all(line_rx.match(ln) for ln in ref[1:] if ln)

@@ -72,14 +72,18 @@ def test_bench_torchrun_one_rank_graphs_both_modes(tmp_path, collective):
     assert d["verified"] is True and d["n_gpus"] == 1 and d["config"]["collective"] == collective
     assert d["config"]["launch"].startswith("graph"), d["config"]["launch"]
     assert d["serial_launch"].startswith("graph"), d["serial_launch"]
-    assert d["serial_gbps"] > 0 and d["serial_ms_per_step"] > 0
+    # the headline IS the per-reduction (serial, one lane) measurement
+    assert d["serial_gbps"] == d["value"] > 0 and d["serial_ms_per_step"] == d["ms_per_step"] > 0
+    assert d["config"]["streams"] == 1 and d["config"]["overlap"].startswith("serial")
     combine = d["config"]["cross_rank_combine"]
+    assert combine.startswith("none at world 1")  # the JSON says the combine is a no-op at world 1
     assert ("RCCL" in combine) if collective == "rccl" else ("fused" in combine)
+    assert d["native_source_hash"] and d["native_source_hash"] != "unknown"
 
 
 def test_bench_fused_two_lanes(tmp_path):
     r = run([sys.executable, BENCH, "--no-vector-extras", "--steps", "24", "--warmup", "2", "--elements", "50000017", "--collective",
-             "fused", "--streams", "2", "--graph-chunk", "8"], cwd=tmp_path, timeout=600)
+             "fused", "--pipelined", "--streams", "2", "--graph-chunk", "8"], cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
     assert d["verified"] is True and d["config"]["streams"] == 2
@@ -136,29 +140,32 @@ def test_fused_missing_peer_times_out_not_hangs(tmp_path):
 
 
 def test_bench_auto_falls_back_to_rccl_on_every_rank(tmp_path, monkeypatch):
-    # One rank cannot create its mailbox: every rank must agree and run the RCCL/gloo combine.
+    # One rank cannot create its mailbox (fault injector, kind mailbox): every rank must agree and run
+    # the RCCL/gloo combine.
     monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
-    monkeypatch.setenv("MIREDUCE_XRANK_FAIL_RANK", "1")
     r = torchrun(2, [BENCH, "--no-vector-extras", "--gpus", "2", "--backend", "gloo", "--steps", "4", "--warmup", "1",
-                     "--elements", "20000003"], cwd=tmp_path, timeout=600)
+                     "--elements", "20000003", "--inject-fault", "mailbox@1"], cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
-    assert d["verified"] is True
-    assert d["config"]["collective"].startswith("rccl (auto; fused unavailable"), d["config"]["collective"]
+    assert d["verified"] is True and d["config"]["collective"] == "rccl"
+    assert d["config"]["collective_choice"].startswith("auto; fused unavailable"), d["config"]["collective_choice"]
+    assert "injected mailbox failure" in d["config"]["collective_choice"]
 
 
-def test_bench_auto_tunes_the_combine(tmp_path):
-    r = run([sys.executable, BENCH, "--no-vector-extras", "--steps", "6", "--warmup", "2", "--elements", "50000017"], cwd=tmp_path,
-            timeout=600)
+def test_bench_auto_headline_is_serial_fused_extras_after(tmp_path):
+    # value = the serial one-lane fused measurement; the pipelined 2-lane number is
+    # an extra measured after the line is final; at world 1 there is no RCCL combine to measure.
+    r = run([sys.executable, BENCH, "--no-vector-extras", "--steps", "12", "--warmup", "2", "--elements", "50000017"],
+            cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
-    assert d["verified"] is True and d["config"]["collective"].endswith("(auto-tuned)")
-    tun = d["collective_tuning"]
-    assert set(tun["gbps"]) == {"fused_1lane", "fused_2lane", "rccl_1lane"} and all(v > 0 for v in tun["gbps"].values())
-    assert tun["chosen"] == max(tun["gbps"], key=tun["gbps"].get)
-    assert tun["steps"] == 400  # auto: ~30 ms of reduction per candidate, clamped (400 MB shard)
-    assert d["config"]["collective"].startswith(tun["chosen"].split("_")[0])
-    assert d["serial_gbps"] > 0 and d["serial_launch"].startswith("graph")
+    assert d["verified"] is True and d["config"]["collective"] == "fused"
+    assert d["value"] == d["serial_gbps"] and d["serial_collective"] == "fused"
+    assert d["config"]["streams"] == 1 and d["config"]["launch"].startswith("graph")
+    c = d["candidates"]
+    assert c["fused_2lane_pipelined"]["verified"] is True and c["fused_2lane_pipelined"]["gbps"] > 0
+    assert d["pipelined_gbps"] == c["fused_2lane_pipelined"]["gbps"]
+    assert d["rccl_serial_gbps"] is None and "world 1" in c["rccl_serial"]["note"]
 
 
 # ---------------------------------------------------------------- direct collective from Python
@@ -200,20 +207,28 @@ def test_bench_vector_direct_ranks_share_one_gpu(tmp_path, nproc, monkeypatch):
 
 
 def test_bench_vector_extras_in_headline(tmp_path):
-    r = run([sys.executable, BENCH, "--steps", "4", "--warmup", "1", "--elements", "50000017"], cwd=tmp_path,
-            timeout=600)
+    r = run([sys.executable, BENCH, "--steps", "4", "--warmup", "1", "--elements", "50000017", "--no-candidates"],
+            cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
     ex = d["reduce_c_vector"]
-    for k in ("reduce_rccl", "reduce_direct", "allreduce_rccl", "allreduce_direct"):
+    for k in ("reduce_direct", "allreduce_direct"):
         assert ex[k].get("verified") is True and ex[k]["gibps"] > 0, (k, ex[k])
+    # world 1: RCCL's 1-rank in-place reduce does no work -> null rows, never a number
+    assert ex["reduce_rccl"]["gibps"] is None and ex["allreduce_rccl"]["gibps"] is None
     assert "peer_read" not in ex  # one rank: no peers to read
-    # reduce.c's whole table (INT / DOUBLE x MAX / MIN / SUM to root 0) over both implementations
     tab = ex["table"]
-    assert [(t["dtype"], t["op"]) for t in tab if t["impl"] == "rccl"] == \
-        [(dt, op) for dt in ("INT", "DOUBLE") for op in ("MAX", "MIN", "SUM")]
-    assert len(tab) == 12 and all(t.get("verified") is True and t["gibps"] > 0 for t in tab), tab
-    assert ex["rows"][0].startswith("INT MAX 1 ") and len(ex["rows"]) == 12
+    rccl = [t for t in tab if t["impl"] == "rccl"]
+    assert len(rccl) == 6 and all(t["gibps"] is None for t in rccl)
+    # reduce.c's table over the direct collective: RETRY_COUNT rounds of INT / DOUBLE x MAX / MIN / SUM,
+    # retry-major, each collective timed on its own and verified (retry 0) / checksum-reproduced
+    direct = [t for t in tab if t["impl"] == "direct"]
+    order = [(dt, op) for dt in ("INT", "DOUBLE") for op in ("MAX", "MIN", "SUM")]
+    assert [(t["retry"], t["dtype"], t["op"]) for t in direct] == [(x, dt, op) for x in range(5) for dt, op in order]
+    assert all(t.get("verified") is True and t["gibps"] > 0 for t in direct), direct
+    rows = ex["rows"]["direct"]
+    assert rows[0] == "# DATATYPE OP NODES GB/sec" and len(rows) == 31 and rows[1].startswith("INT MAX 1 ")
+    assert "rccl" not in ex["rows"]
 
 
 def test_bench_fused_corrupt_rank_fails_verification(tmp_path, monkeypatch):
@@ -251,10 +266,11 @@ def test_bench_eight_ranks_auto_on_one_gpu(tmp_path, monkeypatch):
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
     assert d["verified"] is True and d["n_gpus"] == 8
-    assert "auto" in d["config"]["collective"] and "reduce_c_vector" in d
+    assert d["config"]["collective"] == "fused" and d["value"] == d["serial_gbps"] and "reduce_c_vector" in d
     ex = d["reduce_c_vector"]
     assert ex["reduce_direct"].get("verified") is True, ex
-    assert len(ex["table"]) == 6 and all(t.get("verified") is True for t in ex["table"]), ex["table"]
+    assert len(ex["table"]) == 30 and all(t.get("verified") is True for t in ex["table"]), ex["table"]
+    assert len(ex["rows"]["direct"]) == 31 and ex["rows"]["direct"][1].startswith("INT MAX 8 ")
     pr = ex["peer_read"]  # fabric probe: 8 ranks reading each other's buffers (here all on one GPU)
     assert "error" not in pr and 0 < pr["ingress_gbps_min"] <= pr["ingress_gbps_max"] and pr["node_gbps"] > 0, pr
 
@@ -280,21 +296,19 @@ def test_bench_extras_deadline_keeps_the_headline(tmp_path):
     assert d["verified"] is True and "did not finish" in d["reduce_c_vector"]["error"]
 
 
-def test_bench_serial_number_takes_the_faster_combine(tmp_path):
-    # auto at N=1: when the headline is not the one-lane fused finish, the serial (per-reduction)
-    # measurement runs both the fused finish and the RCCL all-reduce and reports the faster.
-    r = run([sys.executable, BENCH, "--steps", "12", "--warmup", "2", "--elements", "50000017",
-             "--no-vector-extras"], cwd=tmp_path, timeout=600)
+def test_bench_extras_hang_in_rccl_candidate_keeps_the_headline(tmp_path, monkeypatch):
+    # a hang inside an after-headline RCCL candidate (fault site "extras") still
+    # ends the run with the verified headline printed and rc 0 (the extras watchdog), on every rank.
+    monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    r = torchrun(2, [BENCH, "--no-vector-extras", "--gpus", "2", "--backend", "gloo", "--collective", "rccl",
+                     "--steps", "4", "--warmup", "1", "--elements", "20000003", "--extras-deadline", "25",
+                     "--inject-fault", "hang@1:0/extras"], cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
-    assert d["verified"] is True and d["serial_gbps"] > 0
-    cands = d.get("serial_candidates_gbps")
-    if cands is None:  # the headline itself is the serial protocol (fused, one lane)
-        assert d["collective_tuning"]["chosen"] == "fused_1lane" and d["serial_collective"] == "fused"
-    else:
-        assert set(cands) == {"fused", "rccl"}
-        best = max(cands, key=cands.get)
-        assert d["serial_collective"] == best and d["serial_gbps"] == cands[best]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["verified"] is True and d["value"] > 0 and "did not finish" in d["extras_error"]
+    assert "hang at bench extras 0" in r.stderr
 
 
 def test_bench_plan_tuning_at_the_eight_gpu_shard(tmp_path):

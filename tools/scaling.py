@@ -15,7 +15,9 @@ or any JSON document holding such objects, e.g. the driver's scaling file), grou
                                ``reduce_c_vector.table`` (INT / DOUBLE x MAX / MIN / SUM element-wise
                                to root 0, GiB/s of total data, impl = rccl | direct), averaged per N
                                like getAvgs.sh: the counterpart of mpi/results/<DT>_<OP>.txt, plus
-                               ``<out>/vector.md``.
+                               ``<out>/vector.md`` (N > 1 only: one rank has no cross-rank reduction);
+* ``<out>/vector_<impl>/collected.txt``  every run's reduce.c-format stdout rows (``reduce_c_vector.
+                               rows[impl]``, N > 1), the input mpi/getAvgs.sh / utils/getavgs.py expect.
 
 Efficiency = value(N) / (N * value(1)): the whole-node bandwidth of N GPUs against N copies of the
 1-GPU run (bench.py's headline is strong scaling, so this is also t(1) / (N * t(N))).
@@ -91,9 +93,14 @@ def summarise(results):
 
 def summarise_vector(results):
     """{(impl, DT, OP): {N: {"gibps": mean, "runs": k}}} from every result's reduce_c_vector.table
-    (entries with an error are skipped)."""
+    (one entry per timed collective, RETRY_COUNT per (dtype, op), averaged like getAvgs.sh).
+    Skipped: entries without a number (errors; RCCL at world 1) and every N=1 entry — one rank has
+    no cross-rank reduction (RCCL's 1-rank in-place reduce does no work, direct is a local copy),
+    so an N=1 point next to the N>1 ones in results/<DT>_<OP>.txt would be unphysical."""
     acc = defaultdict(lambda: defaultdict(list))
     for r in results:
+        if int(r.get("n_gpus", 0)) <= 1:
+            continue
         for row in ((r.get("reduce_c_vector") or {}).get("table") or []):
             if row.get("gibps") is None:
                 continue
@@ -119,6 +126,27 @@ def write_vector(vsummary, out_dir):
         with open(os.path.join(out_dir, "vector.md"), "w") as f:
             f.write(text)
     return text
+
+
+def write_collected(results, out_dir):
+    """<out>/vector_<impl>/collected.txt: the concatenated reduce.c stdout of every N > 1 run (the
+    reference's mpi/collected.txt, which getAvgs.sh reads). Returns {impl: path}."""
+    by_impl = defaultdict(list)
+    for r in results:
+        if int(r.get("n_gpus", 0)) <= 1:
+            continue
+        rows = (r.get("reduce_c_vector") or {}).get("rows")
+        if isinstance(rows, dict):
+            for impl, lines in rows.items():
+                by_impl[impl].extend(lines)
+    paths = {}
+    for impl, lines in by_impl.items():
+        d = os.path.join(out_dir, f"vector_{impl}")
+        os.makedirs(d, exist_ok=True)
+        paths[impl] = os.path.join(d, "collected.txt")
+        with open(paths[impl], "w") as f:
+            f.write("".join(ln + "\n" for ln in lines))
+    return paths
 
 
 def efficiency(per_n):
@@ -169,6 +197,7 @@ def main(argv=None):
     vs = summarise_vector(results)
     if vs:
         print(write_vector(vs, a.out), end="")
+    write_collected(results, a.out)
     return 0
 
 

@@ -259,7 +259,7 @@ def _checksum(wl, holder: bool) -> float:
     return float(wl.result().to(torch.float64).sum().item()) if holder else 0.0
 
 
-def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES) -> dict:
+def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES, out: "dict | None" = None) -> dict:
     """reduce.c's own measurement on this job's GPUs, next to the scalar headline, in reduce.c's
     shape: element-wise INT and DOUBLE MAX / MIN / SUM of 2 GiB of total data each (NUM_INTS /
     NUM_DOUBLES, mpi/constants.h:1-2) to root 0 (MPI_Reduce, reduce.c:76,90), one warm-up SUM per
@@ -274,15 +274,19 @@ def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES) -> dict:
     utils/getavgs.py; ``reduce_<impl>`` / ``allreduce_<impl>``: DOUBLE SUM to root / to every rank.
     At world 1 RCCL rows are null (its 1-rank in-place reduce does no work). Every (dtype, op) is
     verified against the gathered inputs on its first retry and later retries must reproduce its
-    checksum. Errors are recorded, not raised."""
+    checksum. Errors are recorded, not raised. ``out`` (optional) is filled in place as the table
+    grows, so a watchdog that fires mid-way still reports the rows measured so far; the direct
+    collective (no RCCL) goes first."""
     from cuda_mpi_reductions_amd.models import CONFIGS as _C, VectorReduction
-    out = {"units": "GiB/s (2^30 B of total data per collective, reduce.c:93)", "retries": retries,
-           "order": "retry-major: per retry INT MAX, INT MIN, INT SUM, DOUBLE MAX, DOUBLE MIN, DOUBLE SUM "
-                    "(reduce.c:71-97)", "total_bytes": 256 * 1024 * 1024 * 8}
+    out = {} if out is None else out
+    out.update({"units": "GiB/s (2^30 B of total data per collective, reduce.c:93)", "retries": retries,
+                "order": "retry-major: per retry INT MAX, INT MIN, INT SUM, DOUBLE MAX, DOUBLE MIN, DOUBLE SUM "
+                         "(reduce.c:71-97)", "total_bytes": 256 * 1024 * 1024 * 8})
     # (gloo rehearsals: its GPU-tensor reduce / all_reduce is not RCCL and crashes on 1 GiB
     # tensors, so only the direct collective runs there)
-    impls = ("rccl", "direct") if ctx.backend == "nccl" else ("direct",)
+    impls = ("direct", "rccl") if ctx.backend == "nccl" else ("direct",)
     table, rows = [], {}
+    out["table"], out["rows"] = table, rows
     holder = ctx.rank == 0
     for impl in impls:
         if impl == "rccl" and ctx.world_size == 1:
@@ -292,6 +296,7 @@ def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES) -> dict:
             continue
         wls = {}
         lines = [REDUCE_C_HEADER]
+        rows[impl] = lines
         try:
             for dt, base in REDUCE_C_DTYPES:  # both registered up front: the rounds interleave dtypes
                 wls[dt] = VectorReduction(_C[base], ctx, impl=impl, direct_timeout_s=5.0).setup()
@@ -334,9 +339,6 @@ def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES) -> dict:
             wl.close()  # collective: the next registration may reuse these addresses
         wls.clear()
         torch.cuda.empty_cache()
-        rows[impl] = lines
-    out["table"] = table
-    out["rows"] = rows
     if ctx.world_size == 1:
         out["note"] = ("world 1: RCCL rows are null (no work); direct is one local send -> receive pass (what "
                        "MPI_Reduce does on one rank); tools/scaling.py keeps N=1 out of the results files")
@@ -556,16 +558,25 @@ class _PhaseWatchdog:
 
 class _ExtrasWatchdog(_PhaseWatchdog):
     """The after-headline extras' deadline: on expiry the finished headline ``line`` is printed
-    (extras marked as timed out) and every rank exits with the headline's status."""
+    with whatever extras completed so far (``partial``, filled in place by the extras) and the
+    rest marked as timed out, and every rank exits with the headline's status."""
 
-    def __init__(self, line: "dict | None", deadline_s: float, rc: int):
+    def __init__(self, line: "dict | None", deadline_s: float, rc: int, partial: "dict | None" = None):
         def make():
             if line is None:
                 return None
             out = dict(line)
             msg = f"extras did not finish within {deadline_s:.0f} s (headline measured and verified before them)"
             out["extras_error"] = msg
-            out["reduce_c_vector"] = {"error": msg}
+            for _ in range(3):  # the extras may be mid-update in the main thread: snapshot via JSON
+                try:
+                    out.update(json.loads(json.dumps(partial or {})))
+                    break
+                except (RuntimeError, ValueError):
+                    time.sleep(0.01)
+            rc_vec = dict(out.get("reduce_c_vector") or {})
+            rc_vec["error"] = msg
+            out["reduce_c_vector"] = rc_vec
             return out
         super().__init__("after-headline extras", deadline_s, rc, make)
 
@@ -574,7 +585,7 @@ def _gbps(wl, K: int, elapsed: float) -> float:
     return wl.bytes_total * K / elapsed / 1e9
 
 
-def _candidates(wl, ctx, args, fault, fused_ok: bool) -> dict:
+def _candidates(wl, ctx, args, fault, fused_ok: bool, capture_failed: bool = False) -> dict:
     """After-headline measurements of the other step protocols (extras; never the headline):
 
     * ``fused_2lane_pipelined``: the fused finish over two stream lanes, consecutive independent
@@ -584,7 +595,9 @@ def _candidates(wl, ctx, args, fault, fused_ok: bool) -> dict:
       at world 1 the all-reduce enqueues no kernel).
 
     Each is verified and its error words read; a failure is recorded, never raised. Fault site
-    ``extras`` injects into these steps."""
+    ``extras`` injects into these steps. ``capture_failed``: the headline's graph capture of
+    collective-issuing steps failed (e.g. gloo collectives on GPU tensors), so RCCL candidates are
+    issued eagerly rather than captured again (a second failed capture can abort the process)."""
     K, W = args.steps, min(args.warmup, 2)
     todo = []
     if fused_ok:
@@ -596,7 +609,8 @@ def _candidates(wl, ctx, args, fault, fused_ok: bool) -> dict:
         try:
             wl.use_collective(coll, streams=lanes)
             slots = wl.new_slots(W + K)
-            m = _measure(wl, slots, ctx, args, fault, serial=serial, warmup=W, site="extras")
+            m = _measure(wl, slots, ctx, args, fault, serial=serial, warmup=W, site="extras",
+                         allow_graph=not (capture_failed and coll == "rccl"))
             err = wl.check()
             ok = _verify_slots(wl, slots[:m["written"]], ctx)[0] and err is None
             out[name] = {"gbps": round(_gbps(wl, K, m["elapsed"]), 3),
@@ -799,14 +813,18 @@ def main(argv=None) -> int:
         return 2  # (unreachable: the watchdog ended the process)
 
     # ------------------------------------------------------------------ extras (watchdog; never the headline)
-    guard = _ExtrasWatchdog(line, args.extras_deadline, rc)
+    # Order: reduce.c's table (direct collective first: no RCCL), then the step candidates (the
+    # RCCL ones last), so a hang costs the fewest extras; the watchdog prints what has completed.
     extras = {}
-    if args.candidates and dev.type == "cuda" and hasattr(wl, "use_collective") and not args.pipelined:
-        extras["candidates"] = _candidates(wl, ctx, args, fault, collective == "fused")
+    guard = _ExtrasWatchdog(line, args.extras_deadline, rc, partial=extras)
+    if args.vector_extras and dev.type == "cuda" and cfg.name == NORTH_STAR:
+        extras["reduce_c_vector"] = {}
+        _vector_extras(ctx, out=extras["reduce_c_vector"])
     if args.compare_torch and dev.type == "cuda":
         extras["torch_gbps"] = round(_time_torch_reduction(wl, K, W, ctx), 3)
-    if args.vector_extras and dev.type == "cuda" and cfg.name == NORTH_STAR:
-        extras["reduce_c_vector"] = _vector_extras(ctx)
+    if args.candidates and dev.type == "cuda" and hasattr(wl, "use_collective") and not args.pipelined:
+        extras["candidates"] = _candidates(wl, ctx, args, fault, collective == "fused",
+                                           capture_failed=m["launch"].startswith("eager (graph capture failed"))
     if guard.finish() and line is not None:
         cands = extras.get("candidates")
         if cands is not None:

@@ -63,3 +63,26 @@ def test_plan_candidates_only_for_the_headline_shards():
     assert b._plan_candidates(1e9, 8) == [(0, 0, 0), (256, 8, 1)]                # N=8 shard
     assert b._plan_candidates(0.5 * GB, 8) == [(0, 0, 0)]
     assert b._plan_candidates(8e9, 4) == [(0, 0, 0)] and b._plan_candidates(8e9, 2) == [(0, 0, 0)]
+
+
+def test_extras_watchdog_reports_the_extras_completed_so_far():
+    # a hang mid-way through the extras (e.g. an RCCL collective at N>1) must still publish the rows
+    # measured before it, next to the headline
+    import json
+    import subprocess
+    import sys
+    code = (
+        "import importlib.util, os, sys, time\n"
+        f"spec = importlib.util.spec_from_file_location('b', os.path.join({ROOT!r}, 'bench.py'))\n"
+        "b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)\n"
+        "extras = {}\n"
+        "g = b._ExtrasWatchdog({'metric': 'm', 'value': 1.0}, 0.5, 0, partial=extras)\n"
+        "extras['reduce_c_vector'] = {'rows': {'direct': ['# DATATYPE OP NODES GB/sec', 'INT MAX 8   1.000']}}\n"
+        "time.sleep(30)\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, (r.stdout, r.stderr)
+    d = json.loads(lines[0])
+    v = d["reduce_c_vector"]
+    assert v["rows"]["direct"][1] == "INT MAX 8   1.000" and "did not finish" in v["error"]
+    assert "did not finish" in d["extras_error"] and d["value"] == 1.0

@@ -145,6 +145,99 @@ __global__ __launch_bounds__(BLOCK) void body(TArgs a) {
       tile<BLOCK, UNROLL, 0>(acc, a.v + t * kTile + threadIdx.x);
       ++done;
     }
+  } else if constexpr (!DYN && MODE == 6) {
+    // XCD-residue shift: within each stripe of 8 consecutive tiles, workgroup b takes tile
+    // (b + a.chunk) % 8 instead of b % 8, so under round-robin dispatch (XCD = b % 8) XCD x reads
+    // the tiles of address residue (x + shift) % 8 — shifts 0..7 measure every (XCD, residue) pair.
+    const uint64_t g = gridDim.x;
+    const uint64_t b = (blockIdx.x & ~7ull) | ((blockIdx.x + a.chunk) & 7ull);
+    for (uint64_t t = b; t < ntiles; t += g, ++done) tile<BLOCK, UNROLL, 0>(acc, a.v + t * kTile + threadIdx.x);
+  } else if constexpr (!DYN && MODE >= 100) {
+    // Explicit load window (MODE = 100 + D, D | UNROLL): the thread's loads form one sequence over its
+    // interleaved tiles; exactly D are in flight — each step consumes the load issued D steps earlier
+    // and issues the next one, and a sched_barrier between steps keeps hipcc's scheduler from
+    // regrouping them (its own grouping moves with unrelated code: round 3 found a 2.5 % swing).
+    constexpr int D = MODE - 100;
+    static_assert(UNROLL % D == 0, "window must divide the unroll");
+    const uint64_t g = gridDim.x;
+    const V* base = a.v + threadIdx.x;
+    uint64_t t = blockIdx.x;
+    if (t < ntiles) {
+      V buf[D];
+#pragma unroll
+      for (int j = 0; j < D; ++j) buf[j] = __builtin_nontemporal_load(base + t * kTile + j * BLOCK);
+      for (; t + g < ntiles; t += g, ++done) {
+        const V* p = base + t * kTile;
+        const V* q = base + (t + g) * kTile;
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+          acc[u] += buf[u % D][0] + buf[u % D][1];
+          const int j = u + D;
+          buf[u % D] = __builtin_nontemporal_load(j < UNROLL ? p + j * BLOCK : q + (j - UNROLL) * BLOCK);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      const V* p = base + t * kTile;  // last tile: no next-tile loads
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        acc[u] += buf[u % D][0] + buf[u % D][1];
+        const int j = u + D;
+        if (j < UNROLL) buf[u % D] = __builtin_nontemporal_load(p + j * BLOCK);
+      }
+      ++done;
+    }
+  } else if constexpr (!DYN && MODE == 7) {
+    // Static rounds over tiles [0, a.nbig) (a.nbig a multiple of the grid), then every remaining
+    // vector as WAVE granules of a.chunk wave-tiles (64 lanes x UNROLL vectors each), dealt from 8
+    // heads (a.qctr + 16 h, head h owning a contiguous range of a.nchunks granules): lane 0 takes a
+    // granule with one returning device-scope atomic, issued one granule AHEAD (before the current
+    // granule's loads, so the in-order vmcnt wait of those loads covers it), broadcast with
+    // readfirstlane — no LDS, no barrier. A wave starts at head (wave id % 8) and moves on when a
+    // head runs dry, so fast XCDs simply take more granules.
+    for (uint64_t t = blockIdx.x; t < a.nbig; t += gridDim.x, ++done) tile<BLOCK, UNROLL, 0>(acc, a.v + t * kTile + threadIdx.x);
+    const unsigned lane = threadIdx.x & 63;
+    const uint64_t v0 = a.nbig * kTile;
+    const uint64_t gsz = 64ull * UNROLL * a.chunk;
+    const uint64_t ng = a.nvec > v0 ? (a.nvec - v0 + gsz - 1) / gsz : 0;
+    const uint64_t per = a.nchunks;  // granules per head
+    unsigned h = (blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6)) & 7u;
+    unsigned tried = 0;
+    auto grab = [&](unsigned hh) -> uint64_t {
+      unsigned long long r = 0;
+      if (lane == 0) r = __hip_atomic_fetch_add(a.qctr + 16 * hh, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned lo = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(r));
+      const unsigned hi = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(r >> 32));
+      return (static_cast<uint64_t>(hi) << 32) | lo;
+    };
+    auto head_size = [&](unsigned hh) -> uint64_t {
+      const uint64_t b0 = hh * per;
+      return b0 >= ng ? 0 : (b0 + per <= ng ? per : ng - b0);
+    };
+    uint64_t g = ng ? grab(h) : 0;
+    while (ng) {
+      while (g >= head_size(h)) {  // this head is dry: the next one
+        if (++tried == 8) break;
+        h = (h + 1) & 7u;
+        g = grab(h);
+      }
+      if (tried == 8) break;
+      const uint64_t cur = h * per + g;
+      const uint64_t nxt = grab(h);  // one granule ahead
+      const uint64_t base = v0 + cur * gsz + lane;
+      for (uint64_t c = 0; c < a.chunk; ++c) {
+        V v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+          const uint64_t i = base + (c * UNROLL + u) * 64;
+          v[u] = __builtin_nontemporal_load(a.v + (i < a.nvec ? i : a.nvec - 1));
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+          if (base + (c * UNROLL + u) * 64 < a.nvec) acc[u] += v[u][0] + v[u][1];
+      }
+      ++done;
+      g = nxt;
+    }
   } else if constexpr (!DYN && MODE == 4) {
     // static grid-stride over the first a.nbig tiles, then the tail [a.nbig, ntiles) as 8 queues
     // of a.nchunks granules (a.chunk tiles each); a workgroup drains its own XCD's queue first,
@@ -207,10 +300,11 @@ __global__ __launch_bounds__(BLOCK) void body(TArgs a) {
       slot ^= 1;
     }
   }
-  // vectors past the last full tile
-  for (uint64_t i = ntiles * kTile + static_cast<uint64_t>(blockIdx.x) * BLOCK + threadIdx.x; i < a.nvec;
-       i += static_cast<uint64_t>(gridDim.x) * BLOCK)
-    acc[0] += a.v[i][0] + a.v[i][1];
+  // vectors past the last full tile (MODE 7 covers them in its dynamic part)
+  if constexpr (MODE != 7)
+    for (uint64_t i = ntiles * kTile + static_cast<uint64_t>(blockIdx.x) * BLOCK + threadIdx.x; i < a.nvec;
+         i += static_cast<uint64_t>(gridDim.x) * BLOCK)
+      acc[0] += a.v[i][0] + a.v[i][1];
   double s = 0.0;
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) s += acc[u];
@@ -271,7 +365,7 @@ int main(int argc, char** argv) {
     else if (!std::strncmp(argv[i], "--iters=", 8)) iters = std::atoi(argv[i] + 8);
     else if (!std::strncmp(argv[i], "--set=", 6)) set = argv[i] + 6;
     else {
-      std::fprintf(stderr, "usage: wg_timeline [--n=N] [--rounds=R] [--iters=I] [--set=mlp|sched]\n");
+      std::fprintf(stderr, "usage: wg_timeline [--n=N] [--rounds=R] [--iters=I] [--set=mlp|sched|rotate|steal|shift|wavetail|window]\n");
       return 1;
     }
   }
@@ -307,6 +401,52 @@ int main(int argc, char** argv) {
         mk<512, 16, false, 5>("rot1 512x16x1", 1, 1),
         mk<256, 4, false, 0>("s 256x4x2", 2),
         mk<256, 4, false, 5>("rot1 256x4x2", 2, 1),
+    };
+  } else if (set == "shift") {
+    // (XCD, address residue) affinity: every shift for the production plans (grids are multiples of 8)
+    vars = {
+        mk<256, 2, false, 6>("sh0 256x2x3", 3, 0), mk<256, 2, false, 6>("sh1 256x2x3", 3, 1),
+        mk<256, 2, false, 6>("sh2 256x2x3", 3, 2), mk<256, 2, false, 6>("sh3 256x2x3", 3, 3),
+        mk<256, 2, false, 6>("sh4 256x2x3", 3, 4), mk<256, 2, false, 6>("sh5 256x2x3", 3, 5),
+        mk<256, 2, false, 6>("sh6 256x2x3", 3, 6), mk<256, 2, false, 6>("sh7 256x2x3", 3, 7),
+        mk<256, 8, false, 6>("sh0 256x8x1", 1, 0), mk<256, 8, false, 6>("sh1 256x8x1", 1, 1),
+        mk<256, 8, false, 6>("sh2 256x8x1", 1, 2), mk<256, 8, false, 6>("sh3 256x8x1", 1, 3),
+        mk<256, 8, false, 6>("sh4 256x8x1", 1, 4), mk<256, 8, false, 6>("sh5 256x8x1", 1, 5),
+        mk<256, 8, false, 6>("sh6 256x8x1", 1, 6), mk<256, 8, false, 6>("sh7 256x8x1", 1, 7),
+        mk<512, 8, false, 6>("sh0 512x8x1", 1, 0), mk<512, 8, false, 6>("sh1 512x8x1", 1, 1),
+        mk<512, 8, false, 6>("sh2 512x8x1", 1, 2), mk<512, 8, false, 6>("sh3 512x8x1", 1, 3),
+        mk<512, 8, false, 6>("sh4 512x8x1", 1, 4), mk<512, 8, false, 6>("sh5 512x8x1", 1, 5),
+        mk<512, 8, false, 6>("sh6 512x8x1", 1, 6), mk<512, 8, false, 6>("sh7 512x8x1", 1, 7),
+    };
+  } else if (set == "window") {
+    // explicit in-flight window per thread (MODE 100 + D) against hipcc's own schedule (MODE 0)
+    vars = {
+        mk<512, 16, false, 0>("s 512x16x1", 1),
+        mk<512, 16, false, 102>("w2 512x16x1", 1), mk<512, 16, false, 104>("w4 512x16x1", 1),
+        mk<512, 16, false, 108>("w8 512x16x1", 1), mk<512, 16, false, 116>("w16 512x16x1", 1),
+        mk<256, 8, false, 0>("s 256x8x1", 1),
+        mk<256, 8, false, 102>("w2 256x8x1", 1), mk<256, 8, false, 104>("w4 256x8x1", 1),
+        mk<256, 8, false, 108>("w8 256x8x1", 1),
+        mk<256, 16, false, 0>("s 256x16x1", 1),
+        mk<256, 16, false, 104>("w4 256x16x1", 1), mk<256, 16, false, 108>("w8 256x16x1", 1),
+        mk<256, 16, false, 116>("w16 256x16x1", 1),
+        mk<512, 8, false, 0>("s 512x8x1", 1),
+        mk<512, 8, false, 104>("w4 512x8x1", 1), mk<512, 8, false, 108>("w8 512x8x1", 1),
+        mk<256, 2, false, 0>("s 256x2x3", 3), mk<256, 2, false, 102>("w2 256x2x3", 3),
+        mk<256, 4, false, 104>("w4 256x4x2", 2), mk<256, 4, false, 102>("w2 256x4x2", 2),
+    };
+  } else if (set == "wavetail") {
+    // static rounds + a dynamic per-wave tail (MODE 7): chunk = wave-tiles per granule, tail = % of tiles
+    vars = {
+        mk<256, 8, false, 0>("s 256x8x1", 1),
+        mk<256, 8, false, 7>("wt 256x8x1 c4 t4", 1, 4, 4), mk<256, 8, false, 7>("wt 256x8x1 c4 t8", 1, 4, 8),
+        mk<256, 8, false, 7>("wt 256x8x1 c8 t8", 1, 8, 8), mk<256, 8, false, 7>("wt 256x8x1 c2 t8", 1, 2, 8),
+        mk<256, 8, false, 7>("wt 256x8x1 c4 t15", 1, 4, 15),
+        mk<256, 2, false, 0>("s 256x2x3", 3),
+        mk<256, 2, false, 7>("wt 256x2x3 c8 t8", 3, 8, 8), mk<256, 2, false, 7>("wt 256x2x3 c16 t8", 3, 16, 8),
+        mk<256, 2, false, 7>("wt 256x2x3 c8 t15", 3, 8, 15),
+        mk<512, 16, false, 0>("s 512x16x1", 1),
+        mk<512, 16, false, 7>("wt 512x16x1 c2 t8", 1, 2, 8),
     };
   } else if (set == "steal") {
     vars = {
@@ -357,14 +497,23 @@ int main(int argc, char** argv) {
     const uint64_t ntiles = nvec / tile;
     uint64_t grid = std::min<uint64_t>(static_cast<uint64_t>(cus) * x.wpc, std::max<uint64_t>(ntiles, 1));
     TArgs a{v, nvec, partials, ctr, counter, 0, 0, 0, st, qctr};
-    if (!x.dyn && x.tailpct > 0) {  // tail-steal: chunk = granule tiles, tail = tailpct % of tiles
+    if (x.kern == body<256, 8, false, 7> || x.kern == body<256, 2, false, 7> || x.kern == body<512, 16, false, 7>) {
+      // wave tail: whole static rounds for the first (100 - tailpct) % of tiles, the rest dynamic
+      const uint64_t rounds = static_cast<uint64_t>(std::floor(ntiles * (1.0 - x.tailpct / 100.0))) / grid;
+      a.nbig = rounds * grid;
+      a.chunk = x.chunk;
+      const uint64_t gsz = 64ull * x.unroll * x.chunk;
+      const uint64_t v0 = a.nbig * tile;
+      const uint64_t ng = nvec > v0 ? (nvec - v0 + gsz - 1) / gsz : 0;
+      a.nchunks = (ng + 7) / 8;
+    } else if (!x.dyn && x.tailpct > 0) {  // tail-steal: chunk = granule tiles, tail = tailpct % of tiles
       const uint64_t tail = static_cast<uint64_t>(std::ceil(ntiles * x.tailpct / 100.0));
       a.nbig = ntiles - std::min(tail, ntiles);
       a.chunk = x.chunk;
       const uint64_t granules = (ntiles - a.nbig + x.chunk - 1) / x.chunk;
       a.nchunks = (granules + 7) / 8;
     }
-    if (!x.dyn && x.chunk) a.chunk = x.chunk;  // MODE 3: run length; MODE 5: rotation step
+    if (!x.dyn && x.chunk && !a.nchunks) a.chunk = x.chunk;  // MODE 3: run length; MODE 5: rotation step; MODE 6: shift
     if (x.dyn) {
       const uint64_t tail = static_cast<uint64_t>(std::ceil(ntiles * x.tailpct / 100.0));
       a.chunk = x.chunk;

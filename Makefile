@@ -44,7 +44,7 @@ COMMLIB     := $(BUILD)/lib/libmireduce_comm.a
 APPS := $(BUILD)/bin/reduction $(BUILD)/bin/reduce_xgmi $(BUILD)/bin/bandwidth_test
 MPI_APP := $(BUILD)/bin/reduce_mpi
 
-.PHONY: all python apps mpi clean asan unit diag examples
+.PHONY: all python apps mpi clean asan unit diag examples window_ab
 all: python apps mpi unit diag examples
 
 python: $(PYEXT)
@@ -108,6 +108,15 @@ diag: $(BUILD)/bin/wg_timeline
 $(BUILD)/bin/wg_timeline: tools/wg_timeline.hip
 	@mkdir -p $(dir $@)
 	$(HIPCC) -std=c++17 -O3 --offload-arch=$(ARCH) $< -o $@
+
+# Production-kernel A/B of the streaming body's load schedule (profiles/r3_window/).
+window_ab: $(BUILD)/bin/window_ab
+$(BUILD)/obj/tools/window_ab.o: tools/window_ab.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+$(BUILD)/bin/window_ab: $(BUILD)/obj/tools/window_ab.o $(LIB)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive $(LDLIBS) -o $@
 
 # C++ library consumer example (examples/cpp_consumer; the CMake build links it via find_package).
 examples: $(BUILD)/bin/cpp_consumer

@@ -30,6 +30,11 @@ struct ReduceConfig {
   int groups = 0;         // fan-in shards of the arrival ticket (<= 64)
   int policy = -1;        // streaming-load cache policy: -1 auto, 0 default, 1 non-temporal (nt)
   int pipeline = -1;      // software-pipelined body: -1 auto, 0 off, 1 on (BLOCK*UNROLL <= 8192)
+  // Streaming body's load schedule: -1 auto (tuned), 0 hipcc's own, 2 or 4 = an explicit window of
+  // that many 16-byte loads per thread, the next one issued before the oldest is consumed
+  // (non-temporal policy, 256/512 threads, unroll 2..8 divisible by it; otherwise hipcc's).
+  // profiles/r3_window/.
+  int window = -1;
   bool single_pass = true;   // last-arriver finalisation vs a second finalize launch
   // Fused cross-rank finish: XrankChannel::device_desc() (xrank.hpp). The launch then writes the
   // fold over every rank's partial into out (single-pass only).
@@ -51,6 +56,7 @@ struct LaunchPlan {
   int groups = 0;
   bool nontemporal = true;
   bool pipelined = false;
+  int window = 0;      // explicit load window per thread (0: hipcc's schedule)
   bool single_pass = true;
   bool poll = false;   // single-pass fan-in: polled tagged slots (default, no tickets)
   bool flat = false;   // ticketed fan-in: flat (final arriver folds every partial) vs two-level

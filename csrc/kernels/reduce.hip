@@ -15,6 +15,8 @@ namespace {
 using namespace detail;
 
 int block_index(int b) { return b == 256 ? 0 : (b == 512 ? 1 : (b == 1024 ? 2 : -1)); }
+// Table body slot of a plan: 0 hipcc's schedule, 1 pipelined, 2 / 3 explicit window 2 / 4.
+int body_index(const LaunchPlan& p) { return p.window == 2 ? 2 : (p.window == 4 ? 3 : (p.pipelined ? 1 : 0)); }
 int unroll_index(int u) { return u == 2 ? 0 : (u == 4 ? 1 : (u == 8 ? 2 : (u == 16 ? 3 : -1))); }
 
 // combo index: (op, dtype, acc) → 0..28
@@ -88,7 +90,7 @@ const Table& table() {
 //   8 GB f16 max        512 x 4 x 1 7.18, 256 x 4 x 2 7.14 (profiles/r1_session3/tune_half.txt)
 // Fewer, fatter workgroups beat the "fill every wave slot" grid (8 WG/CU: 6.91 TB/s at 8 GB).
 struct Defaults {
-  int block, unroll, wg_per_cu, policy, pipeline;
+  int block, unroll, wg_per_cu, policy, pipeline, window;
 };
 Defaults tuned_defaults(size_t bytes, DType t) {
   constexpr size_t MB = 1ull << 20;
@@ -100,11 +102,16 @@ Defaults tuned_defaults(size_t bytes, DType t) {
   // forcing all 16 up front with a sched_barrier was slower still: 6.95 TB/s, r2_plan/run2.sh.)
   // 4-byte types: one 512-thread WG per CU, 4 vectors per lane (tools/tune_types.sh,
   // profiles/r1_session3/tune_types.txt: f32 7.17, i32 7.19 vs 7.14).
-  if (dtype_size(t) == 8 && bytes >= 3072 * MB) return {256, 8, 1, 1, 0};
-  if (dtype_size(t) == 4 && bytes >= 3072 * MB) return {512, 4, 1, 1, 0};
-  if (dtype_is_half(t) && bytes > 192 * MB) return {256, 4, 2, 1, 0};
-  if (bytes > 192 * MB) return {256, 2, 3, 1, 0};
-  return {256, 4, 3, 1, 0};
+  // Round 3 (profiles/r3_window/, production kernel, same box, 7 interleaved rounds): 8-byte types
+  // above 192 MB stream fastest as 256 threads x 8 vectors x 1 WG per CU with an explicit load
+  // window of 4 (~18 loads in flight per CU): 8 GB 1092.1 vs 1112.4 us for hipcc's schedule of
+  // the same plan, 1 GB 141.0 vs 144.5 us for 256x2x3. (hipcc's own schedule of a plan moves with
+  // unrelated kernel code, profiles/r3_regress/; the explicit window does not.)
+  if (dtype_size(t) == 8 && bytes > 192 * MB) return {256, 8, 1, 1, 0, 4};
+  if (dtype_size(t) == 4 && bytes >= 3072 * MB) return {512, 4, 1, 1, 0, 0};
+  if (dtype_is_half(t) && bytes > 192 * MB) return {256, 4, 2, 1, 0, 0};
+  if (bytes > 192 * MB) return {256, 2, 3, 1, 0, 0};
+  return {256, 4, 3, 1, 0, 0};
 }
 constexpr int kDefaultGroups = 8;
 constexpr int kOneGroupGrid = 64;
@@ -246,6 +253,14 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   p.pipelined = (cfg.pipeline < 0 ? d.pipeline == 1 : cfg.pipeline == 1) && p.block * p.unroll <= 8192;
   MIREDUCE_REQUIRE(block_index(p.block) >= 0, "block must be 256, 512 or 1024");
   MIREDUCE_REQUIRE(unroll_index(p.unroll) >= 0, "unroll must be 2, 4, 8 or 16");
+  MIREDUCE_REQUIRE(cfg.window == -1 || cfg.window == 0 || cfg.window == 2 || cfg.window == 4,
+                   "window must be 0, 2 or 4");
+  {  // an explicit window where one is instantiated (non-temporal, not pipelined), else hipcc's schedule
+    const int w = cfg.window < 0 ? d.window : cfg.window;
+    const bool explicit_plan = cfg.block || cfg.unroll;  // a window tuned for the default plan only
+    const int wd = cfg.window < 0 && explicit_plan ? 0 : w;
+    p.window = (wd > 0 && p.nontemporal && !p.pipelined && window_ok(p.block, p.unroll, wd)) ? wd : 0;
+  }
   const size_t vec = 16 / es;
   const uintptr_t addr = reinterpret_cast<uintptr_t>(in);
   MIREDUCE_REQUIRE(n == 0 || addr % es == 0, "input pointer is not aligned to its element size");
@@ -310,7 +325,7 @@ LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out
   a.slots = p.poll ? ws.slots() : nullptr;
   a.fan = ws.fan();
   a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
-  const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0];
+  const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][body_index(p)];
   fn(a, p.grid, stream);
   MIREDUCE_HIP_THROW(hipGetLastError());
   if (!p.single_pass) reduce_finalize(ws.partials(), p.grid, acc, op, out, stream);
@@ -343,7 +358,7 @@ BoundReduce::BoundReduce(const void* in, size_t n, DType t, Op op, DType acc, vo
   a.slots = p.poll ? ws.slots() : nullptr;
   a.fan = ws.fan();
   a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
-  impl_ = new Impl{a, table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0],
+  impl_ = new Impl{a, table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][body_index(p)],
                    p, op, acc, &ws};
 }
 
@@ -372,7 +387,7 @@ LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, 
   kern::Args a = make_args(in, p, t, c2);
   a.partials = partials;
   a.groups = 0;
-  const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][p.pipelined ? 1 : 0];
+  const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][body_index(p)];
   fn(a, p.grid, stream);
   MIREDUCE_HIP_THROW(hipGetLastError());
   return p;
@@ -433,11 +448,16 @@ std::vector<std::string> compiled_variants() {
   std::vector<std::string> v;
   for (int b : kBlocks)
     for (int u : kUnrolls)
-      for (int nt = 0; nt < 2; ++nt)
+      for (int nt = 0; nt < 2; ++nt) {
         for (int pp = 0; pp < 2; ++pp)
           if (!pp || b * u <= 8192)
             v.push_back("block=" + std::to_string(b) + " unroll=" + std::to_string(u) +
                         (nt ? " policy=nt" : " policy=default") + (pp ? " pipelined" : ""));
+        for (int w : {2, 4})
+          if (nt && window_ok(b, u, w))
+            v.push_back("block=" + std::to_string(b) + " unroll=" + std::to_string(u) + " policy=nt window=" +
+                        std::to_string(w));
+      }
   return v;
 }
 

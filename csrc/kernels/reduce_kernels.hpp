@@ -185,6 +185,12 @@ __device__ __forceinline__ AccT xrank_finish(const XrankDesc* d, const XrankLane
   return wave_reduce<OpT>(v);
 }
 
+template <class V, bool NT>
+__device__ __forceinline__ V ld16(const V* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 template <class V, int BLOCK, int UNROLL, bool NT>
 __device__ __forceinline__ void load_tile(V (&v)[UNROLL], const V* p) {
 #pragma unroll
@@ -203,10 +209,69 @@ __device__ __forceinline__ void consume_tile(AccT (&acc)[UNROLL], const V (&v)[U
   }
 }
 
+// Explicit load window: the thread's loads over its tiles t0, t0+step, ... < t1 form one sequence
+// held in WIN registers — each step issues the load WIN ahead and then consumes the oldest (so
+// WIN + 1 are in flight at each issue, WIN after each wait; STRICT consumes first: WIN at most);
+// a sched_barrier between steps pins the interleave (hipcc's own grouping of the plain body moves
+// with unrelated code in the kernel: profiles/r3_regress). Measured (profiles/r3_window/): the
+// loose form with ~18-20 loads in flight per CU is fastest (256x8x1 with 4: 8 GB 1092 vs 1112 us
+// for hipcc's schedule, 1 GB 141.0 vs 144.5 us for 256x2x3), the strict form 1-70 % slower. The loads are raw buffer loads:
+// the tile base rides in a wave-uniform descriptor (SGPRs), the lane's byte offset in one VGPR and
+// each load's tile offset in soffset, so a load costs no address arithmetic, and the non-temporal
+// bit is part of the instruction (aux = 2: a plain-pointer nontemporal load lost it under this
+// interleave, profiles/r3_window/).
+constexpr int kAuxNT = 2;  // buffer-load cache policy: nt
+
+template <class V>
+__device__ __forceinline__ V ld_buf_nt(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kAuxNT));
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
+}
+
+template <class OpT, class T, class AccT, class V, int N, int BLOCK, int UNROLL, int WIN, bool STRICT = true>
+__device__ __forceinline__ void stream_window(AccT (&acc)[UNROLL], const V* __restrict__ vin, uint64_t t0,
+                                              uint64_t t1, uint64_t step) {
+  static_assert(UNROLL % WIN == 0, "the window must divide the unroll");
+  constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
+  constexpr uint32_t kStride = BLOCK * 16;  // bytes between a lane's loads within a tile
+  if (t0 >= t1) return;
+  const uint32_t voff = threadIdx.x * 16;
+  __amdgpu_buffer_rsrc_t rp = tile_rsrc(vin + t0 * kTile);
+  V buf[WIN];
+#pragma unroll
+  for (int j = 0; j < WIN; ++j) buf[j] = ld_buf_nt<V>(rp, voff, j * kStride);
+  uint64_t t = t0;
+  for (; t + step < t1; t += step) {
+    const __amdgpu_buffer_rsrc_t rq = tile_rsrc(vin + (t + step) * kTile);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(buf[u % WIN], k)));
+      // STRICT: the consume completes before the next load issues (at most WIN in flight);
+      // otherwise hipcc hoists the load above the consume (WIN + 1 in flight at its issue).
+      if constexpr (STRICT) __builtin_amdgcn_sched_barrier(0);
+      const int j = u + WIN;
+      buf[u % WIN] = j < UNROLL ? ld_buf_nt<V>(rp, voff, j * kStride) : ld_buf_nt<V>(rq, voff, (j - UNROLL) * kStride);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    rp = rq;
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {  // the last tile: no loads of a next one
+#pragma unroll
+    for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(buf[u % WIN], k)));
+    const int j = u + WIN;
+    if (j < UNROLL) buf[u % WIN] = ld_buf_nt<V>(rp, voff, j * kStride);
+  }
+}
+
 // PIPE: software-pipelined body — tile t+grid's loads are issued before tile t is consumed, so
 // a wave always has UNROLL loads in flight while it computes (two register sets). The loop has
 // no per-load condition (the last tile is peeled), see cdna_hip_programming.md §5 trap (c).
-template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT, bool PIPE>
+template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT, bool PIPE, int WIN = 0>
 __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   using V = typename Vec16<T>::type;
   constexpr int N = Vec16<T>::N;
@@ -248,6 +313,10 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       }
       consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, cur);
     }
+  } else if constexpr (WIN > 0) {
+    stream_window<OpT, T, AccT, V, N, BLOCK, UNROLL, WIN, false>(acc, vin, t0, t1, step);
+  } else if constexpr (WIN < 0) {  // strict window (experiments only: tools/window_ab.hip)
+    stream_window<OpT, T, AccT, V, N, BLOCK, UNROLL, -WIN, true>(acc, vin, t0, t1, step);
   } else {
     for (uint64_t t = t0; t < t1; t += step) {
       V v[UNROLL];
@@ -551,9 +620,9 @@ namespace detail {
 
 using LaunchFn = void (*)(const kern::Args&, int grid, hipStream_t);
 
-template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT, bool PIPE>
+template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT, bool PIPE, int WIN = 0>
 void launch_stream(const kern::Args& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((kern::reduce_stream<OpT, T, AccT, BLOCK, UNROLL, NT, PIPE>), dim3(grid), dim3(BLOCK),
+  hipLaunchKernelGGL((kern::reduce_stream<OpT, T, AccT, BLOCK, UNROLL, NT, PIPE, WIN>), dim3(grid), dim3(BLOCK),
                      0, s, a);
 }
 
@@ -564,13 +633,19 @@ constexpr int kNumUnrolls = 4;
 
 constexpr int kCombos = 29;
 
+// Body schedules: 0 = hipcc's own schedule of the plain loop, 1 = software-pipelined (PIPE),
+// 2 / 3 = explicit load window of 2 / 4 registers per thread (stream_window; nt only).
+constexpr int kNumBodies = 4;
 struct Table {
-  LaunchFn fn[kCombos][kNumBlocks][kNumUnrolls][2][2];  // [..][policy nt][pipelined]
+  LaunchFn fn[kCombos][kNumBlocks][kNumUnrolls][2][kNumBodies];  // [..][policy nt][body]
 };
 
 // Pipelined variants need two register sets of UNROLL 16-byte vectors: only where the
 // per-SIMD register budget allows it (BLOCK * UNROLL <= 8192); elsewhere the plain body.
 constexpr bool pipe_ok(int b, int u) { return b * u <= 8192; }
+// Explicit windows are instantiated for the non-temporal policy, 256- and 512-thread blocks and
+// unroll 2..8 (profiles/r3_window/: the measured winners and their neighbours); elsewhere null.
+constexpr bool window_ok(int b, int u, int w) { return (b == 256 || b == 512) && u <= 8 && u % w == 0; }
 
 template <class OpT, class T, class AccT, int BI, int UI>
 void fill_one(Table& tb, int c) {
@@ -581,6 +656,8 @@ void fill_one(Table& tb, int c) {
   tb.fn[c][BI][UI][1][0] = launch_stream<OpT, T, AccT, B, U, true, false>;
   tb.fn[c][BI][UI][0][1] = launch_stream<OpT, T, AccT, B, U, false, P>;
   tb.fn[c][BI][UI][1][1] = launch_stream<OpT, T, AccT, B, U, true, P>;
+  if constexpr (window_ok(B, U, 2)) tb.fn[c][BI][UI][1][2] = launch_stream<OpT, T, AccT, B, U, true, false, 2>;
+  if constexpr (window_ok(B, U, 4)) tb.fn[c][BI][UI][1][3] = launch_stream<OpT, T, AccT, B, U, true, false, 4>;
 }
 
 template <class OpT, class T, class AccT, int BI>

@@ -45,6 +45,7 @@ py::dict plan_dict(const LaunchPlan& p) {
   d["groups"] = p.groups;
   d["nontemporal"] = p.nontemporal;
   d["pipelined"] = p.pipelined;
+  d["window"] = p.window;
   d["single_pass"] = p.single_pass;
   d["flat"] = p.flat;
   d["poll"] = p.poll;
@@ -57,8 +58,9 @@ py::dict plan_dict(const LaunchPlan& p) {
 }
 
 ReduceConfig make_cfg(int block, int unroll, int wg_per_cu, int max_blocks, int groups,
-                      int policy, bool single_pass, int pipeline = -1) {
+                      int policy, bool single_pass, int pipeline = -1, int window = -1) {
   ReduceConfig c;
+  c.window = window;
   c.block = block;
   c.unroll = unroll;
   c.wg_per_cu = wg_per_cu;
@@ -173,8 +175,9 @@ PYBIND11_MODULE(_C, m) {
   py::class_<BoundReduce>(m, "BoundReduce")
       .def(py::init([](Workspace& ws, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out,
                        int block, int unroll, int wg_per_cu, int max_blocks, int groups, int policy,
-                       bool single_pass, int pipeline, uintptr_t xrank) {
-             ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline);
+                       bool single_pass, int pipeline, uintptr_t xrank, int window) {
+             ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline,
+                                         window);
              cfg.xrank = as_ptr<const void>(xrank);
              return new BoundReduce(as_ptr<const void>(in), n, static_cast<DType>(dtype), static_cast<Op>(op),
                                     static_cast<DType>(acc), as_ptr<void>(out), ws, cfg);
@@ -182,7 +185,8 @@ PYBIND11_MODULE(_C, m) {
            py::arg("ws"), py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"), py::arg("acc"),
            py::arg("out_ptr"), py::arg("block") = 0, py::arg("unroll") = 0, py::arg("wg_per_cu") = 0,
            py::arg("max_blocks") = 0, py::arg("groups") = 0, py::arg("policy") = -1,
-           py::arg("single_pass") = true, py::arg("pipeline") = -1, py::arg("xrank") = 0, py::keep_alive<1, 2>())
+           py::arg("single_pass") = true, py::arg("pipeline") = -1, py::arg("xrank") = 0, py::arg("window") = -1,
+           py::keep_alive<1, 2>())
       .def("launch", [](const BoundReduce& b, uintptr_t stream, uintptr_t out) { b.launch(as_stream(stream), as_ptr<void>(out)); },
            py::arg("stream"), py::arg("out_ptr") = 0)
       .def_property_readonly("plan", [](const BoundReduce& b) { return plan_dict(b.plan()); })
@@ -259,8 +263,8 @@ PYBIND11_MODULE(_C, m) {
       [](Workspace& ws, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out,
          uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks, int groups,
          int policy, bool single_pass, int pipeline, uint64_t fanin_bound_ticks, int debug_delay_wg,
-         uint64_t debug_delay_ticks) {
-        ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline);
+         uint64_t debug_delay_ticks, int window) {
+        ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline, window);
         cfg.fanin_bound_ticks = fanin_bound_ticks;
         cfg.debug_delay_wg = debug_delay_wg;
         cfg.debug_delay_ticks = debug_delay_ticks;
@@ -274,21 +278,21 @@ PYBIND11_MODULE(_C, m) {
       py::arg("unroll") = 0, py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0,
       py::arg("groups") = 0, py::arg("policy") = -1, py::arg("single_pass") = true,
       py::arg("pipeline") = -1, py::arg("fanin_bound_ticks") = 0, py::arg("debug_delay_wg") = -1,
-      py::arg("debug_delay_ticks") = 0);
+      py::arg("debug_delay_ticks") = 0, py::arg("window") = -1);
 
   m.def(
       "plan",
       [](uintptr_t in, uint64_t n, int dtype, int num_cus, int max_grid, int block, int unroll,
-         int wg_per_cu, int max_blocks, int groups, int policy, bool single_pass, int pipeline) {
+         int wg_per_cu, int max_blocks, int groups, int policy, bool single_pass, int pipeline, int window) {
         return plan_dict(plan_reduce(as_ptr<const void>(in), n, static_cast<DType>(dtype),
                                      make_cfg(block, unroll, wg_per_cu, max_blocks, groups,
-                                              policy, single_pass, pipeline),
+                                              policy, single_pass, pipeline, window),
                                      num_cus, max_grid));
       },
       py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("num_cus") = 256,
       py::arg("max_grid") = 16384, py::arg("block") = 0, py::arg("unroll") = 0,
       py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0, py::arg("groups") = 0,
-      py::arg("policy") = -1, py::arg("single_pass") = true, py::arg("pipeline") = -1);
+      py::arg("policy") = -1, py::arg("single_pass") = true, py::arg("pipeline") = -1, py::arg("window") = -1);
 
   m.def(
       "reduce_partials",

@@ -76,6 +76,7 @@ class KernelConfig:
     nontemporal: Optional[bool] = None  # None: size-dependent tuned choice
     single_pass: bool = True
     pipelined: Optional[bool] = None    # None: tuned choice
+    window: Optional[int] = None        # loads in flight per thread: None tuned, 0 hipcc's schedule, 2 | 4
 
     @property
     def policy(self) -> int:
@@ -91,6 +92,7 @@ class KernelConfig:
             policy=self.policy,
             single_pass=self.single_pass,
             pipeline=-1 if self.pipelined is None else int(bool(self.pipelined)),
+            window=-1 if self.window is None else int(self.window),
         )
 
 

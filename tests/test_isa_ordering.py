@@ -15,7 +15,7 @@ from helpers import ROOT, ensure_built
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 pytestmark = pytest.mark.skipif(not os.path.exists(OBJDUMP), reason="llvm-objdump not available")
 
-STREAM_F64 = "_ZN8mireduce4kern13reduce_streamINS_5SumOpEddLi256ELi8ELb1ELb0EEEvNS0_4ArgsE"  # the >= 3 GB f64 plan
+STREAM_F64 = "_ZN8mireduce4kern13reduce_streamINS_5SumOpEddLi256ELi8ELb1ELb0ELi0EEEvNS0_4ArgsE"  # the >= 3 GB f64 plan
 DIRECT_F64_W8 = "_ZN8mireduce4kern13direct_kernelINS_5SumOpEdLi8EEEvPKNS_10DirectDescEmi"
 
 
@@ -138,3 +138,35 @@ def test_headline_kernel_keeps_its_loads_in_flight(tmp_path):
         elif ln.startswith("s_waitcnt") or ln.startswith("v_add_f64"):
             run = 0
     assert best >= 8, best
+
+
+HEADLINE_F64 = "_ZN8mireduce4kern13reduce_streamINS_5SumOpEddLi256ELi8ELb1ELb0ELi4EEEvNS0_4ArgsE"  # 8-byte > 192 MB
+
+
+def test_headline_kernel_explicit_load_window(tmp_path):
+    # The tuned plan for 8-byte arrays above 192 MB (the 1e9-double headline and the 1 GB N=8 shard):
+    # 256 x 8 with an explicit load window of 4 (reduce_kernels.hpp stream_window; profiles/r3_window).
+    # Its streaming loop is raw buffer loads that keep the nt bit (a plain-pointer nontemporal load
+    # lost it under this interleave) in the pinned order "issue, wait until 4 remain, consume":
+    # 8 x (buffer_load nt, s_waitcnt vmcnt(4), 2 x v_add_f64) per tile, no waterfall around them.
+    ins = _disasm(tmp_path, "reduce_tab_f64.o", HEADLINE_F64)
+    seq = []
+    for ln in ins:
+        if ln.startswith("buffer_load_dwordx4"):
+            seq.append("B" if ln.endswith(" nt") else "Bplain")
+        elif ln.startswith("global_load_dwordx4"):
+            seq.append("G")
+        elif ln.startswith("s_waitcnt vmcnt"):
+            seq.append("W" + re.search(r"vmcnt\((\d+)\)", ln).group(1))
+        elif ln.startswith("v_add_f64"):
+            seq.append("a")
+        elif ln.startswith("s_and_saveexec"):
+            seq.append("X")
+    s = " ".join(seq)
+    assert "Bplain" not in s, "a streaming buffer load lost its nt bit"
+    assert " ".join(["B W4 a a"] * 8) in s, s[:300]
+    # the fan-in epoch load sits in the prologue and no vmcnt(0) separates it from the first body load
+    ep = _first(ins, r"^global_load_dword v\d+, v\d+, s\[\d+:\d+\] sc1$")
+    body = _first(ins, r"^buffer_load_dwordx4 .* nt$")
+    assert ep is not None and body is not None and ep < body
+    assert _first(ins, r"^s_waitcnt vmcnt\(0\)", ep) is None or _first(ins, r"^s_waitcnt vmcnt\(0\)", ep) > body

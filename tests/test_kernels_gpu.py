@@ -336,3 +336,56 @@ def test_planted_extremes_large(dt, where):
     assert reduce(x, "max").item() == hi
     del base, x
     torch.cuda.empty_cache()
+
+
+# ---- explicit load windows (reduce_kernels.hpp stream_window; round 3, profiles/r3_window)
+WINDOWS = [(b, u, w) for b in (256, 512) for u in (2, 4, 8) for w in (2, 4) if u % w == 0]
+
+
+@pytest.mark.parametrize("block,unroll,window", WINDOWS, ids=lambda v: str(v))
+@pytest.mark.parametrize("dt,op,acc", COMBOS, ids=lambda v: str(v).replace("torch.", ""))
+@pytest.mark.parametrize("n,misalign", [(5, 0), (1_000_003, 1), (3_000_017, 0)])
+def test_window_variants(block, unroll, window, dt, op, acc, n, misalign):
+    # every instantiated window against the fp64/int64 reference: tiny n (no full tile: the body is
+    # skipped), a misaligned head, and tile counts that do not divide the grid
+    base = torch.empty(n + misalign, dtype=dt, device=DEV)
+    fill_(base, "fullrange" if not dt.is_floating_point else "uniform", seed=n + 13 * misalign + window)
+    x = base[misalign:]
+    r = Reducer(DEV, config=KernelConfig(block=block, unroll=unroll, window=window))
+    got = r(x, op, acc).item()
+    assert r.last_plan["window"] == window and r.last_plan["nontemporal"]
+    check(got, x, op, acc, n)
+
+
+@pytest.mark.parametrize("dt,op", [(torch.bfloat16, "sum"), (torch.float16, "max"), (torch.float64, "sumsq"),
+                                   (torch.float32, "amax"), (torch.float32, "sumsq")])
+def test_window_fused_and_half_types(dt, op):
+    n = 2_000_011
+    x = torch.empty(n, dtype=dt, device=DEV)
+    fill_(x, "uniform", seed=5)
+    r = Reducer(DEV, config=KernelConfig(block=256, unroll=8, window=4))
+    got = r(x, op).item()
+    xd = x.double()
+    ref = {"sum": lambda: xd.sum(), "max": lambda: xd.max(), "sumsq": lambda: (xd * xd).sum(),
+           "amax": lambda: xd.abs().max()}[op]().item()
+    if op in ("sum", "sumsq"):
+        acc = torch.float64 if dt == torch.float64 or (dt == torch.float32 and op == "sumsq") else torch.float32
+        tol = sum_tolerance(dt, acc, n, (xd * xd).sum().item() if op == "sumsq" else xd.abs().sum().item())
+        assert abs(got - ref) <= tol, (got, ref, tol)
+    else:
+        assert got == ref
+    assert r.last_plan["window"] == 4
+
+
+@pytest.mark.parametrize("dt,op", [(torch.float64, "sum"), (torch.int64, "min"), (torch.int64, "sum")])
+def test_default_plan_above_192mb_uses_the_window(dt, op):
+    # the tuned plan for 8-byte arrays > 192 MB is 256x8x1 with window 4: check it at 320 MB, misaligned
+    n = 40_000_003
+    base = torch.empty(n + 1, dtype=dt, device=DEV)
+    fill_(base, "fullrange" if not dt.is_floating_point else "uniform", seed=77)
+    x = base[1:]
+    r = Reducer(DEV)
+    got = r(x, op).item()
+    p = r.last_plan
+    assert (p["block"], p["unroll"], p["window"]) == (256, 8, 4), p
+    check(got, x, op, dt if op != "sum" or dt.is_floating_point else torch.int64, n)

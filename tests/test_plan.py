@@ -41,20 +41,38 @@ def test_grid_bounds_and_groups(n):
 
 def test_tuned_defaults_by_size():
     C = native()
-    big = C.plan(0, 10**9, F64)            # 8 GB of 8-byte elements
-    assert (big["block"], big["unroll"], big["grid"], big["nontemporal"]) == (256, 8, 256, True)
+    big = C.plan(0, 10**9, F64)            # 8 GB of 8-byte elements: explicit load window 4 (profiles/r3_window)
+    assert (big["block"], big["unroll"], big["grid"], big["nontemporal"], big["window"]) == (256, 8, 256, True, 4)
     mid = C.plan(0, 125_000_000, F64)      # 1 GB: the 8-GPU shard of the north star
-    assert (mid["block"], mid["unroll"], mid["grid"], mid["nontemporal"]) == (256, 2, 768, True)
+    assert (mid["block"], mid["unroll"], mid["grid"], mid["nontemporal"], mid["window"]) == (256, 8, 256, True, 4)
     l3 = C.plan(0, 1 << 25, F64)           # 256 MB: nt is fast warm and cold (plan_256mb.csv)
-    assert (l3["block"], l3["unroll"], l3["grid"], l3["nontemporal"]) == (256, 2, 768, True)
+    assert (l3["block"], l3["unroll"], l3["grid"], l3["nontemporal"], l3["window"]) == (256, 8, 256, True, 4)
+    small = C.plan(0, 1 << 24, F64)        # 128 MB (the reference default): hipcc's schedule
+    assert (small["block"], small["unroll"], small["window"]) == (256, 4, 0)
     # no size band picks the default (non-nt) policy: it collapses to 2.7 TB/s on a cold cache
     assert all(C.plan(0, n, F64)["nontemporal"] for n in (1, 1 << 20, 3 << 23, 1 << 25, 3 << 24, 1 << 27))
     f32 = C.plan(0, 2 * 10**9, 2)          # 8 GB of fp32: one 512-thread WG per CU, 4 vectors per lane
     assert (f32["block"], f32["unroll"], f32["grid"]) == (512, 4, 256)
     i64 = C.plan(0, 10**9, 1)              # 8 GB of int64: like fp64
-    assert (i64["block"], i64["unroll"], i64["grid"]) == (256, 8, 256)
+    assert (i64["block"], i64["unroll"], i64["grid"], i64["window"]) == (256, 8, 256, 4)
     f32_1g = C.plan(0, 250_000_000, 2)     # 1 GB keeps the 256x2x3 plan
-    assert (f32_1g["block"], f32_1g["unroll"]) == (256, 2)
+    assert (f32_1g["block"], f32_1g["unroll"], f32_1g["window"]) == (256, 2, 0)
+
+
+def test_window_only_where_instantiated():
+    C = native()
+    # explicit plans keep hipcc's schedule unless a window is asked for
+    assert C.plan(0, 10**9, F64, block=256, unroll=8)["window"] == 0
+    assert C.plan(0, 10**9, F64, block=256, unroll=8, window=4)["window"] == 4
+    # not instantiated: 1024 threads, unroll 16, the default (non-nt) policy, pipelined bodies
+    assert C.plan(0, 10**9, F64, block=1024, unroll=4, window=2)["window"] == 0
+    assert C.plan(0, 10**9, F64, block=256, unroll=16, window=4)["window"] == 0
+    assert C.plan(0, 10**9, F64, block=256, unroll=4, window=2, policy=0)["window"] == 0
+    assert C.plan(0, 10**9, F64, block=256, unroll=4, window=2, pipeline=1)["window"] == 0
+    assert C.plan(0, 10**9, F64, block=256, unroll=2, window=4)["window"] == 0  # 4 does not divide 2
+    assert C.plan(0, 10**9, F64, window=0)["window"] == 0  # the tuned plan with hipcc's schedule
+    with pytest.raises(C.NativeError):
+        C.plan(0, 10, F64, window=3)
 
 
 def test_overrides_and_caps():
@@ -93,9 +111,12 @@ def test_ladder_geometry_matches_reference_planner(kernel, n):
 
 def test_compiled_variants_cover_grid():
     v = native().compiled_variants()
-    plain = [s for s in v if not s.endswith("pipelined")]
+    plain = [s for s in v if not s.endswith("pipelined") and "window" not in s]
     piped = [s for s in v if s.endswith("pipelined")]
+    win = [s for s in v if "window" in s]
     assert len(plain) == 3 * 4 * 2  # block x unroll x policy
+    # explicit windows: nt, 256/512 threads, unroll 2..8 divisible by the window
+    assert len(win) == 2 * (3 + 2) and "block=256 unroll=4 policy=nt window=2" in v
     # software-pipelined bodies exist where BLOCK * UNROLL <= 8192 (two register sets)
     assert len(piped) == 2 * sum(1 for b in (256, 512, 1024) for u in (2, 4, 8, 16) if b * u <= 8192)
     assert "block=512 unroll=16 policy=nt" in v

@@ -320,9 +320,11 @@ def test_bench_plan_tuning_at_the_eight_gpu_shard(tmp_path):
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["verified"] is True
     pt = d["plan_tuning"]
-    assert set(pt["gbps"]) == {"tuned default", "256x8x1"} and pt["chosen"] == max(pt["gbps"], key=pt["gbps"].get)
+    assert set(pt["gbps"]) == {"tuned default", "256x4x2 window 2", "256x2x3 hipcc schedule"}
+    assert pt["chosen"] == max(pt["gbps"], key=pt["gbps"].get)
     plan = d["config"]["kernel_plan"]
-    assert (plan["block"], plan["unroll"]) == ((256, 8) if pt["chosen"] == "256x8x1" else (256, 2))
+    want = {"tuned default": (256, 8, 4), "256x4x2 window 2": (256, 4, 2), "256x2x3 hipcc schedule": (256, 2, 0)}
+    assert (plan["block"], plan["unroll"], plan["window"]) == want[pt["chosen"]]
 
 
 def test_bench_maxloc_config_skips_plan_tuning(tmp_path):

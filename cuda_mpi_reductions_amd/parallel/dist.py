@@ -99,12 +99,18 @@ def init(backend: Optional[str] = None, device_type: Optional[str] = None,
         device = torch.device("cpu")
     owns = False
     if not dist.is_initialized():
-        if "MASTER_ADDR" not in os.environ:
-            os.environ["MASTER_ADDR"] = "127.0.0.1"
-        if "MASTER_PORT" not in os.environ:
-            os.environ["MASTER_PORT"] = str(_free_port())
         kwargs = dict(backend=backend, rank=rank, world_size=world,
                       timeout=datetime.timedelta(seconds=timeout_s))
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            # A lone process (not launched by torchrun): an in-process store, no TCP rendezvous —
+            # picking a free port and binding it again later can lose the port to another process
+            # in between (EADDRINUSE seen on the GPU box).
+            kwargs["store"] = dist.HashStore()
+        else:
+            if "MASTER_ADDR" not in os.environ:
+                os.environ["MASTER_ADDR"] = "127.0.0.1"
+            if "MASTER_PORT" not in os.environ:
+                os.environ["MASTER_PORT"] = str(_free_port())
         if backend == "nccl":
             kwargs["device_id"] = device  # eager communicator creation, inside the redirect
         with stdout_to_stderr():

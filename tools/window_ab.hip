@@ -3,7 +3,7 @@
 // (reduce_kernels.hpp stream_window), for the plans that matter at the headline sizes. The real
 // kern::reduce_stream with the polled fan-in and a Workspace, hipEvent per launch, rounds
 // interleaved in a shuffled order, median per variant; every launch's result is checked.
-//   build: make window_ab        run: build/bin/window_ab [--n=1e9] [--rounds=7] [--iters=20]
+//   build: make window_ab        run: build/bin/window_ab [--n=1e9] [--rounds=7] [--iters=20] [--type=float]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,9 +33,9 @@ struct Var {
   void (*fn)(const kern::Args&, int, hipStream_t);
 };
 
-template <int B, int U, int W>
+template <int B, int U, int W, class T = double>
 Var mk(const char* name, int wpc) {
-  return {name, B, U, wpc, detail::launch_stream<SumOp, double, double, B, U, true, false, W>};
+  return {name, B, U, wpc, detail::launch_stream<SumOp, T, double, B, U, true, false, W>};
 }
 
 // Control: the first window implementation (plain-pointer nontemporal loads, no sched_barrier
@@ -96,38 +96,51 @@ Var mkg(const char* name, int wpc) {
   return {name, B, U, wpc, launch_global_window<B, U, W>};
 }
 
-__global__ void fill(double* x, uint64_t n) {
+template <class T>
+__global__ void fill(T* x, uint64_t n) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull)
-    x[i] = static_cast<double>(i & 1023);  // exact sums
+    x[i] = static_cast<T>(i & 1023);  // exact sums (fp64 accumulation)
 }
 
 int main(int argc, char** argv) {
   uint64_t n = 1000000000ull;
   int rounds = 7, iters = 20;
+  bool f32 = false;
   for (int i = 1; i < argc; ++i) {
     if (!std::strncmp(argv[i], "--n=", 4)) n = static_cast<uint64_t>(std::atof(argv[i] + 4));
     else if (!std::strncmp(argv[i], "--rounds=", 9)) rounds = std::atoi(argv[i] + 9);
     else if (!std::strncmp(argv[i], "--iters=", 8)) iters = std::atoi(argv[i] + 8);
+    else if (!std::strcmp(argv[i], "--type=float")) f32 = true;
   }
+  const size_t es = f32 ? 4 : 8;
   // l<D>: buffer loads, D registers, the next load issued before the consume (D + 1 in flight at
   // issue; the production window, template WIN = D); w<D>: strict, consume first (WIN = -D);
   // g<D>: the first (plain-pointer) window, control.
-  std::vector<Var> vars = {
+  std::vector<Var> vars64 = {
       mk<256, 8, 0>("256x8x1 hipcc", 1),  mk<256, 2, 0>("256x2x3 hipcc", 3),  mk<512, 16, 0>("512x16x1 hipcc", 1),
       mk<256, 8, 4>("256x8x1 l4", 1),     mk<256, 8, 8>("256x8x1 l8", 1),     mk<256, 8, 2>("256x8x1 l2", 1),
       mk<256, 4, 2>("256x4x2 l2", 2),     mk<256, 4, 4>("256x4x2 l4", 2),     mk<256, 4, 2>("256x4x3 l2", 3),
       mk<512, 8, 2>("512x8x1 l2", 1),     mk<512, 8, 4>("512x8x1 l4", 1),     mk<512, 4, 2>("512x4x1 l2", 1),
       mk<256, 8, 2>("256x8x2 l2", 2),     mk<256, 8, 4>("256x8x2 l4", 2),     mkg<256, 4, 2>("256x4x2 g2", 2),
       mk<256, 8, -4>("256x8x1 w4", 1),    mk<256, 8, -8>("256x8x1 w8", 1),
+  };  std::vector<Var> vars32 = {
+      mk<512, 4, 0, float>("f32 512x4x1 hipcc", 1), mk<256, 2, 0, float>("f32 256x2x3 hipcc", 3),
+      mk<256, 8, 0, float>("f32 256x8x1 hipcc", 1),
+      mk<512, 4, 2, float>("f32 512x4x1 l2", 1),   mk<512, 4, 4, float>("f32 512x4x1 l4", 1),
+      mk<256, 8, 4, float>("f32 256x8x1 l4", 1),   mk<256, 4, 2, float>("f32 256x4x2 l2", 2),
+      mk<512, 8, 4, float>("f32 512x8x1 l4", 1),   mk<256, 8, 2, float>("f32 256x8x2 l2", 2),
   };
+  std::vector<Var>& vars = f32 ? vars32 : vars64;
+
 
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  double* x;
+  void* x;
   double* out;
-  CK(hipMalloc(&x, n * 8));
+  CK(hipMalloc(&x, n * es));
   CK(hipMalloc(&out, 8));
-  fill<<<4096, 256>>>(x, n);
+  if (f32) fill<float><<<4096, 256>>>(static_cast<float*>(x), n);
+  else fill<double><<<4096, 256>>>(static_cast<double*>(x), n);
   CK(hipDeviceSynchronize());
   // closed form of sum(i & 1023)
   const uint64_t full = n / 1024, rem = n % 1024;
@@ -138,7 +151,7 @@ int main(int argc, char** argv) {
     c.block = v.block;
     c.unroll = v.unroll;
     c.wg_per_cu = v.wpc;
-    LaunchPlan p = plan_reduce(x, n, DType::Float64, c, ws.num_cus(), ws.max_grid());
+    LaunchPlan p = plan_reduce(x, n, f32 ? DType::Float32 : DType::Float64, c, ws.num_cus(), ws.max_grid());
     kern::Args a{};
     a.head_ptr = x;
     a.body = x;
@@ -187,14 +200,14 @@ int main(int argc, char** argv) {
       }
     }
   }
-  std::printf("n=%llu doubles (%.3f GB), %d CUs, %d rounds x %d launches, hipEvent per launch\n",
-              static_cast<unsigned long long>(n), n * 8e-9, cus, rounds, iters);
+  std::printf("n=%llu %s (%.3f GB), %d CUs, %d rounds x %d launches, hipEvent per launch\n",
+              static_cast<unsigned long long>(n), f32 ? "floats" : "doubles", n * es * 1e-9, cus, rounds, iters);
   std::printf("%-18s %10s %10s %10s %8s\n", "variant", "med us", "p10 us", "min us", "TB/s");
   for (size_t i = 0; i < vars.size(); ++i) {
     std::vector<double> v = ms[i];
     std::sort(v.begin(), v.end());
     const double med = v[v.size() / 2] * 1e3, p10 = v[v.size() / 10] * 1e3, mn = v[0] * 1e3;
-    std::printf("%-18s %10.1f %10.1f %10.1f %8.3f\n", vars[i].name, med, p10, mn, n * 8.0 / (med * 1e-6) / 1e12);
+    std::printf("%-18s %10.1f %10.1f %10.1f %8.3f\n", vars[i].name, med, p10, mn, n * double(es) / (med * 1e-6) / 1e12);
   }
   return 0;
 }

@@ -65,6 +65,7 @@ struct Options {
   bool batch_timing = false;  // one event pair around all iterations (throughput) vs per iteration
   bool cold = false;          // flush L2 + Infinity Cache before every timed iteration
   int unroll = 0;
+  int window = -1;  // streaming body's load window: -1 tuned, 0 hipcc's schedule, 2 | 4
   int wg_per_cu = 0;
   int policy = -1;
   Pattern pattern = Pattern::SmallInt;  // rand() & 0xFF (reduction.cpp:698-705)
@@ -78,7 +79,7 @@ struct Options {
 
 const std::set<std::string> kKnown = {
     "method", "type", "n", "threads", "kernel", "maxblocks", "cpufinal", "cputhresh", "shmoo",
-    "device", "qatest", "noprompt", "prompt", "help", "version", "quiet", "iterations", "acc", "unroll",
+    "device", "qatest", "noprompt", "prompt", "help", "version", "quiet", "iterations", "acc", "unroll", "window",
     "wg-per-cu", "policy", "pattern", "seed", "fill", "noverify", "json", "log", "master-log",
     "countdown", "shmoo-max", "trace", "timing", "cold", "arg"};
 
@@ -98,6 +99,7 @@ void usage() {
       "  --cold           overwrite a 1 GiB scratch buffer before every timed iteration (evicts the\n"
       "                   256 MB Infinity Cache and the L2s): HBM numbers for small arrays; per-iter timing\n"
       "  --iterations=100 --acc=TYPE --unroll=2|4|8 --wg-per-cu=N --policy=auto|nt|default\n"
+      "  --window=0|2|4   streaming body: hipcc's load schedule (0) or an explicit window (default: tuned)\n"
       "  --pattern=smallint|uniform|fullrange|iotamod --seed=N --fill=host|device --noverify\n"
       "  --device=N --json=PATH --log=FILE|none --master-log=FILE|none (default SdkMasterLog.csv) --qatest\n"
       "  --prompt --countdown\n"
@@ -163,6 +165,7 @@ struct Runner {
     ReduceConfig c;
     c.block = o.threads;
     c.unroll = o.unroll;
+    c.window = o.window;
     c.wg_per_cu = o.wg_per_cu;
     c.max_blocks = o.max_blocks;
     c.policy = o.policy;
@@ -475,7 +478,7 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
     Json j;
     j.set("app", "reduction").set("method", op_name(o.op)).set("type", dtype_cli_name(o.dtype))
         .set("acc", dtype_cli_name(o.acc)).set("n", o.n).set("bytes", static_cast<uint64_t>(bytes))
-        .set("kernel", o.kernel).set("block", r.plan.block).set("grid", r.plan.grid).set("unroll", r.plan.unroll)
+        .set("kernel", o.kernel).set("block", r.plan.block).set("grid", r.plan.grid).set("unroll", r.plan.unroll).set("window", r.plan.window)
         .set("groups", r.plan.groups).set("nontemporal", r.plan.nontemporal).set("cpufinal", o.cpufinal)
         .set("iterations", o.iterations).set("cold", o.cold).set("timing", o.batch_timing && !o.cold ? "batch" : "per-iter").set("avg_ms", t.avg_ms).set("median_ms", st.median).set("min_ms", st.min)
         .set("max_ms", st.max).set("std_ms", st.stddev).set("gb_per_s", secs > 0 ? bytes / secs / kGB : 0.0)
@@ -589,6 +592,7 @@ int main(int argc, char** argv) {
     o.cputhresh = args.int_or<int>("cputhresh", o.cputhresh);
     o.iterations = args.int_or<int>("iterations", o.iterations);
     o.unroll = args.int_or<int>("unroll", o.unroll);
+    o.window = args.int_or<int>("window", o.window);
     o.wg_per_cu = args.int_or<int>("wg-per-cu", o.wg_per_cu);
     {
       const std::string pol = args.str_or("policy", "auto");

@@ -33,6 +33,15 @@ def run(cmd, timeout=300, cwd=None, env=None):
 
 
 def torchrun(nproc, script_args, timeout=600, cwd=None, env=None):
+    master = free_port()
+    boot = free_port()
+    while boot == master:
+        boot = free_port()
+    # The native TCP bootstrap (csrc/comm/bootstrap.cpp) would otherwise listen on MASTER_PORT + 17,
+    # which nobody checked was free (a busy port there failed a run on the GPU box).
+    e = {"MIREDUCE_BOOTSTRAP_PORT": str(boot)}
+    if env:
+        e.update(env)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port())] + script_args
-    return run(cmd, timeout=timeout, cwd=cwd, env=env)
+           "--master-addr", "127.0.0.1", "--master-port", str(master)] + script_args
+    return run(cmd, timeout=timeout, cwd=cwd, env=e)

@@ -4,6 +4,7 @@ one figure per dtype, single-GPU results as horizontal reference lines. gnuplot 
 in this image, so this uses matplotlib (tools/makePlots.gp is the gnuplot twin).
 
     python tools/plot.py --results results/ --out plots/ [--reference-cuda] [--single INT:SUM=7200,...]
+        [--label "8-CPU MPICH" --xlabel "MPI ranks (CPU cores)"]
 """
 import argparse
 import os
@@ -32,6 +33,8 @@ def main():
     ap.add_argument("--reference-cuda", action="store_true", help="draw the reference CUDA constants")
     ap.add_argument("--single", default="", help="DT:OP=value,... single-GPU lines to draw")
     ap.add_argument("--ylabel", default="Bandwidth (GB/sec)")
+    ap.add_argument("--label", default="MI355X", help="legend prefix of the measured series")
+    ap.add_argument("--xlabel", default="Number of ranks (GPUs)")
     a = ap.parse_args()
     import matplotlib
     matplotlib.use("Agg")
@@ -51,12 +54,12 @@ def main():
         fig, ax = plt.subplots(figsize=(6, 4.5))
         for op, pts in series.items():
             if pts:
-                ax.plot([p[0] for p in pts], [p[1] for p in pts], "-x", lw=2, color=colors[op], label=f"MI355X {op}")
+                ax.plot([p[0] for p in pts], [p[1] for p in pts], "-x", lw=2, color=colors[op], label=f"{a.label} {op}")
             if a.reference_cuda and (dt, op) in REF_CUDA:
                 ax.axhline(REF_CUDA[(dt, op)], ls="--", lw=1.5, color=colors[op], label=f"ref CUDA {op}")
             if (dt, op) in singles:
                 ax.axhline(singles[(dt, op)], ls=":", lw=2, color=colors[op], label=f"1 GPU {op}")
-        ax.set_xlabel("Number of ranks (GPUs)")
+        ax.set_xlabel(a.xlabel)
         ax.set_ylabel(a.ylabel)
         ax.set_title({"INT": "Integers", "DOUBLE": "Doubles", "LONG": "int64", "FLOAT": "fp32"}[dt])
         ax.legend(loc="lower right", fontsize=8)

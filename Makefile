@@ -4,6 +4,7 @@
 #   make            library, python extension, apps (reduction, reduce_xgmi, bandwidth_test, reduce_mpi)
 #   make python     only the python extension (cuda_mpi_reductions_amd/_C*.so)
 #   make asan       host-code ASan/UBSan build of the CPU-only apps + unit tests (GPU code untouched)
+#   make tsan       ThreadSanitizer build of the threaded host reference reducers (race_unit)
 #   make clean
 #
 # Variables: ARCH=gfx950  DEBUG=1  MPI_HOME=/opt/conda  SAVE_TEMPS=1 (keep .s for inspection)
@@ -44,7 +45,7 @@ COMMLIB     := $(BUILD)/lib/libmireduce_comm.a
 APPS := $(BUILD)/bin/reduction $(BUILD)/bin/reduce_xgmi $(BUILD)/bin/bandwidth_test
 MPI_APP := $(BUILD)/bin/reduce_mpi
 
-.PHONY: all python apps mpi clean asan unit diag examples window_ab
+.PHONY: all python apps mpi clean asan tsan unit diag examples window_ab
 all: python apps mpi unit diag examples
 
 python: $(PYEXT)
@@ -146,6 +147,15 @@ asan: csrc/apps/reduce_mpi.cpp
 	    -o $(BUILD)/asan/reduce_mpi
 	g++ $(CXXSTD) -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -Icsrc/include -I$(BUILD)/gen -DMIREDUCE_NO_HIP \
 	    tests/native/host_unit.cpp $(filter-out csrc/apps/reduce_mpi.cpp,$(MPI_SRCS)) -o $(BUILD)/asan/host_unit
+
+# Race detection: the threaded host reference reducers / arg-reductions under
+# ThreadSanitizer (tests/native/race_unit.cpp; exits non-zero on any report).
+TSAN_SRCS := csrc/runtime/cpu_reference.cpp csrc/runtime/arg_reduce_cpu.cpp csrc/runtime/types.cpp
+tsan: $(BUILD)/tsan/race_unit
+$(BUILD)/tsan/race_unit: tests/native/race_unit.cpp $(TSAN_SRCS) $(HEADERS)
+	@mkdir -p $(dir $@)
+	g++ $(CXXSTD) -O1 -g -fsanitize=thread -fno-omit-frame-pointer -Icsrc/include -I$(ROCM)/include \
+	    -D__HIP_PLATFORM_AMD__ -DMIREDUCE_NO_HIP tests/native/race_unit.cpp $(TSAN_SRCS) -o $@
 
 clean:
 	rm -rf $(BUILD) $(PYEXT)

@@ -47,6 +47,16 @@ def test_host_sanitizers():
         assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
 
 
+def test_threaded_host_references_race_free():
+    # SURVEY.md §5.2 race detection: the multi-threaded CPU oracles under ThreadSanitizer agree
+    # with their single-threaded results, and TSan reports nothing (it exits 66 on a report).
+    subprocess.run(["make", "-C", ROOT, "tsan"], check=True, stdout=subprocess.DEVNULL)
+    r = run([os.path.join(ROOT, "build", "tsan", "race_unit")], timeout=300,
+            env={"TSAN_OPTIONS": "halt_on_error=1 exitcode=66"})
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    assert "ThreadSanitizer" not in r.stderr and "ok" in r.stdout
+
+
 @pytest.mark.skipif(not os.path.exists(MPIRUN), reason="MPICH not available")
 def test_sweep_resume_and_collect(tmp_path):
     out = tmp_path / "sweep"

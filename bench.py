@@ -27,7 +27,8 @@ eager Python issue leaves ~22 us GPU gaps per step). The headline phase runs und
 non-zero instead of waiting out the process-group timeout. Only after the line is final do the
 extras run (pipelined / 2-lane / RCCL candidates, reduce.c's element-wise table, the xGMI peer-read
 probe), under their own watchdog (``--extras-deadline``): a hung extra still leaves the printed,
-verified headline. Every step's result is checked after timing against torch's own fp64 reduction
+verified headline; the teardown after the line (``--teardown-deadline``) is bounded the same way.
+Every step's result is checked after timing against torch's own fp64 reduction
 of the shards (AND over ranks), and every device-side error word (polled fan-in, fused finish) is
 read and agreed over ranks.
 
@@ -91,6 +92,9 @@ def parse_args(argv=None):
     p.add_argument("--extras-deadline", type=float, default=240.0,
                    help="seconds the reduce.c extras may take after the headline; past it rank 0 prints the "
                         "headline (extras marked as timed out) and the run ends")
+    p.add_argument("--teardown-deadline", type=float, default=120.0,
+                   help="seconds the teardown after the printed line (device sync, process-group destruction) "
+                        "may take; past it every rank exits with the headline's status")
     p.add_argument("--local-only", action="store_true",
                    help="single rank: skip the cross-rank combine (by default it is issued even at N=1)")
     p.add_argument("--streams", type=int, default=1,
@@ -848,8 +852,13 @@ def main(argv=None) -> int:
         print(json.dumps(line), flush=True)
     elif line is not None:  # the watchdog printed it
         pass
+    # The line is out: a teardown stuck in a collective (communicator destruction) must not hold
+    # the job either, so it gets a deadline of its own and exits with the headline's status.
+    teardown = _PhaseWatchdog("teardown", args.teardown_deadline, rc, lambda: None)
+    fault.at(ctx.rank, fault.spec.step, site="teardown")
     _sync(dev)
     pdist.shutdown(ctx)
+    teardown.finish()
     return rc
 
 

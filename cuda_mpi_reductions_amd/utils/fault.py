@@ -10,7 +10,9 @@ RANK defaults to 1, STEP to 0, SITE to ``step`` (also read from ``MIREDUCE_INJEC
 
 * SITE ``step``: the measured steps of the headline (bench.py counts warm-up steps first);
   ``extras``: the steps of bench.py's after-headline candidates (pipelined / RCCL measurements) —
-  a hang there must still leave a printed, verified headline (the extras watchdog).
+  a hang there must still leave a printed, verified headline (the extras watchdog);
+  ``teardown``: just before the process-group teardown that follows the printed line (STEP is
+  ignored) — a hang there must end within the teardown deadline with the headline's status.
 * KIND ``mailbox``: rank RANK fails to create its fused-finish mailbox
   (:func:`parallel.xrank.open_channel`); every rank must then agree on the RCCL fallback.
 """
@@ -25,7 +27,7 @@ from typing import Optional
 __all__ = ["FaultSpec", "FaultInjector", "parse_fault_spec"]
 
 KINDS = ("none", "exit", "hang", "corrupt", "delay", "mailbox")
-SITES = ("step", "extras")
+SITES = ("step", "extras", "teardown")
 
 
 @dataclass(frozen=True)

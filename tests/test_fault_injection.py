@@ -32,6 +32,7 @@ def test_parse_fault_spec():
     assert parse_fault_spec("hang@3:17") == FaultSpec("hang", 3, 17, 0)
     assert parse_fault_spec("delay=250@0:2") == FaultSpec("delay", 0, 2, 250)
     assert parse_fault_spec("corrupt:5") == FaultSpec("corrupt", 1, 5, 0)
+    assert parse_fault_spec("hang@1/teardown") == FaultSpec("hang", 1, 0, 0, "teardown")
     for bad in ("boom", "exit@", "exit@x", "hang:-1", "delay=", "corrupt@1:2x"):
         with pytest.raises(ValueError):
             parse_fault_spec(bad)
@@ -74,6 +75,19 @@ def test_hung_rank_hits_deadline(tmp_path):
     assert _json(r) is None
     assert "[fault] rank 1 hang" in r.stderr
     assert time.time() - t0 < 150
+
+
+def test_hang_in_teardown_keeps_the_line_and_status(tmp_path):
+    # rank 1 hangs after the line is printed (e.g. stuck destroying its communicator): the teardown
+    # deadline ends every rank with the headline's status, well before the process-group timeout.
+    t0 = time.time()
+    r = torchrun(2, [BENCH, *SCALAR, "--inject-fault", "hang@1/teardown", "--teardown-deadline", "5",
+                     "--pg-timeout", "300"], cwd=tmp_path, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json(r)
+    assert d is not None and d["verified"] is True
+    assert "[fault] rank 1 hang at teardown" in r.stderr and "teardown exceeded 5 s" in r.stderr
+    assert time.time() - t0 < 120
 
 
 # ---------------------------------------------------------------- native apps on CPU ranks (MPICH)

@@ -5,8 +5,9 @@ Driver contract: ``python bench.py --gpus N --steps K --warmup W`` (N>1 under
 ``torch.distributed.run``, one rank per GPU, RCCL over xGMI). One *step* is one complete global
 reduction of the 1e9-element float64 array (BASELINE.json config 4): every rank reduces its
 contiguous 1e9/N shard with the native single-pass HIP kernel (csrc/kernels/reduce_kernels.hpp) into a
-1-element slot, then the slots are all-reduced with RCCL. The array is synthetic (on-device
-counter-based U[0,1) fill, untimed) and fixed in size as N grows -> strong scaling.
+1-element slot, and the N partials are combined across ranks (``--collective`` below). The array is
+synthetic (on-device counter-based U[0,1) fill, untimed) and fixed in size as N grows -> strong
+scaling.
 
 Timing: W untimed warm-up steps; then barrier + synchronize, K timed steps, synchronize; the
 MAX elapsed time over ranks defines the measurement. Value = total bytes reduced per step x K /

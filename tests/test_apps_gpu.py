@@ -368,7 +368,11 @@ def test_sweep_node_preset_on_one_gpu(tmp_path):
     r = run([sys.executable, os.path.join(ROOT, "tools", "sweep.py"), "--preset", "node", "--ranks", "1",
              "--out", str(out), "--timeout", "300", "--", "--ints=1000003", "--doubles=1000003", "--retries=1"],
             timeout=1200)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    if r.returncode != 0:  # name the failing point's own stderr, not only the sweep's summary
+        errs = sorted(out.glob("*/stdout-*.rc"))
+        bad = [p for p in errs if p.read_text().strip() != "0"]
+        detail = "".join(f"\n--- {p.name}\n" + p.with_suffix(".err").read_text()[-3000:] for p in bad)
+        raise AssertionError(r.stdout[-2000:] + r.stderr[-2000:] + detail)
     for name in ("vector-reduce", "vector-allreduce", "vector-direct-reduce", "vector-direct", "scalar-allreduce",
                  "scalar-fused", "bench"):
         assert (out / name / f"stdout-{name}-P1.rc").read_text().strip() == "0", name

@@ -90,6 +90,36 @@ def test_sweep_node_preset_matrix():
     assert names[-1] == "bench"
 
 
+def test_sweep_retries_a_taken_rendezvous_port(tmp_path, monkeypatch):
+    # A launcher that loses its port to another process between free_port() and its bind fails with
+    # EADDRINUSE: the point is relaunched once on a new port; any other failure is recorded as is.
+    import importlib.util
+    import sys
+    spec = importlib.util.spec_from_file_location("sweep_retry", os.path.join(ROOT, "tools", "sweep.py"))
+    sw = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sw)
+    marker = tmp_path / "launched_once"
+    script = ("import os, sys\n"
+              f"m = {str(marker)!r}\n"
+              "if not os.path.exists(m):\n"
+              "    open(m, 'w').close()\n"
+              "    sys.stderr.write('RuntimeError: EADDRINUSE: address already in use\\n'); sys.exit(1)\n"
+              "print('INT SUM 2   1.000')\n")
+    calls = []
+
+    def fake_command(app, p, extra):
+        calls.append(p)
+        return [sys.executable, "-c", script]
+    monkeypatch.setattr(sw, "command", fake_command)
+    assert sw.run_points("reduce_xgmi", "x", [2], [], str(tmp_path), 60, False) == 0
+    assert calls == [2, 2] and (tmp_path / "stdout-x-P2.rc").read_text().strip() == "0"
+    assert "INT SUM 2" in (tmp_path / "stdout-x-P2.txt").read_text()
+    monkeypatch.setattr(sw, "command", lambda app, p, extra: [sys.executable, "-c", "import sys; sys.exit(5)"])
+    assert sw.run_points("reduce_xgmi", "y", [2], [], str(tmp_path), 60, False) == 1
+    assert (tmp_path / "stdout-y-P2.rc").read_text().strip() == "5"
+    assert not sw._port_taken("some other failure") and sw._port_taken(b"bind: Address already in use")
+
+
 def test_plot_tool(tmp_path):
     res = tmp_path / "results"
     res.mkdir()

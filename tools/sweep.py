@@ -44,6 +44,11 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def _port_taken(stderr) -> bool:
+    text = (stderr if isinstance(stderr, str) else (stderr or b"").decode(errors="replace")).lower()
+    return "eaddrinuse" in text or "address already in use" in text
+
+
 def command(app: str, p: int, extra: list[str]) -> list[str]:
     if app == "reduce_mpi":
         return [MPIRUN, "-np", str(p), os.path.join(ROOT, "build", "bin", "reduce_mpi")] + extra
@@ -86,13 +91,21 @@ def run_points(app: str, name: str, ranks: list, extra: list[str], out: str, tim
             cmd = [os.path.join(ROOT, "build", "bin", app)] + extra
         else:
             cmd = command(app, p, extra)
-        print(f"[sweep] {name} P={p}: {' '.join(cmd)}", flush=True)
         t0 = time.time()
-        try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=out)
-            rc, stdout, err = r.returncode, r.stdout, r.stderr
-        except subprocess.TimeoutExpired as e:
-            rc, stdout, err = 124, e.stdout or "", (e.stderr or "") + "\n[sweep] timeout"
+        for attempt in range(2):
+            print(f"[sweep] {name} P={p}: {' '.join(cmd)}", flush=True)
+            try:
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=out)
+                rc, stdout, err = r.returncode, r.stdout, r.stderr
+            except subprocess.TimeoutExpired as e:
+                rc, stdout, err = 124, e.stdout or "", (e.stderr or "") + "\n[sweep] timeout"
+            # free_port() closes the port before the launcher binds it: another process can take it
+            # in between. That is a launch failure, not a result: one retry on a new port.
+            if attempt == 0 and rc != 0 and p is not None and app != "reduce_mpi" and _port_taken(err):
+                print(f"[sweep] {name} P={p}: rendezvous port taken, retrying on a new port", flush=True)
+                cmd = command(app, p, extra)
+                continue
+            break
         with open(base + ".txt", "w") as f:
             f.write(stdout if isinstance(stdout, str) else stdout.decode())
         with open(base + ".err", "w") as f:

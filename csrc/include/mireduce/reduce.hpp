@@ -108,8 +108,10 @@ class Workspace {
 constexpr int kTicketStride = 32;  // one counter per 128-byte line
 constexpr int kMaxGroups = 64;
 
+// The tuned plan depends on the element type, the size and (for 4- and 2-byte types) the operator:
+// see tuned_defaults in reduce.hip.
 LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cfg, int num_cus,
-                       int max_grid);
+                       int max_grid, Op op = Op::Sum);
 
 // Enqueue a full reduction of n elements at device pointer `in` into out[0] (device pointer,
 // element type `acc`). Asynchronous on `stream`; safe to capture into a hipGraph.

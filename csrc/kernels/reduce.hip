@@ -92,7 +92,7 @@ const Table& table() {
 struct Defaults {
   int block, unroll, wg_per_cu, policy, pipeline, window;
 };
-Defaults tuned_defaults(size_t bytes, DType t) {
+Defaults tuned_defaults(size_t bytes, DType t, Op op) {
   constexpr size_t MB = 1ull << 20;
   // >= 3 GB, 8-byte types: one 256-thread workgroup per CU, 8 vectors in flight per lane. Round 1
   // picked 512 x 16 x 1 (f64 7.29 vs 7.23 for 256 x 8 x 1, profiles/r1_tuning/); on round 2's boxes
@@ -100,17 +100,25 @@ Defaults tuned_defaults(size_t bytes, DType t) {
   // for f64 SUM and int64 MAX (8 GB: 7.21 / 7.22 vs 7.07 / 7.17, profiles/r2_plan/, r2_tune/).
   // (Its compiled body issues 4 loads then interleaves waits and adds, ~9 in flight at 86 VGPRs;
   // forcing all 16 up front with a sched_barrier was slower still: 6.95 TB/s, r2_plan/run2.sh.)
-  // 4-byte types: one 512-thread WG per CU, 4 vectors per lane (tools/tune_types.sh,
-  // profiles/r1_session3/tune_types.txt: f32 7.17, i32 7.19 vs 7.14).
+  // (Rounds 1-2 ran 4-byte types >= 3 GB as 512 x 4 x 1 and other types above 192 MB as 256 x 2 x 3 /
+  // 256 x 4 x 2 for 16-bit, all with hipcc's schedule: profiles/r1_session3/tune_types.txt.)
   // Round 3 (profiles/r3_window/, production kernel, same box, 7 interleaved rounds): 8-byte types
   // above 192 MB stream fastest as 256 threads x 8 vectors x 1 WG per CU with an explicit load
   // window of 4 (~18 loads in flight per CU): 8 GB 1092.1 vs 1112.4 us for hipcc's schedule of
   // the same plan, 1 GB 141.0 vs 144.5 us for 256x2x3. (hipcc's own schedule of a plan moves with
   // unrelated kernel code, profiles/r3_regress/; the explicit window does not.)
+  // 4- and 2-byte types (profiles/r3_types/, tools/tune.py, 5 interleaved rounds per sweep, 1 / 2 /
+  // 8 GB): the window-4 plan is first for f32 SUM at all three sizes (8 GB 7.26 vs 7.23 TB/s for the
+  // old 512x4x1; 1 GB 7.14 vs 7.09 for 256x2x3), for int32 MAX and bf16 SUM (8 GB 7.38 vs 7.21 for
+  // 256x4x2) and within 0.2 % of first for f32 MAX. Two exceptions: int32 SUM/SUMSQ, whose int64
+  // accumulation doubles the VALU work per load, collapses with it (6.06-6.22 TB/s) and streams
+  // best as 256x8x2 with a window of 2 (7.15-7.27, first at every size); 16-bit MIN/MAX run the
+  // window-4 plan at 7.13 and 256x8x2 window 2 at 7.25 (8 GB f16 MAX; the old 256x4x2: 7.16).
+  const bool widening_int = t == DType::Int32 && (op == Op::Sum || op == Op::SumSq);
+  const bool half_cmp = dtype_is_half(t) && op != Op::Sum && op != Op::SumSq;
   if (dtype_size(t) == 8 && bytes > 192 * MB) return {256, 8, 1, 1, 0, 4};
-  if (dtype_size(t) == 4 && bytes >= 3072 * MB) return {512, 4, 1, 1, 0, 0};
-  if (dtype_is_half(t) && bytes > 192 * MB) return {256, 4, 2, 1, 0, 0};
-  if (bytes > 192 * MB) return {256, 2, 3, 1, 0, 0};
+  if ((widening_int || half_cmp) && bytes > 192 * MB) return {256, 8, 2, 1, 0, 2};
+  if (dtype_size(t) <= 4 && bytes > 192 * MB) return {256, 8, 1, 1, 0, 4};
   return {256, 4, 3, 1, 0, 0};
 }
 constexpr int kDefaultGroups = 8;
@@ -240,10 +248,10 @@ void Workspace::reset(hipStream_t stream) {
 }
 
 LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cfg, int num_cus,
-                       int max_grid) {
+                       int max_grid, Op op) {
   LaunchPlan p;
   const size_t es = dtype_size(t);
-  const Defaults d = tuned_defaults(n * es, t);
+  const Defaults d = tuned_defaults(n * es, t, op);
   p.block = cfg.block ? cfg.block : d.block;
   p.unroll = cfg.unroll ? cfg.unroll : d.unroll;
   p.nontemporal = cfg.policy < 0 ? d.policy == 1 : cfg.policy == 1;
@@ -314,7 +322,7 @@ LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out
   const int c = combo_index(op, t, acc);
   MIREDUCE_REQUIRE(c >= 0, "unsupported (dtype, op, accumulator) combination");
   MIREDUCE_REQUIRE(out != nullptr, "output pointer is null");
-  LaunchPlan p = plan_reduce(in, n, t, cfg, ws.num_cus(), ws.max_grid());
+  LaunchPlan p = plan_reduce(in, n, t, cfg, ws.num_cus(), ws.max_grid(), op);
   kern::Args a = make_args(in, p, t, cfg);
   a.partials = ws.partials();
   a.group_partials = ws.group_partials();
@@ -347,7 +355,7 @@ BoundReduce::BoundReduce(const void* in, size_t n, DType t, Op op, DType acc, vo
   const int c = combo_index(op, t, acc);
   MIREDUCE_REQUIRE(c >= 0, "unsupported (dtype, op, accumulator) combination");
   MIREDUCE_REQUIRE(out != nullptr, "output pointer is null");
-  const LaunchPlan p = plan_reduce(in, n, t, cfg, ws.num_cus(), ws.max_grid());
+  const LaunchPlan p = plan_reduce(in, n, t, cfg, ws.num_cus(), ws.max_grid(), op);
   kern::Args a = make_args(in, p, t, cfg);
   a.partials = ws.partials();
   a.group_partials = ws.group_partials();
@@ -383,7 +391,7 @@ LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, 
   ReduceConfig c2 = cfg;
   c2.single_pass = false;
   c2.xrank = nullptr;
-  LaunchPlan p = plan_reduce(in, n, t, c2, num_cus, max_grid);
+  LaunchPlan p = plan_reduce(in, n, t, c2, num_cus, max_grid, op);
   kern::Args a = make_args(in, p, t, c2);
   a.partials = partials;
   a.groups = 0;

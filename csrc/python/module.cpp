@@ -283,16 +283,19 @@ PYBIND11_MODULE(_C, m) {
   m.def(
       "plan",
       [](uintptr_t in, uint64_t n, int dtype, int num_cus, int max_grid, int block, int unroll,
-         int wg_per_cu, int max_blocks, int groups, int policy, bool single_pass, int pipeline, int window) {
+         int wg_per_cu, int max_blocks, int groups, int policy, bool single_pass, int pipeline, int window,
+         int op) {
+        MIREDUCE_REQUIRE(op >= 0 && op < kNumOps, "op out of range");
         return plan_dict(plan_reduce(as_ptr<const void>(in), n, static_cast<DType>(dtype),
                                      make_cfg(block, unroll, wg_per_cu, max_blocks, groups,
                                               policy, single_pass, pipeline, window),
-                                     num_cus, max_grid));
+                                     num_cus, max_grid, static_cast<Op>(op)));
       },
       py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("num_cus") = 256,
       py::arg("max_grid") = 16384, py::arg("block") = 0, py::arg("unroll") = 0,
       py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0, py::arg("groups") = 0,
-      py::arg("policy") = -1, py::arg("single_pass") = true, py::arg("pipeline") = -1, py::arg("window") = -1);
+      py::arg("policy") = -1, py::arg("single_pass") = true, py::arg("pipeline") = -1, py::arg("window") = -1,
+      py::arg("op") = 0);
 
   m.def(
       "reduce_partials",

@@ -75,10 +75,14 @@ def test_host_reducer(dt, pattern):
 def test_half_plan_uses_tuned_point():
     from cuda_mpi_reductions_amd._native import native
     C = native()
-    for code in (4, 5):  # bf16, f16: 8 GB and 1 GB -> 256 x 4, 2 WG/CU, nt
+    for code in (4, 5):  # bf16, f16 at 8 GB and 1 GB (profiles/r3_types/)
         for n in (4_000_000_000, 500_000_000):
-            p = C.plan(0, n, code)
-            assert (p["block"], p["unroll"], p["grid"], p["nontemporal"]) == (256, 4, 512, True), (code, n, p)
+            p = C.plan(0, n, code)  # SUM: 256 x 8, 1 WG/CU, window 4
+            assert (p["block"], p["unroll"], p["grid"], p["nontemporal"], p["window"]) == (256, 8, 256, True, 4), \
+                (code, n, p)
+            p = C.plan(0, n, code, op=2)  # MAX: 256 x 8, 2 WG/CU, window 2
+            assert (p["block"], p["unroll"], p["grid"], p["nontemporal"], p["window"]) == (256, 8, 512, True, 2), \
+                (code, n, p)
 
 
 def test_reduction_app_rejects_ladder_for_half():

@@ -389,3 +389,25 @@ def test_default_plan_above_192mb_uses_the_window(dt, op):
     p = r.last_plan
     assert (p["block"], p["unroll"], p["window"]) == (256, 8, 4), p
     check(got, x, op, dt if op != "sum" or dt.is_floating_point else torch.int64, n)
+
+
+@pytest.mark.parametrize("dt,op,want", [
+    (torch.float32, "sum", (256, 8, 1, 4)), (torch.float32, "max", (256, 8, 1, 4)),
+    (torch.int32, "max", (256, 8, 1, 4)), (torch.int32, "sum", (256, 8, 2, 2)),
+    (torch.bfloat16, "sum", (256, 8, 1, 4)), (torch.float16, "min", (256, 8, 2, 2))])
+def test_default_plan_above_192mb_narrow_types(dt, op, want):
+    # the round-3 defaults for 4- and 2-byte arrays > 192 MB (profiles/r3_types/): (block, unroll,
+    # workgroups per CU, window), misaligned by one element (head scalar + tail), 256 MB of data
+    n = (256 << 20) // torch.empty((), dtype=dt).element_size() + 3
+    base = torch.empty(n + 1, dtype=dt, device=DEV)
+    fill_(base, "fullrange" if not dt.is_floating_point else "uniform", seed=78)
+    x = base[1:]
+    r = Reducer(DEV)
+    got = r(x, op).item()
+    p = r.last_plan
+    cus = torch.cuda.get_device_properties(DEV).multi_processor_count
+    assert (p["block"], p["unroll"], p["grid"], p["window"]) == (want[0], want[1], cus * want[2], want[3]), p
+    half = dt in (torch.bfloat16, torch.float16)
+    wide = {torch.int32: torch.int64, torch.float32: torch.float64}
+    acc = torch.float32 if half else (wide[dt] if op == "sum" else dt)
+    check(got, x, op, acc, n)

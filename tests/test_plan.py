@@ -51,12 +51,27 @@ def test_tuned_defaults_by_size():
     assert (small["block"], small["unroll"], small["window"]) == (256, 4, 0)
     # no size band picks the default (non-nt) policy: it collapses to 2.7 TB/s on a cold cache
     assert all(C.plan(0, n, F64)["nontemporal"] for n in (1, 1 << 20, 3 << 23, 1 << 25, 3 << 24, 1 << 27))
-    f32 = C.plan(0, 2 * 10**9, 2)          # 8 GB of fp32: one 512-thread WG per CU, 4 vectors per lane
-    assert (f32["block"], f32["unroll"], f32["grid"]) == (512, 4, 256)
     i64 = C.plan(0, 10**9, 1)              # 8 GB of int64: like fp64
     assert (i64["block"], i64["unroll"], i64["grid"], i64["window"]) == (256, 8, 256, 4)
-    f32_1g = C.plan(0, 250_000_000, 2)     # 1 GB keeps the 256x2x3 plan
-    assert (f32_1g["block"], f32_1g["unroll"], f32_1g["window"]) == (256, 2, 0)
+
+
+# op codes: SUM 0, MIN 1, MAX 2, SUMSQ 3, AMAX 4; dtypes: int32 0, int64 1, f32 2, f64 3, bf16 4, f16 5
+@pytest.mark.parametrize("dtype,n,op,want", [
+    (2, 2 * 10**9, 0, (256, 8, 256, 4)),   # f32 SUM 8 GB: window 4 (profiles/r3_types/)
+    (2, 250_000_000, 0, (256, 8, 256, 4)),  # f32 SUM 1 GB
+    (2, 2 * 10**9, 2, (256, 8, 256, 4)),   # f32 MAX 8 GB
+    (0, 2 * 10**9, 2, (256, 8, 256, 4)),   # int32 MAX 8 GB
+    (0, 2 * 10**9, 0, (256, 8, 512, 2)),   # int32 SUM (int64 accumulation): 256x8x2, window 2
+    (0, 250_000_000, 0, (256, 8, 512, 2)),  # int32 SUM 1 GB
+    (4, 4 * 10**9, 0, (256, 8, 256, 4)),   # bf16 SUM 8 GB
+    (4, 5 * 10**8, 0, (256, 8, 256, 4)),   # bf16 SUM 1 GB
+    (5, 4 * 10**9, 2, (256, 8, 512, 2)),   # f16 MAX 8 GB: 256x8x2, window 2
+    (3, 10**9, 1, (256, 8, 256, 4)),       # f64 MIN: the operator does not move 8-byte plans
+    (2, 1 << 24, 0, (256, 4, 768, 0)),     # <= 192 MB: unchanged (256x4x3, hipcc's schedule)
+])
+def test_tuned_defaults_by_dtype_and_op(dtype, n, op, want):
+    p = native().plan(0, n, dtype, op=op)
+    assert (p["block"], p["unroll"], p["grid"], p["window"]) == want and p["nontemporal"]
 
 
 def test_window_only_where_instantiated():

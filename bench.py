@@ -316,22 +316,28 @@ def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES, out: "dict | None" = No
                         wl.cfg = replace(_C[base], op=op)
                         el = _one_collective(wl, ctx)
                         gib = wl.bytes_total / el / float(1 << 30)
+                        dev_err = None
                         if x == 0:  # full check against the gathered inputs, and the reference checksum
-                            ok = wl.verify()["ok"]
+                            v = wl.verify()
+                            ok, dev_err = v["ok"], v.get("device_error")
                             first[(dt, op)] = _checksum(wl, holder)
                         else:
                             same = _checksum(wl, holder) == first[(dt, op)]
                             ok = -pdist.max_over_ranks(-float(same), ctx) > 0.5  # AND over ranks
                         table.append({"retry": x, "dtype": dt, "op": op.upper(), "impl": impl,
                                       "gibps": round(gib, 3), "ms": round(el * 1e3, 4), "verified": ok})
+                        if dev_err:
+                            table[-1]["device_error"] = dev_err
                         lines.append("%s %s %d %10.3lf" % (dt, op.upper(), ctx.world_size, gib))
             for kind, coll in (("reduce", "reduce"), ("allreduce", "allreduce")):  # DOUBLE SUM summaries
                 wl = wls["DOUBLE"]
                 wl.cfg = replace(_C["xgmi_2g_double_sum_reduce"], op="sum", collective=coll)
                 els = [_one_collective(wl, ctx) for _ in range(retries)]
-                ok = wl.verify()["ok"]
+                v = wl.verify()
                 out[f"{kind}_{impl}"] = {"gibps": round(wl.bytes_total * retries / sum(els) / float(1 << 30), 3),
-                                         "ms": round(sum(els) / retries * 1e3, 4), "verified": ok}
+                                         "ms": round(sum(els) / retries * 1e3, 4), "verified": v["ok"]}
+                if v.get("device_error"):
+                    out[f"{kind}_{impl}"]["device_error"] = v["device_error"]
         except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
             import traceback
             err = {"error": f"{type(e).__name__}: {e}"[:200]}
@@ -512,12 +518,40 @@ def _try_fused(wl, ctx) -> "str | None":
     _sync(ctx.device)
     err = wl.check()
     if err is None:
-        ok, ref = _verify_slots(wl, slots, ctx)
+        ok, ref = _selfcheck_slots(wl, slots, ctx)
         if not ok:
             err = f"self-check mismatch: {ref}"
     if err is not None:
         wl.use_collective("rccl", streams=1)
     return err
+
+
+def _selfcheck_slots(wl, slots: torch.Tensor, ctx) -> tuple:
+    """The fused finish's self-check value: this rank's partial from the SAME kernel launched
+    without a channel, combined over the process group (what the fused exchange replaces). It
+    tests the exchange, not the kernel, and needs no torch pass over the array before the timed
+    steps: the full torch reference still checks every timed slot afterwards (``_verify_slots``).
+    Every slot must match on every rank (AND over ranks)."""
+    loc = wl.new_slots(1)
+    wl.local(loc)
+    _sync(ctx.device)
+    floating = loc.dtype.is_floating_point
+    host = loc.to(torch.float64 if floating else torch.int64).cpu()
+    mag = host.abs().to(torch.float64)
+    if ctx.world_size > 1:
+        dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
+        t, m = host.to(dev), mag.to(dev)
+        torch.distributed.all_reduce(t, op=pdist.reduce_op(wl.cfg.op))
+        torch.distributed.all_reduce(m)
+        host, mag = t.cpu(), m.cpu()
+    expect = host.item()
+    tol = 0.0
+    if floating and wl.cfg.op in ("sum", "sumsq"):  # the partials fold in another order: a few ulps
+        tol = 8.0 * ctx.world_size * torch.finfo(loc.dtype).eps * mag.item()
+    got = slots.to(torch.float64 if floating else torch.int64).cpu()
+    ok = bool(((got - expect).abs() <= tol).all().item()) if floating else bool((got == expect).all().item())
+    ok = -pdist.max_over_ranks(-float(ok), ctx) > 0.5
+    return ok, {"got": got.tolist(), "expected": expect, "tolerance": tol}
 
 
 def _verify_slots(wl, written: torch.Tensor, ctx) -> tuple:

@@ -530,10 +530,14 @@ class VectorReduction:
                 gathered[0].copy_(xs)
             if holder and ok:
                 ok = self._check_chunk(torch.stack(gathered), ys, world)
-        if self.comm is not None and self.comm.check() is not None:
+        dev_err = self.comm.check() if self.comm is not None else None  # collective
+        if dev_err is not None:
             ok = False
         t = torch.tensor([1 if ok else 0], dtype=torch.int32,
                          device=self.ctx.device if self.ctx.backend == "nccl" else "cpu")
         if world > 1:
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
-        return {"ok": bool(t.item())}
+        out = {"ok": bool(t.item())}
+        if dev_err is not None:
+            out["device_error"] = dev_err
+        return out

@@ -268,8 +268,9 @@ def test_bench_eight_ranks_auto_on_one_gpu(tmp_path, monkeypatch):
     assert d["verified"] is True and d["n_gpus"] == 8
     assert d["config"]["collective"] == "fused" and d["value"] == d["serial_gbps"] and "reduce_c_vector" in d
     ex = d["reduce_c_vector"]
-    assert ex["reduce_direct"].get("verified") is True, ex
-    assert len(ex["table"]) == 30 and all(t.get("verified") is True for t in ex["table"]), ex["table"]
+    bad = [t for t in ex["table"] if t.get("verified") is not True]
+    assert not bad and len(ex["table"]) == 30, (bad, r.stderr[-2000:])
+    assert ex["reduce_direct"].get("verified") is True, (ex["reduce_direct"], ex.get("allreduce_direct"))
     assert len(ex["rows"]["direct"]) == 31 and ex["rows"]["direct"][1].startswith("INT MAX 8 ")
     pr = ex["peer_read"]  # fabric probe: 8 ranks reading each other's buffers (here all on one GPU)
     assert "error" not in pr and 0 < pr["ingress_gbps_min"] <= pr["ingress_gbps_max"] and pr["node_gbps"] > 0, pr

@@ -87,3 +87,66 @@ def test_extras_watchdog_reports_the_extras_completed_so_far():
     v = d["reduce_c_vector"]
     assert v["rows"]["direct"][1] == "INT MAX 8   1.000" and "did not finish" in v["error"]
     assert "did not finish" in d["extras_error"] and d["value"] == 1.0
+
+
+class _StubWorkload:
+    """Just what bench._selfcheck_slots reads: the op, slot allocation and the channel-free launch."""
+
+    def __init__(self, op, value, dtype):
+        import torch
+        from types import SimpleNamespace
+        self.cfg = SimpleNamespace(op=op)
+        self._value, self._dtype = value, dtype
+        self._torch = torch
+
+    def new_slots(self, k):
+        return self._torch.empty(k, dtype=self._dtype)
+
+    def local(self, out):
+        out.fill_(self._value)
+        return out
+
+
+def test_fused_selfcheck_compares_with_the_local_partials():
+    # The fused finish's self-check (no torch pass over the array before the timed steps,
+    # profiles/r3_selfcheck/): every slot must equal the channel-free launch's value, combined over
+    # the group — exactly for MIN/MAX and integers, within a few ulps of the accumulator for SUM.
+    import torch
+    from types import SimpleNamespace
+    b = _bench()
+    ctx = SimpleNamespace(world_size=1, backend="gloo", device=torch.device("cpu"))
+    wl = _StubWorkload("sum", 1000.0, torch.float32)
+    eps = torch.finfo(torch.float32).eps
+    ok, ref = b._selfcheck_slots(wl, torch.tensor([1000.0, 1000.0 + 2 * eps * 1000, 1000.0]), ctx)
+    assert ok and ref["expected"] == 1000.0 and ref["tolerance"] > 0
+    ok, _ = b._selfcheck_slots(wl, torch.tensor([1000.0, 1000.1, 1000.0]), ctx)
+    assert not ok
+    wl = _StubWorkload("max", 7.5, torch.float64)
+    assert b._selfcheck_slots(wl, torch.tensor([7.5, 7.5, 7.5], dtype=torch.float64), ctx)[0]
+    assert not b._selfcheck_slots(wl, torch.tensor([7.5, 7.5, 7.5 + 1e-12], dtype=torch.float64), ctx)[0]
+    wl = _StubWorkload("sum", 123456789012, torch.int64)
+    assert b._selfcheck_slots(wl, torch.tensor([123456789012] * 3), ctx)[0]
+    assert not b._selfcheck_slots(wl, torch.tensor([123456789012, 123456789013, 123456789012]), ctx)[0]
+
+
+def test_fused_selfcheck_two_ranks_gloo(tmp_path):
+    # world 2 (gloo, CPU): the partials are combined over the group and the verdict is agreed; a
+    # slot that matches only this rank's own partial (a broken exchange) fails on every rank.
+    from helpers import torchrun
+    script = tmp_path / "sc.py"
+    script.write_text(
+        "import importlib.util, os, sys, torch\n"
+        f"sys.path.insert(0, {ROOT!r}); sys.path.insert(0, {os.path.join(ROOT, 'tests')!r})\n"
+        "from test_bench_policy import _StubWorkload, _bench\n"
+        "from cuda_mpi_reductions_amd.parallel import dist as pdist\n"
+        "b = _bench()\n"
+        "ctx = pdist.init(backend='gloo', device_type='cpu')\n"
+        "wl = _StubWorkload('sum', float(ctx.rank + 1), torch.float64)\n"
+        "good = b._selfcheck_slots(wl, torch.tensor([3.0, 3.0], dtype=torch.float64), ctx)[0]\n"
+        "own = float(ctx.rank + 1) if ctx.rank == 1 else 3.0\n"
+        "bad = b._selfcheck_slots(wl, torch.tensor([own, own], dtype=torch.float64), ctx)[0]\n"
+        "print(f'rank {ctx.rank} good={good} bad={bad}', flush=True)\n"
+        "pdist.shutdown(ctx)\n")
+    r = torchrun(2, [str(script)], timeout=300, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "rank 0 good=True bad=False" in r.stdout and "rank 1 good=True bad=False" in r.stdout, r.stdout

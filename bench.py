@@ -633,7 +633,7 @@ def _gbps(wl, K: int, elapsed: float) -> float:
     return wl.bytes_total * K / elapsed / 1e9
 
 
-def _candidates(wl, ctx, args, fault, fused_ok: bool, capture_failed: bool = False) -> dict:
+def _candidates(wl, ctx, args, fault, fused_ok: bool, capture_failed: bool = False, which: str = "all") -> dict:
     """After-headline measurements of the other step protocols (extras; never the headline):
 
     * ``fused_2lane_pipelined``: the fused finish over two stream lanes, consecutive independent
@@ -642,17 +642,20 @@ def _candidates(wl, ctx, args, fault, fused_ok: bool, capture_failed: bool = Fal
       completion / the all-reduce of step i overlapping the local reduce of step i+1 (N > 1 only:
       at world 1 the all-reduce enqueues no kernel).
 
-    Each is verified and its error words read; a failure is recorded, never raised. Fault site
+    ``which``: ``fused`` / ``rccl`` / ``all`` of them. Each one's error words are read right after
+    it; the slots of all of them are verified after the last measurement (a torch reference pass
+    slows the run that follows it, ``profiles/r3_selfcheck/``). A failure is recorded, never raised. Fault site
     ``extras`` injects into these steps. ``capture_failed``: the headline's graph capture of
     collective-issuing steps failed (e.g. gloo collectives on GPU tensors), so RCCL candidates are
     issued eagerly rather than captured again (a second failed capture can abort the process)."""
     K, W = args.steps, min(args.warmup, 2)
     todo = []
-    if fused_ok:
+    if fused_ok and which in ("all", "fused"):
         todo.append(("fused_2lane_pipelined", "fused", 2, False))
-    if ctx.world_size > 1:
+    if ctx.world_size > 1 and which in ("all", "rccl"):
         todo += [("rccl_serial", "rccl", 1, True), ("rccl_pipelined", "rccl", 1, False)]
     out = {}
+    pending = []  # verified after ALL candidates are measured: a torch pass slows the run after it
     for name, coll, lanes, serial in todo:
         try:
             wl.use_collective(coll, streams=lanes)
@@ -660,15 +663,20 @@ def _candidates(wl, ctx, args, fault, fused_ok: bool, capture_failed: bool = Fal
             m = _measure(wl, slots, ctx, args, fault, serial=serial, warmup=W, site="extras",
                          allow_graph=not (capture_failed and coll == "rccl"))
             err = wl.check()
-            ok = _verify_slots(wl, slots[:m["written"]], ctx)[0] and err is None
             out[name] = {"gbps": round(_gbps(wl, K, m["elapsed"]), 3),
-                         "ms_per_step": round(m["elapsed"] / K * 1e3, 5), "launch": m["launch"], "verified": ok}
+                         "ms_per_step": round(m["elapsed"] / K * 1e3, 5), "launch": m["launch"], "verified": None}
             if err:
                 out[name]["error"] = err
+            pending.append((name, slots[:m["written"]]))
         except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
             out[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
             print(f"[bench] rank {ctx.rank}: candidate {name} failed: {e}", file=sys.stderr)
-    if ctx.world_size == 1:
+    for name, written in pending:
+        try:
+            out[name]["verified"] = _verify_slots(wl, written, ctx)[0] and "error" not in out[name]
+        except Exception as e:  # noqa: BLE001
+            out[name].update(verified=False, error=f"verification: {type(e).__name__}: {e}"[:300])
+    if ctx.world_size == 1 and which in ("all", "rccl"):
         out["rccl_serial"] = out["rccl_pipelined"] = {"gbps": None, "note": "world 1: a 1-rank RCCL all-reduce "
                                                       "enqueues no kernel, so there is no combine to measure"}
     return out
@@ -862,18 +870,23 @@ def main(argv=None) -> int:
         return 2  # (unreachable: the watchdog ended the process)
 
     # ------------------------------------------------------------------ extras (watchdog; never the headline)
-    # Order: reduce.c's table (direct collective first: no RCCL), then the step candidates (the
-    # RCCL ones last), so a hang costs the fewest extras; the watchdog prints what has completed.
+    # Order: the fused 2-lane candidate (kernels only), reduce.c's table (direct collective first: no
+    # RCCL), then the RCCL step candidates, so a hang costs the fewest extras; the watchdog prints
+    # what has completed.
     extras = {}
     guard = _ExtrasWatchdog(line, args.extras_deadline, rc, partial=extras)
+    run_cands = args.candidates and dev.type == "cuda" and hasattr(wl, "use_collective") and not args.pipelined
+    cap_failed = m["launch"].startswith("eager (graph capture failed")
+    if run_cands:  # the fused (kernel-only) candidate first: before the torch-heavy extras below
+        extras["candidates"] = _candidates(wl, ctx, args, fault, collective == "fused", cap_failed, which="fused")
     if args.vector_extras and dev.type == "cuda" and cfg.name == NORTH_STAR:
         extras["reduce_c_vector"] = {}
         _vector_extras(ctx, out=extras["reduce_c_vector"])
     if args.compare_torch and dev.type == "cuda":
         extras["torch_gbps"] = round(_time_torch_reduction(wl, K, W, ctx), 3)
-    if args.candidates and dev.type == "cuda" and hasattr(wl, "use_collective") and not args.pipelined:
-        extras["candidates"] = _candidates(wl, ctx, args, fault, collective == "fused",
-                                           capture_failed=m["launch"].startswith("eager (graph capture failed"))
+    if run_cands:  # the RCCL candidates last: a hang there costs the fewest extras
+        extras["candidates"].update(_candidates(wl, ctx, args, fault, collective == "fused", cap_failed,
+                                                which="rccl"))
     if guard.finish() and line is not None:
         cands = extras.get("candidates")
         if cands is not None:

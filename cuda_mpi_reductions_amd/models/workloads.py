@@ -341,10 +341,13 @@ class ScalarReduction:
         return "; ".join(msgs) or None
 
     # ------------------------------------------------------------------ verify
-    def reference(self, chunk: int = 1 << 28):
+    def reference(self, chunk: int = 1 << 24):
         """Independent global result: torch's own reduction of each shard (in chunks, so HBM-filling
         arrays need no full-size temporaries), combined across ranks in fp64 / int64 (parity: the
-        CPU check of reduction.cpp:748-780)."""
+        CPU check of reduction.cpp:748-780). The chunks stay small (16M elements: <= 128 MB fp64
+        temporaries): releasing GB-sized temporaries to the driver (``empty_cache``, which every
+        graph capture calls) slowed the streaming kernel after it by ~6 % (tools/settle_probe.py,
+        profiles/r3_selfcheck/)."""
         x = self.x
         dev = x.device
         if self.cfg.op == "sum":

@@ -8,6 +8,7 @@ cost the bf16 bench 6 % for the whole timed run. This probe times the same bound
     A  nothing (baseline)              D  torch pass, then 100 untimed launches
     B  torch pass                      E  torch pass, then torch.cuda.empty_cache()
     C  torch pass, then 0.5 s idle     F  torch's own bf16 sum (no fp64 temporaries)
+    G  E, then 0.5 s idle              H  torch pass in 16M-element chunks, then empty_cache()
 
     python tools/settle_probe.py [--n 4e9] [--dtype bfloat16] [--steps 30] [--json out.json]
 """
@@ -80,16 +81,16 @@ def main() -> int:
     timed()  # warm-up
     torch.cuda.synchronize()
     res = {}
-    for name in "ABCDEF":
+    for name in "ABCDEFGH":
         if name != "A":
             if name == "F":
                 x.sum().item()
             else:
-                torch_pass(x)
-        if name == "C":
-            time.sleep(0.5)
-        if name == "E":
+                torch_pass(x, chunk=1 << 24 if name == "H" else 1 << 28)
+        if name in ("E", "G", "H"):
             torch.cuda.empty_cache()
+        if name in ("C", "G"):
+            time.sleep(0.5)
         us = timed(100 if name == "D" else 0)
         med = statistics.median(us)
         res[name] = {"median_us": round(med, 1), "TBps": round(nbytes / med / 1e6, 3),

@@ -685,8 +685,8 @@ def _candidates(wl, ctx, args, fault, fused_ok: bool, capture_failed: bool = Fal
 def _tune_plan(wl, ctx, args, fault, kernel, cands) -> "tuple[KernelConfig, dict]":
     """Streaming-kernel plan for this shard: the tuned default against the runners-up
     (profiles/r2_plan/), each measured with the headline protocol (one lane, fused finish, serial,
-    graph replay, MAX over ranks) in two rounds, best of each (the first candidate of round 1 pays
-    for the GPU ramping its clocks). A candidate whose fused exchange or fan-in flagged an error is
+    graph replay, MAX over ranks) in two rounds, best of each (a first candidate measured while the
+    driver works on memory released just before it runs slow: profiles/r3_selfcheck/). A candidate whose fused exchange or fan-in flagged an error is
     out for good (-1, sticky)."""
     T = max(4, args.tune_steps) if args.tune_steps else _auto_tune_steps(wl.bytes_total / ctx.world_size)
     res = {}

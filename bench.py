@@ -55,6 +55,7 @@ from cuda_mpi_reductions_amd.utils.fault import FaultInjector
 from cuda_mpi_reductions_amd.utils.graphs import StepGraph
 
 METRIC = "reduction bandwidth (GB/s, whole node), 1B-double sum at 1/2/4/8 MI355X"
+RELEASE_SETTLE_S = 0.5  # idle after handing GB-sized buffers back to the driver, before timing again
 
 
 def parse_args(argv=None):
@@ -350,6 +351,10 @@ def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES, out: "dict | None" = No
             wl.close()  # collective: the next registration may reuse these addresses
         wls.clear()
         torch.cuda.empty_cache()
+        # GB-sized buffers just went back to the driver: the stream that follows such a release runs
+        # ~6 % slow for a few tens of ms (profiles/r3_passW/settle_bf16.txt, phases E and G), so the
+        # next measurement starts after it has passed.
+        time.sleep(RELEASE_SETTLE_S)
     if ctx.world_size == 1:
         out["note"] = ("world 1: RCCL rows are null (no work); direct is one local send -> receive pass (what "
                        "MPI_Reduce does on one rank); tools/scaling.py keeps N=1 out of the results files")

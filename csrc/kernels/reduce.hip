@@ -119,10 +119,9 @@ Defaults tuned_defaults(size_t bytes, DType t, Op op) {
   if (dtype_size(t) == 8 && bytes > 192 * MB) return {256, 8, 1, 1, 0, 4};
   if ((widening_int || half_cmp) && bytes > 192 * MB) return {256, 8, 2, 1, 0, 2};
   if (dtype_size(t) <= 4 && bytes > 192 * MB) return {256, 8, 1, 1, 0, 4};
-  // 32-192 MB of 4- and 8-byte elements (the reference's default 2^24 doubles is 128 MiB): 256x8x2
-  // with a window of 2 is first or within 0.3 % of first at 64 / 128 / 192 MB f64 and 128 MB f32,
-  // 0.5-4 % ahead of 256x4x3 (profiles/r3_types/small/); at 32 MB every plan ties (launch-bound).
-  if (dtype_size(t) >= 4 && bytes > 32 * MB) return {256, 8, 2, 1, 0, 2};
+  // <= 192 MB: 256x4x3 with hipcc's schedule. (256x8x2 window 2 led tune.py's back-to-back launches
+  // at 64-192 MiB by 0.5-4 %, but not the reduction app's per-iteration timing at the reference's
+  // 2^24 doubles, warm or cold: profiles/r3_types/small/.)
   return {256, 4, 3, 1, 0, 0};
 }
 constexpr int kDefaultGroups = 8;

@@ -47,10 +47,8 @@ def test_tuned_defaults_by_size():
     assert (mid["block"], mid["unroll"], mid["grid"], mid["nontemporal"], mid["window"]) == (256, 8, 256, True, 4)
     l3 = C.plan(0, 1 << 25, F64)           # 256 MB: nt is fast warm and cold (plan_256mb.csv)
     assert (l3["block"], l3["unroll"], l3["grid"], l3["nontemporal"], l3["window"]) == (256, 8, 256, True, 4)
-    small = C.plan(0, 1 << 24, F64)        # 128 MB (the reference default): 256x8x2, window 2
-    assert (small["block"], small["unroll"], small["grid"], small["window"]) == (256, 8, 512, 2)
-    tiny = C.plan(0, 1 << 22, F64)         # 32 MB and less: 256x4x3, hipcc's schedule
-    assert (tiny["block"], tiny["unroll"], tiny["window"]) == (256, 4, 0)
+    small = C.plan(0, 1 << 24, F64)        # 128 MB (the reference default): hipcc's schedule
+    assert (small["block"], small["unroll"], small["window"]) == (256, 4, 0)
     # no size band picks the default (non-nt) policy: it collapses to 2.7 TB/s on a cold cache
     assert all(C.plan(0, n, F64)["nontemporal"] for n in (1, 1 << 20, 3 << 23, 1 << 25, 3 << 24, 1 << 27))
     i64 = C.plan(0, 10**9, 1)              # 8 GB of int64: like fp64
@@ -69,9 +67,8 @@ def test_tuned_defaults_by_size():
     (4, 5 * 10**8, 0, (256, 8, 256, 4)),   # bf16 SUM 1 GB
     (5, 4 * 10**9, 2, (256, 8, 512, 2)),   # f16 MAX 8 GB: 256x8x2, window 2
     (3, 10**9, 1, (256, 8, 256, 4)),       # f64 MIN: the operator does not move 8-byte plans
-    (2, 1 << 24, 0, (256, 8, 512, 2)),     # 32-192 MB: 256x8x2, window 2 (profiles/r3_types/small/)
-    (4, 1 << 25, 0, (256, 4, 768, 0)),     # 16-bit types <= 192 MB: 256x4x3, hipcc's schedule
-    (3, 1 << 22, 0, (256, 4, 768, 0)),     # <= 32 MB: 256x4x3
+    (2, 1 << 24, 0, (256, 4, 768, 0)),     # <= 192 MB: unchanged (256x4x3, hipcc's schedule)
+    (4, 1 << 25, 0, (256, 4, 768, 0)),
 ])
 def test_tuned_defaults_by_dtype_and_op(dtype, n, op, want):
     p = native().plan(0, n, dtype, op=op)

@@ -2,7 +2,7 @@
 # Round 3, GPU pass W: the whole GPU suite on the current tree, smoke(), the driver's default bench,
 # and the settle probe's new phases (G: release + 0.5 s idle; H: small-chunk torch pass + release).
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r3w
+O=gpurun_out/${PASS:-r3w}
 mkdir -p $O
 timeout -k 10 300 python -u tools/settle_probe.py --json $O/settle_bf16.json > $O/settle_bf16.txt 2>&1
 echo "settle rc=$?" >> $O/status.txt

@@ -306,6 +306,8 @@ def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES, out: "dict | None" = No
         try:
             for dt, base in REDUCE_C_DTYPES:  # both registered up front: the rounds interleave dtypes
                 wls[dt] = VectorReduction(_C[base], ctx, impl=impl, direct_timeout_s=5.0).setup()
+            if impl == "direct" and getattr(wls["DOUBLE"], "comm", None) is not None:
+                out["direct_grid"] = wls["DOUBLE"].comm.grid  # CUs / (most ranks sharing one GPU)
             for dt, base in REDUCE_C_DTYPES:  # warm-up SUM per dtype (reduce.c:61-64)
                 wls[dt].cfg = replace(_C[base], op="sum")
                 _one_collective(wls[dt], ctx)

@@ -18,7 +18,6 @@ use, write into ``comm.in_view(n, dtype)`` and read ``comm.out_view(n, dtype)``.
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -27,6 +26,16 @@ import torch.distributed as dist
 from .._native import native
 
 __all__ = ["DirectComm"]
+
+
+def _max_ranks_per_gpu(idx: int, world: int, group) -> int:
+    """The most ranks of ``group`` that run on one physical GPU (collective)."""
+    import socket
+    props = torch.cuda.get_device_properties(idx)
+    key = (socket.gethostname(), str(getattr(props, "uuid", "")) or str(getattr(props, "pci_bus_id", idx)))
+    keys: list = [None] * world
+    dist.all_gather_object(keys, key, group=group)
+    return max(keys.count(k) for k in keys)
 
 
 class _CudaArray:
@@ -40,7 +49,12 @@ class _CudaArray:
 class DirectComm:
     """Registered peer buffers + the one-kernel direct all-reduce / reduce (collective ctor)."""
 
-    def __init__(self, device: torch.device, nbytes: int, group=None, grid: int = 0, timeout_s: float = 10.0):
+    def __init__(self, device: torch.device, nbytes: int, group=None, grid: int = 0, timeout_s: float = 10.0,
+                 fault=None):
+        """``grid`` 0: one workgroup per CU, divided by the most ranks that share one GPU (every
+        rank's workgroups must be co-resident to meet at the device-side barriers; ranks sharing a
+        GPU — the one-GPU rehearsals — split its CUs). ``fault`` (:class:`utils.fault.FaultInjector`,
+        kind ``mailbox``): that rank fails to register its buffers (the failure-path test)."""
         C = native()
         self.device = torch.device(device)
         self.group = group
@@ -49,13 +63,17 @@ class DirectComm:
             world, rank = dist.get_world_size(group), dist.get_rank(group)
         else:
             world, rank = 1, 0
+        if grid <= 0 and world > 1:
+            share = _max_ranks_per_gpu(idx, world, group)
+            if share > 1:
+                grid = max(1, torch.cuda.get_device_properties(idx).multi_processor_count // share)
         # Same failure-safe protocol as parallel.xrank.open_channel: every rank reaches every
         # collective, errors are agreed on and raised on all ranks together.
         err, handles = None, b""
         self._d = None
         try:
-            if os.environ.get("MIREDUCE_DIRECT_FAIL_RANK") == str(rank):  # failure-path test hook
-                raise RuntimeError("injected registration failure (MIREDUCE_DIRECT_FAIL_RANK)")
+            if fault is not None and fault.mailbox(rank):
+                raise RuntimeError("injected registration failure (--inject-fault mailbox)")
             self._d = C.DirectAllreduce(idx, int(nbytes), int(grid), float(timeout_s))
             handles = self._d.handles()
         except Exception as e:  # noqa: BLE001
@@ -84,6 +102,7 @@ class DirectComm:
             raise RuntimeError("direct collective unavailable: " + "; ".join(bad)[:500])
         self.rank, self.world = rank, world
         self.nbytes = self._d.bytes
+        self.grid = self._d.grid  # workgroups per collective (see ``grid`` above)
 
     # ------------------------------------------------------------------ buffers
     def in_view(self, n: int, dtype: torch.dtype) -> torch.Tensor:

@@ -191,6 +191,19 @@ def test_direct_comm_world1_views_and_staging():
         comm.read_peers((1 << 20) + 4096)
 
 
+def test_direct_comm_registration_fault():
+    # --inject-fault mailbox: this rank fails to register its buffers; the collective constructor
+    # reports it (on every rank) instead of leaving a peer blocked
+    from cuda_mpi_reductions_amd.parallel import DirectComm
+    from cuda_mpi_reductions_amd.utils.fault import FaultInjector, parse_fault_spec
+    with pytest.raises(RuntimeError, match="direct collective unavailable: rank 0: .*injected registration failure"):
+        DirectComm(torch.device("cuda", 0), 1 << 20, fault=FaultInjector(parse_fault_spec("mailbox@0")))
+    comm = DirectComm(torch.device("cuda", 0), 1 << 20)  # world 1: one workgroup per CU
+    assert comm.grid == torch.cuda.get_device_properties(0).multi_processor_count
+    print("device uuid:", getattr(torch.cuda.get_device_properties(0), "uuid", None),
+          "pci_bus_id:", getattr(torch.cuda.get_device_properties(0), "pci_bus_id", None))
+
+
 @pytest.mark.parametrize("nproc", [2, 3])
 def test_bench_vector_direct_ranks_share_one_gpu(tmp_path, nproc, monkeypatch):
     # reduce.c semantics through bench.py with the direct one-kernel collective (verified against the
@@ -271,6 +284,8 @@ def test_bench_eight_ranks_auto_on_one_gpu(tmp_path, monkeypatch):
     bad = [t for t in ex["table"] if t.get("verified") is not True]
     assert not bad and len(ex["table"]) == 30, (bad, r.stderr[-2000:])
     assert ex["reduce_direct"].get("verified") is True, (ex["reduce_direct"], ex.get("allreduce_direct"))
+    # eight ranks on one GPU split its CUs, so every rank's barrier kernel can be co-resident
+    assert ex["direct_grid"] == torch.cuda.get_device_properties(0).multi_processor_count // 8, ex["direct_grid"]
     assert len(ex["rows"]["direct"]) == 31 and ex["rows"]["direct"][1].startswith("INT MAX 8 ")
     pr = ex["peer_read"]  # fabric probe: 8 ranks reading each other's buffers (here all on one GPU)
     assert "error" not in pr and 0 < pr["ingress_gbps_min"] <= pr["ingress_gbps_max"] and pr["node_gbps"] > 0, pr

@@ -41,6 +41,17 @@ ArgPlan arg_reduce_rows(const void* in, size_t rows, size_t cols, DType t, Op op
                         int64_t* out_index, void* scratch, int num_cus, hipStream_t stream,
                         ArgTune tune = {});
 
+// Cross-rank MAXLOC / MINLOC combine of one (value, index) pair per rank, device-side and
+// graph-capturable (models/loc.py): loc_pack writes this rank's pair — the value's comparison key
+// bits (16-bit floats widened to fp32) and index + index_offset — as 2 uint64 words; after an
+// all-gather of the pairs, loc_pick folds `world` of them with arg_reduce's rules (the extreme
+// wins, NaN being the extreme; equal values: the smaller index) and writes the winning global index
+// to out_index[0] (and, when out_value is not null, its value in element type t). One thread each.
+void loc_pack(const void* value, const int64_t* index, int64_t index_offset, DType t, uint64_t* pair,
+              hipStream_t stream);
+void loc_pick(const uint64_t* pairs, int world, DType t, Op op, int64_t* out_index, void* out_value,
+              hipStream_t stream);
+
 // Host reference with the same semantics (multi-threaded over rows).
 void cpu_arg_reduce_rows(const void* in, size_t rows, size_t cols, DType t, Op op, void* out_value,
                          int64_t* out_index);

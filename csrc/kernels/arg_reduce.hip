@@ -508,6 +508,34 @@ __global__ __launch_bounds__(kArgBlock) void arg_short_kernel(ArgArgs a) {
   }
 }
 
+// Cross-rank MAXLOC / MINLOC pairs (arg_reduce.hpp loc_pack / loc_pick): one thread each.
+template <class T>
+__global__ void loc_pack_kernel(const T* __restrict__ value, const int64_t* __restrict__ index, int64_t offset,
+                                uint64_t* __restrict__ pair) {
+  using K = typename ArgKey<T>::type;
+  pair[0] = key_bits(load_key<T, K>(value));
+  pair[1] = static_cast<uint64_t>(index[0] + offset);
+}
+
+template <bool MAX, class T>
+__global__ void loc_pick_kernel(const uint64_t* __restrict__ pairs, int world, int64_t* __restrict__ out_index,
+                                T* __restrict__ out_value) {
+  using K = typename ArgKey<T>::type;
+  using C = ArgCmp<MAX, K>;
+  K bv = bits_key<K>(pairs[0]);
+  int64_t bi = static_cast<int64_t>(pairs[1]);
+  for (int r = 1; r < world; ++r) {
+    const K v = bits_key<K>(pairs[2 * r]);
+    const int64_t i = static_cast<int64_t>(pairs[2 * r + 1]);
+    if (C::pair_beats(v, i, bv, bi)) {
+      bv = v;
+      bi = i;
+    }
+  }
+  out_index[0] = bi;
+  if (out_value) out_value[0] = key_to_elem<T, K>(bv);
+}
+
 }  // namespace kern
 
 namespace {
@@ -654,6 +682,19 @@ ArgEntry arg_lookup(Op op, DType t) {
   return op == Op::Max ? arg_lookup_dtype<true>(t) : arg_lookup_dtype<false>(t);
 }
 
+template <class T>
+void launch_loc_pack(const void* value, const int64_t* index, int64_t offset, uint64_t* pair, hipStream_t s) {
+  hipLaunchKernelGGL(kern::loc_pack_kernel<T>, dim3(1), dim3(1), 0, s, static_cast<const T*>(value), index, offset, pair);
+}
+
+template <class T>
+void launch_loc_pick(const uint64_t* pairs, int world, bool max, int64_t* out_index, void* out_value, hipStream_t s) {
+  if (max) hipLaunchKernelGGL((kern::loc_pick_kernel<true, T>), dim3(1), dim3(1), 0, s, pairs, world, out_index,
+                              static_cast<T*>(out_value));
+  else hipLaunchKernelGGL((kern::loc_pick_kernel<false, T>), dim3(1), dim3(1), 0, s, pairs, world, out_index,
+                          static_cast<T*>(out_value));
+}
+
 size_t ticket_bytes(uint64_t rows) { return (rows * sizeof(unsigned) + 255) / 256 * 256; }
 
 // Split rows have rows < target = num_cus x resident <= num_cus x kMaxResident (arg_layout), so
@@ -728,6 +769,36 @@ ArgPlan arg_reduce_rows(const void* in, size_t rows, size_t cols, DType t, Op op
   plan.unroll = variant == kLong || variant == kWave ? unroll : kern::kArgUnroll;
   plan.wg_per_cu = resident;
   return plan;
+}
+
+void loc_pack(const void* value, const int64_t* index, int64_t index_offset, DType t, uint64_t* pair,
+              hipStream_t stream) {
+  MIREDUCE_REQUIRE(value != nullptr && index != nullptr && pair != nullptr, "loc_pack: null pointer");
+  switch (t) {
+    case DType::Int32: launch_loc_pack<int32_t>(value, index, index_offset, pair, stream); break;
+    case DType::Int64: launch_loc_pack<int64_t>(value, index, index_offset, pair, stream); break;
+    case DType::Float32: launch_loc_pack<float>(value, index, index_offset, pair, stream); break;
+    case DType::Float64: launch_loc_pack<double>(value, index, index_offset, pair, stream); break;
+    case DType::BFloat16: launch_loc_pack<bf16_t>(value, index, index_offset, pair, stream); break;
+    case DType::Float16: launch_loc_pack<f16_t>(value, index, index_offset, pair, stream); break;
+  }
+  MIREDUCE_HIP_THROW(hipGetLastError());
+}
+
+void loc_pick(const uint64_t* pairs, int world, DType t, Op op, int64_t* out_index, void* out_value,
+              hipStream_t stream) {
+  MIREDUCE_REQUIRE(op == Op::Max || op == Op::Min, "loc_pick: the operator must be MAX or MIN");
+  MIREDUCE_REQUIRE(world >= 1 && pairs != nullptr && out_index != nullptr, "loc_pick: bad arguments");
+  const bool mx = op == Op::Max;
+  switch (t) {
+    case DType::Int32: launch_loc_pick<int32_t>(pairs, world, mx, out_index, out_value, stream); break;
+    case DType::Int64: launch_loc_pick<int64_t>(pairs, world, mx, out_index, out_value, stream); break;
+    case DType::Float32: launch_loc_pick<float>(pairs, world, mx, out_index, out_value, stream); break;
+    case DType::Float64: launch_loc_pick<double>(pairs, world, mx, out_index, out_value, stream); break;
+    case DType::BFloat16: launch_loc_pick<bf16_t>(pairs, world, mx, out_index, out_value, stream); break;
+    case DType::Float16: launch_loc_pick<f16_t>(pairs, world, mx, out_index, out_value, stream); break;
+  }
+  MIREDUCE_HIP_THROW(hipGetLastError());
 }
 
 }  // namespace mireduce

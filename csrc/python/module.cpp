@@ -493,6 +493,22 @@ PYBIND11_MODULE(_C, m) {
       py::arg("in_ptr"), py::arg("rows"), py::arg("cols"), py::arg("dtype"), py::arg("op"), py::arg("out_value_ptr"),
       py::arg("out_index_ptr"), py::arg("scratch_ptr"), py::arg("num_cus"), py::arg("stream") = 0,
       py::arg("unroll") = 0, py::arg("wg_per_cu") = 0);
+  m.def(
+      "loc_pack",
+      [](uintptr_t value, uintptr_t index, int64_t offset, int dtype, uintptr_t pair, uintptr_t stream) {
+        loc_pack(as_ptr<const void>(value), as_ptr<const int64_t>(index), offset, static_cast<DType>(dtype),
+                 as_ptr<uint64_t>(pair), as_stream(stream));
+      },
+      py::arg("value_ptr"), py::arg("index_ptr"), py::arg("offset"), py::arg("dtype"), py::arg("pair_ptr"),
+      py::arg("stream") = 0);
+  m.def(
+      "loc_pick",
+      [](uintptr_t pairs, int world, int dtype, int op, uintptr_t out_index, uintptr_t out_value, uintptr_t stream) {
+        loc_pick(as_ptr<const uint64_t>(pairs), world, static_cast<DType>(dtype), static_cast<Op>(op),
+                 as_ptr<int64_t>(out_index), as_ptr<void>(out_value), as_stream(stream));
+      },
+      py::arg("pairs_ptr"), py::arg("world"), py::arg("dtype"), py::arg("op"), py::arg("out_index_ptr"),
+      py::arg("out_value_ptr") = 0, py::arg("stream") = 0);
   m.def("arg_reduce_scratch_bytes", [](uint64_t rows, uint64_t cols, int dtype, int num_cus) {
     return arg_reduce_scratch_bytes(rows, cols, static_cast<DType>(dtype), num_cus);
   });

@@ -7,8 +7,11 @@ north-star shape — local HIP pass over this rank's shard, then a tiny cross-ra
 
 * local: ``arg_reduce_rows`` (csrc/kernels/arg_reduce.hip) on a prepared scratch buffer — first
   index of the extreme and its value, one launch, single-pass finish;
-* global: :func:`parallel.dist.loc_allreduce` — two 1-element all-gathers over RCCL and a
-  device-side pick of the smallest index among the ranks holding the extreme.
+* global, GPUs over RCCL: ``loc_pack`` writes this rank's (value key, global index) pair, ONE
+  all-gather of the pairs, ``loc_pick`` folds them with arg_reduce's rules and writes the global
+  index into the step's slot — three launches and one collective per step (the torch version, two
+  all-gathers and ~8 elementwise ops, cost 27 us per step at N=1: profiles/r3_configs/);
+* global, gloo / CPU ranks: :func:`parallel.dist.loc_allreduce` (two all-gathers and a pick).
 
 No host synchronisation anywhere, so bench.py captures the steps into hipGraphs like the scalar
 reductions. The slot a step writes holds the global index (int64).
@@ -74,6 +77,9 @@ class LocReduction:
             self._ncu = torch.cuda.get_device_properties(dev).multi_processor_count
             need = self._C.arg_reduce_scratch_bytes(1, self.count, self._dt, self._ncu)
             self._scratch = torch.zeros(max(need, 256), dtype=torch.uint8, device=dev)  # tickets start at 0
+            self._pair = torch.empty(2, dtype=torch.int64, device=dev)
+            self._pairs = torch.empty(2 * self.ctx.world_size, dtype=torch.int64, device=dev)
+            self._device_pick = self.ctx.world_size == 1 or self.ctx.backend == "nccl"
             self.lanes = [(torch.cuda.current_stream(dev), None)]
             torch.cuda.synchronize(dev)
         return self
@@ -99,6 +105,16 @@ class LocReduction:
         """Local arg-reduction, then the cross-rank MAXLOC/MINLOC; writes the global index into
         ``out`` (1 element). ``corrupt`` (fault injection) shifts this rank's local index."""
         self._local()
+        if self.ctx.device.type == "cuda" and self._device_pick:
+            sh = _stream_handle(self.ctx.device)
+            self._C.loc_pack(self.val.data_ptr(), self.idx.data_ptr(), self.offset + (1 if corrupt else 0), self._dt,
+                             self._pair.data_ptr(), sh)
+            pairs, world = self._pair, 1
+            if self.issues_collective:
+                torch.distributed.all_gather_into_tensor(self._pairs, self._pair)
+                pairs, world = self._pairs, self.ctx.world_size
+            self._C.loc_pick(pairs.data_ptr(), world, self._dt, self._op, out.data_ptr(), 0, sh)
+            return None
         gi = self.idx + self._offset_t
         if corrupt:
             gi = gi + 1

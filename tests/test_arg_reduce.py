@@ -246,3 +246,40 @@ def test_device_native_kernel_runs():
                              torch.cuda.current_stream().cuda_stream)
     assert plan["splits"] > 1 and plan["grid"] >= 256
     assert int(i) == int(x.cpu().argmax())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("op", ["max", "min"])
+def test_device_loc_pack_pick(dt, op):
+    # the device-side MAXLOC / MINLOC combine (models/loc.py): one (value, index + offset) pair per
+    # "rank", folded with arg_reduce's rules — the extreme wins, equal values go to the smaller
+    # global index, NaN is the extreme
+    from cuda_mpi_reductions_amd._native import native
+    from cuda_mpi_reductions_amd.ops.reduce import DTYPE_CODES, op_code
+    C = native()
+    code, oc = DTYPE_CODES[dt], op_code(op)
+
+    def pick(values, local_idx, offsets):
+        w = len(values)
+        pairs = torch.empty(2 * w, dtype=torch.int64, device="cuda")
+        val = torch.tensor(values, dtype=torch.float64).to(dt).cuda()
+        idx = torch.tensor(local_idx, dtype=torch.int64, device="cuda")
+        for r in range(w):
+            C.loc_pack(val[r:].data_ptr(), idx[r:].data_ptr(), offsets[r], code, pairs[2 * r:].data_ptr())
+        out_i = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+        out_v = torch.empty(1, dtype=dt, device="cuda")
+        C.loc_pick(pairs.data_ptr(), w, code, oc, out_i.data_ptr(), out_v.data_ptr())
+        torch.cuda.synchronize()
+        return int(out_i), out_v.cpu().double().item()
+
+    # ties on the extreme across ranks: the smallest GLOBAL index wins (offset + local index)
+    vals = [3, 7, 7, -2, 7, -2]
+    loc = [50, 40, 10, 5, 30, 6]
+    offs = [0, 100, 200, 300, 400, 500]
+    gi, v = pick(vals, loc, offs)
+    assert (gi, v) == ((140, 7.0) if op == "max" else (305, -2.0))
+    assert pick([5], [9], [1000]) == (1009, 5.0)  # world 1
+    if dt.is_floating_point:
+        gi, v = pick([3, float("nan"), 7, float("nan")], [1, 9, 2, 4], [0, 10, 20, 30])
+        assert gi == 19 and v != v  # the first NaN (global index 10 + 9) beats every number, max or min

@@ -4,4 +4,5 @@ from .dist import (  # noqa: F401
     vector_allreduce, vector_reduce,
 )
 from .direct import DirectComm  # noqa: F401,E402
+from .topology import PeerMap, peer_map, peer_verdict  # noqa: F401,E402
 from .xrank import check_channel, open_channel  # noqa: F401,E402

@@ -24,18 +24,9 @@ import torch
 import torch.distributed as dist
 
 from .._native import native
+from .topology import peer_map
 
 __all__ = ["DirectComm"]
-
-
-def _max_ranks_per_gpu(idx: int, world: int, group) -> int:
-    """The most ranks of ``group`` that run on one physical GPU (collective)."""
-    import socket
-    props = torch.cuda.get_device_properties(idx)
-    key = (socket.gethostname(), str(getattr(props, "uuid", "")) or str(getattr(props, "pci_bus_id", idx)))
-    keys: list = [None] * world
-    dist.all_gather_object(keys, key, group=group)
-    return max(keys.count(k) for k in keys)
 
 
 class _CudaArray:
@@ -63,10 +54,12 @@ class DirectComm:
             world, rank = dist.get_world_size(group), dist.get_rank(group)
         else:
             world, rank = 1, 0
-        if grid <= 0 and world > 1:
-            share = _max_ranks_per_gpu(idx, world, group)
-            if share > 1:
-                grid = max(1, torch.cuda.get_device_properties(idx).multi_processor_count // share)
+        if world > 1:
+            pm = peer_map(idx, group)  # collective; the same verdict on every rank
+            if pm.error:
+                raise RuntimeError("direct collective unavailable: " + pm.error)
+            if grid <= 0 and pm.ranks_per_gpu > 1:
+                grid = max(1, torch.cuda.get_device_properties(idx).multi_processor_count // pm.ranks_per_gpu)
         # Same failure-safe protocol as parallel.xrank.open_channel: every rank reaches every
         # collective, errors are agreed on and raised on all ranks together.
         err, handles = None, b""

@@ -19,6 +19,7 @@ import torch
 import torch.distributed as dist
 
 from .._native import native
+from .topology import peer_map
 
 __all__ = ["open_channel", "check_channel", "close_channels"]
 
@@ -37,6 +38,9 @@ def open_channel(device: torch.device, group=None, timeout_s: float = 2.0, fault
     rank = dist.get_rank(group)
     if world > C.XRANK_MAX_RANKS:
         raise ValueError(f"fused finish supports at most {C.XRANK_MAX_RANKS} ranks, got {world}")
+    pm = peer_map(idx, group)  # collective; the same verdict on every rank
+    if pm.error:
+        raise RuntimeError("fused cross-rank finish unavailable: " + pm.error)
     # Every step below is reached by every rank (errors are agreed on, not raised mid-protocol),
     # so one rank's failure to allocate or map cannot leave the others blocked in a collective.
     err, ch, handle = None, None, b""

@@ -133,7 +133,11 @@ __global__ __launch_bounds__(kDimBlock) void rows_kernel(RowArgs a) {
 // loads in flight, instead of one load per loop trip.
 // ALIGNED (base and row length multiples of 16 bytes): rows are whole vectors — no per-row
 // alignment arithmetic or head/tail loops (8 / 64-column bf16 rows: VALU-bound without it).
-template <class OpT, class T, class AccT, bool ALIGNED>
+// PIPE (aligned rows only): two register batches, the next batch's loads issued before the current
+// one is folded, so a wave keeps 2 x kRowUnroll vectors in flight across loop trips instead of
+// draining to zero at every trip's fold (the single-batch loop waits one full memory latency per
+// trip: 2.7 TB/s at one workgroup per CU for 8-column bf16 rows).
+template <class OpT, class T, class AccT, bool ALIGNED, bool PIPE = false>
 __global__ __launch_bounds__(kDimBlock) void short_rows_kernel(RowArgs a) {
   using V = typename Vec16<T>::type;
   constexpr int N = Vec16<T>::N;
@@ -147,6 +151,49 @@ __global__ __launch_bounds__(kDimBlock) void short_rows_kernel(RowArgs a) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * (kDimBlock / 64) * batch;
   const T* base = static_cast<const T*>(a.in);
   AccT* out = static_cast<AccT*>(a.out);
+  if constexpr (ALIGNED && PIPE) {
+    const uint64_t vecs = a.cols / N;
+    const V* vbase = reinterpret_cast<const V*>(base);
+    auto load = [&](uint64_t row0, V* v) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const uint64_t r = row0 + static_cast<uint64_t>(j) * per_wave + sub;
+        const bool ok = r < a.rows && static_cast<uint64_t>(sl) < vecs;
+        v[j] = __builtin_nontemporal_load(ok ? vbase + r * vecs + sl : &g_dummy_vec<V>);
+      }
+    };
+    auto fold = [&](uint64_t row0, const V* v) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const uint64_t r = row0 + static_cast<uint64_t>(j) * per_wave + sub;
+        AccT acc = OpT::template identity<AccT>();
+        if (r < a.rows && static_cast<uint64_t>(sl) < vecs) {
+#pragma unroll
+          for (int k = 0; k < N; ++k) acc = OpT::apply(acc, OpT::pre(elem<T, AccT>(v[j], k)));
+        }
+        for (int off = lpr >> 1; off > 0; off >>= 1) acc = OpT::apply(acc, __shfl_xor(acc, off, 64));
+        if (sl == 0 && r < a.rows) out[r] = acc;
+      }
+    };
+    uint64_t row0 = wave * batch;
+    if (row0 >= a.rows) return;  // wave-uniform; the kernel has no workgroup barrier
+    V va[U], vb[U];
+    load(row0, va);
+    for (;;) {  // wave-uniform trips, unrolled by two so the batches stay in fixed registers
+      const uint64_t r1 = row0 + stride;
+      if (r1 < a.rows) load(r1, vb);
+      __builtin_amdgcn_sched_barrier(0);
+      fold(row0, va);
+      if (r1 >= a.rows) break;
+      const uint64_t r2 = r1 + stride;
+      if (r2 < a.rows) load(r2, va);
+      __builtin_amdgcn_sched_barrier(0);
+      fold(r1, vb);
+      if (r2 >= a.rows) break;
+      row0 = r2;
+    }
+    return;
+  }
   for (uint64_t row0 = wave * batch; row0 < a.rows; row0 += stride) {  // wave-uniform loop
     // Issue all U loads first, without branches: a lane with no vector in its row (or past the
     // last row) loads the dummy vector instead (a branch per load made hipcc wait for every load
@@ -409,6 +456,16 @@ int wg_cap(int occ, int preferred) {
   return cap > 0 ? std::min(occ, cap) : occ;
 }
 
+// Aligned short rows: the two-batch pipelined loop (short_rows_kernel PIPE). MIREDUCE_DIM_SHORT_PIPE=0
+// selects the single-batch loop (A/B runs).
+bool short_pipe() {
+  static const bool on = [] {
+    const char* e = std::getenv("MIREDUCE_DIM_SHORT_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 using RowFn = void (*)(const kern::RowArgs&, int, hipStream_t);
 using OccFn = int (*)(bool);  // resident workgroups per CU of the (short-row | vector) variant
 using ColFn = void (*)(const kern::ColArgs&, dim3, bool, hipStream_t);
@@ -416,7 +473,9 @@ using FoldFn = void (*)(const void*, uint64_t, uint64_t, void*, hipStream_t);
 
 template <class OpT, class T, class AccT>
 void launch_rows(const kern::RowArgs& a, int grid, hipStream_t s) {
-  if (a.lpr < 64 && a.aligned)
+  if (a.lpr < 64 && a.aligned && short_pipe())
+    hipLaunchKernelGGL((kern::short_rows_kernel<OpT, T, AccT, true, true>), dim3(grid), dim3(kern::kDimBlock), 0, s, a);
+  else if (a.lpr < 64 && a.aligned)
     hipLaunchKernelGGL((kern::short_rows_kernel<OpT, T, AccT, true>), dim3(grid), dim3(kern::kDimBlock), 0, s, a);
   else if (a.lpr < 64)
     hipLaunchKernelGGL((kern::short_rows_kernel<OpT, T, AccT, false>), dim3(grid), dim3(kern::kDimBlock), 0, s, a);
@@ -442,7 +501,8 @@ void launch_fold(const void* partials, uint64_t splits, uint64_t cols, void* out
 
 template <class OpT, class T, class AccT>
 int rows_resident(bool short_rows) {
-  static const int s = resident_per_cu(kern::short_rows_kernel<OpT, T, AccT, false>);
+  static const int s = std::min(resident_per_cu(kern::short_rows_kernel<OpT, T, AccT, false>),
+                                resident_per_cu(kern::short_rows_kernel<OpT, T, AccT, true, true>));
   static const int l = resident_per_cu(kern::rows_kernel<OpT, T, AccT>);
   return short_rows ? s : l;
 }

@@ -402,10 +402,8 @@ __global__ __launch_bounds__(kArgBlock) void arg_wave_rows_kernel(ArgArgs a) {
 
 // Short 16-byte-aligned rows (cols * sizeof(T) a multiple of 16, at most lpr * M vectors): lpr
 // lanes per row, each lane M 16-byte vectors per row, kArgUnroll batches of (64 / lpr) rows per
-// wave trip, all loads issued before the first compare. PIPE: two register sets, the next trip's
-// loads issued before this trip's compares (a wave never drains its loads to zero between trips;
-// same scheme as reduce_dim.hip's short_rows_kernel PIPE).
-template <bool MAX, class T, int M, bool PIPE = false>
+// wave trip, all loads issued before the first compare.
+template <bool MAX, class T, int M>
 __global__ __launch_bounds__(kArgBlock) void arg_short_vec_kernel(ArgArgs a) {
   using K = typename ArgKey<T>::type;
   using C = ArgCmp<MAX, K>;
@@ -420,9 +418,9 @@ __global__ __launch_bounds__(kArgBlock) void arg_short_vec_kernel(ArgArgs a) {
   const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * kArgBlock + threadIdx.x) / 64;
   const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * (kArgBlock / 64);
   const uint64_t per_trip = static_cast<uint64_t>(per_wave) * U;
-  const uint64_t step = nwaves * per_trip;
   const V* base = static_cast<const V*>(a.in);
-  auto load = [&](uint64_t r0, V (&v)[U][M]) {
+  for (uint64_t r0 = wave * per_trip; r0 < a.rows; r0 += nwaves * per_trip) {  // wave-uniform
+    V v[U][M];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t r = r0 + static_cast<uint64_t>(u) * per_wave + sub;
@@ -433,8 +431,7 @@ __global__ __launch_bounds__(kArgBlock) void arg_short_vec_kernel(ArgArgs a) {
         v[u][mm] = __builtin_nontemporal_load(ok ? base + r * vecs + c : &g_arg_dummy_vec<V>);
       }
     }
-  };
-  auto pick = [&](uint64_t r0, const V (&v)[U][M]) {
+    __builtin_amdgcn_sched_barrier(0);  // all loads out before the first compare
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint64_t r = r0 + static_cast<uint64_t>(u) * per_wave + sub;
@@ -458,32 +455,6 @@ __global__ __launch_bounds__(kArgBlock) void arg_short_vec_kernel(ArgArgs a) {
         static_cast<T*>(a.out_value)[r] = key_to_elem<T, K>(bv);
         a.out_index[r] = bi == kNoIndex32 ? 0 : static_cast<int64_t>(bi);
       }
-    }
-  };
-  if constexpr (PIPE) {
-    uint64_t r0 = wave * per_trip;
-    if (r0 >= a.rows) return;  // wave-uniform; the kernel has no workgroup barrier
-    V va[U][M], vb[U][M];
-    load(r0, va);
-    for (;;) {  // wave-uniform trips, unrolled by two so the register sets stay fixed
-      const uint64_t r1 = r0 + step;
-      if (r1 < a.rows) load(r1, vb);
-      __builtin_amdgcn_sched_barrier(0);
-      pick(r0, va);
-      if (r1 >= a.rows) break;
-      const uint64_t r2 = r1 + step;
-      if (r2 < a.rows) load(r2, va);
-      __builtin_amdgcn_sched_barrier(0);
-      pick(r1, vb);
-      if (r2 >= a.rows) break;
-      r0 = r2;
-    }
-  } else {
-    for (uint64_t r0 = wave * per_trip; r0 < a.rows; r0 += step) {  // wave-uniform
-      V v[U][M];
-      load(r0, v);
-      __builtin_amdgcn_sched_barrier(0);  // all loads out before the first compare
-      pick(r0, v);
     }
   }
 }
@@ -632,16 +603,6 @@ int resident_of(Kern k) {
   return std::min(n, kMaxResident);
 }
 
-// 1- and 2-vector short rows: the two-set pipelined loop (arg_short_vec_kernel PIPE).
-// MIREDUCE_ARG_SHORT_PIPE=0 selects the single-set loop (A/B runs).
-bool arg_short_pipe() {
-  static const bool on = [] {
-    const char* e = std::getenv("MIREDUCE_ARG_SHORT_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 using ArgFn = void (*)(const kern::ArgArgs&, int variant, int unroll, int grid, hipStream_t);
 using ArgOccFn = int (*)(int variant, int unroll);
 
@@ -657,19 +618,13 @@ void launch_arg(const kern::ArgArgs& a, int variant, int unroll, int grid, hipSt
     case kScalar1: hipLaunchKernelGGL((kern::arg_short_kernel<MAX, T, 1>), g, b, 0, s, a); break;
     case kScalar2: hipLaunchKernelGGL((kern::arg_short_kernel<MAX, T, 2>), g, b, 0, s, a); break;
     case kScalar4: hipLaunchKernelGGL((kern::arg_short_kernel<MAX, T, 4>), g, b, 0, s, a); break;
-    case kVec1:
-      if (arg_short_pipe()) hipLaunchKernelGGL((kern::arg_short_vec_kernel<MAX, T, 1, true>), g, b, 0, s, a);
-      else hipLaunchKernelGGL((kern::arg_short_vec_kernel<MAX, T, 1>), g, b, 0, s, a);
-      break;
+    case kVec1: hipLaunchKernelGGL((kern::arg_short_vec_kernel<MAX, T, 1>), g, b, 0, s, a); break;
     case kWave:
       if (unroll == 2) hipLaunchKernelGGL((kern::arg_wave_rows_kernel<MAX, T, 2>), g, b, 0, s, a);
       else if (unroll == 8) hipLaunchKernelGGL((kern::arg_wave_rows_kernel<MAX, T, 8>), g, b, 0, s, a);
       else hipLaunchKernelGGL((kern::arg_wave_rows_kernel<MAX, T, 4>), g, b, 0, s, a);
       break;
-    case kVec2:
-      if (arg_short_pipe()) hipLaunchKernelGGL((kern::arg_short_vec_kernel<MAX, T, 2, true>), g, b, 0, s, a);
-      else hipLaunchKernelGGL((kern::arg_short_vec_kernel<MAX, T, 2>), g, b, 0, s, a);
-      break;
+    case kVec2: hipLaunchKernelGGL((kern::arg_short_vec_kernel<MAX, T, 2>), g, b, 0, s, a); break;
     default: hipLaunchKernelGGL((kern::arg_short_vec_kernel<MAX, T, 4>), g, b, 0, s, a); break;
   }
 }
@@ -686,10 +641,8 @@ int arg_resident(int variant, int unroll) {
                              resident_of(kern::arg_short_kernel<MAX, T, 1>),
                              resident_of(kern::arg_short_kernel<MAX, T, 2>),
                              resident_of(kern::arg_short_kernel<MAX, T, 4>),
-                             arg_short_pipe() ? resident_of(kern::arg_short_vec_kernel<MAX, T, 1, true>)
-                                              : resident_of(kern::arg_short_vec_kernel<MAX, T, 1>),
-                             arg_short_pipe() ? resident_of(kern::arg_short_vec_kernel<MAX, T, 2, true>)
-                                              : resident_of(kern::arg_short_vec_kernel<MAX, T, 2>)};
+                             resident_of(kern::arg_short_vec_kernel<MAX, T, 1>),
+                             resident_of(kern::arg_short_vec_kernel<MAX, T, 2>)};
   switch (variant) {
     case kLong: return occ_long[unroll == 2 ? 0 : unroll == 8 ? 2 : 1];
     case kWave: return occ_wave[unroll == 2 ? 0 : unroll == 8 ? 2 : 1];

@@ -43,6 +43,7 @@ struct RowArgs {
   uint64_t seg_len;  // elements per segment (multiple of the vector width)
   int lpr;           // lanes per segment (power of two, 1..64)
   int aligned;       // short rows: base and row length multiples of 16 bytes
+  int nt_out;        // short rows, pipelined loop: non-temporal result stores (MIREDUCE_DIM_NT_OUT)
   void* out;
   void* partials;    // [rows * splits] AccT (splits > 1)
   unsigned* tickets; // [rows] (splits > 1)
@@ -172,7 +173,10 @@ __global__ __launch_bounds__(kDimBlock) void short_rows_kernel(RowArgs a) {
           for (int k = 0; k < N; ++k) acc = OpT::apply(acc, OpT::pre(elem<T, AccT>(v[j], k)));
         }
         for (int off = lpr >> 1; off > 0; off >>= 1) acc = OpT::apply(acc, __shfl_xor(acc, off, 64));
-        if (sl == 0 && r < a.rows) out[r] = acc;
+        if (sl == 0 && r < a.rows) {
+          if (a.nt_out) __builtin_nontemporal_store(acc, out + r);  // streaming output, no L2 reuse
+          else out[r] = acc;
+        }
       }
     };
     uint64_t row0 = wave * batch;
@@ -466,6 +470,17 @@ bool short_pipe() {
   return on;
 }
 
+// Pipelined short rows: MIREDUCE_DIM_NT_OUT=1 writes the results with non-temporal stores (one
+// AccT per row is up to a quarter of the traffic at 8 columns); plain stores by default until an
+// A/B on the GPU says otherwise (tools/gpu/r3zb.sh).
+bool short_nt_out() {
+  static const bool on = [] {
+    const char* e = std::getenv("MIREDUCE_DIM_NT_OUT");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 using RowFn = void (*)(const kern::RowArgs&, int, hipStream_t);
 using OccFn = int (*)(bool);  // resident workgroups per CU of the (short-row | vector) variant
 using ColFn = void (*)(const kern::ColArgs&, dim3, bool, hipStream_t);
@@ -609,6 +624,7 @@ DimPlan reduce_rows(const void* in, size_t rows, size_t cols, DType t, Op op, DT
   a.lpr = L.lpr;
   a.aligned = reinterpret_cast<uintptr_t>(in) % 16 == 0 && (cols * dtype_size(t)) % 16 == 0;
   a.out = out;
+  a.nt_out = short_nt_out() ? 1 : 0;
   if (L.splits > 1) {
     MIREDUCE_REQUIRE(scratch != nullptr, "reduce_rows: this shape needs scratch (reduce_rows_scratch_bytes)");
     MIREDUCE_REQUIRE(rows < static_cast<size_t>(num_cus) * 16, "reduce_rows: split rows exceed the ticket region");

@@ -714,6 +714,20 @@ def _tune_plan(wl, ctx, args, fault, kernel, cands) -> "tuple[KernelConfig, dict
     return kernel, {"steps": T, "gbps": res, "chosen": best}
 
 
+def _topology(ctx) -> dict:
+    """Where the ranks ran (parallel/topology.py peer_map): hosts, physical GPUs, ranks per GPU and
+    the agreed peer-access verdict of the IPC-mapped paths (collective at N > 1)."""
+    from cuda_mpi_reductions_amd.parallel.topology import peer_map
+    try:
+        pm = peer_map(ctx.device.index if ctx.device.index is not None else torch.cuda.current_device())
+    except Exception as e:  # noqa: BLE001 - a record field must never cost the headline
+        return {"error": f"{type(e).__name__}: {e}"[:200]}
+    return {"hosts": len({k[0] for k in pm.keys}), "gpus": len({(k[0], k[1]) for k in pm.keys}),
+            "ranks_per_gpu": pm.ranks_per_gpu,
+            "peer_access": "n/a (one GPU)" if len({(k[0], k[1]) for k in pm.keys}) == 1 else
+                           (pm.error or "every pair of GPUs")}
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     C = native()  # fail loudly if the HIP extension is missing
@@ -807,6 +821,7 @@ def main(argv=None) -> int:
 
     gbps = _gbps(wl, K, m["elapsed"])
     ms = m["elapsed"] / K * 1e3
+    topo = _topology(ctx) if dev.type == "cuda" else None  # collective at N > 1 (cached after fused)
     line = None
     if ctx.is_root:
         world1 = ctx.world_size == 1
@@ -872,6 +887,8 @@ def main(argv=None) -> int:
             line["serial_collective"] = collective
         if plan_tuning is not None:
             line["plan_tuning"] = plan_tuning
+        if topo is not None:
+            line["config"]["topology"] = topo
     rc = 0 if verified in (None, True) else 1
     if not watch.finish():
         return 2  # (unreachable: the watchdog ended the process)

@@ -79,6 +79,7 @@ def test_bench_torchrun_one_rank_graphs_both_modes(tmp_path, collective):
     assert combine.startswith("none at world 1")  # the JSON says the combine is a no-op at world 1
     assert ("RCCL" in combine) if collective == "rccl" else ("fused" in combine)
     assert d["native_source_hash"] and d["native_source_hash"] != "unknown"
+    assert d["config"]["topology"] == {"hosts": 1, "gpus": 1, "ranks_per_gpu": 1, "peer_access": "n/a (one GPU)"}
 
 
 def test_bench_fused_two_lanes(tmp_path):
@@ -280,6 +281,8 @@ def test_bench_eight_ranks_auto_on_one_gpu(tmp_path, monkeypatch):
     d = _json(r)
     assert d["verified"] is True and d["n_gpus"] == 8
     assert d["config"]["collective"] == "fused" and d["value"] == d["serial_gbps"] and "reduce_c_vector" in d
+    # peer_map: eight ranks, one physical GPU, nothing to map across devices
+    assert d["config"]["topology"] == {"hosts": 1, "gpus": 1, "ranks_per_gpu": 8, "peer_access": "n/a (one GPU)"}
     ex = d["reduce_c_vector"]
     bad = [t for t in ex["table"] if t.get("verified") is not True]
     assert not bad and len(ex["table"]) == 30, (bad, r.stderr[-2000:])

@@ -129,10 +129,11 @@ $(BUILD)/bin/cpp_consumer: examples/cpp_consumer/main.cpp $(LIB) $(HEADERS)
 UNIT := $(BUILD)/bin/host_unit $(BUILD)/bin/bootstrap_test
 unit: $(UNIT)
 
-$(BUILD)/bin/host_unit: tests/native/host_unit.cpp $(filter-out csrc/apps/reduce_mpi.cpp,$(MPI_SRCS)) $(HEADERS)
+UNIT_SRCS := $(filter-out csrc/apps/reduce_mpi.cpp,$(MPI_SRCS)) csrc/runtime/peer_access.cpp
+$(BUILD)/bin/host_unit: tests/native/host_unit.cpp $(UNIT_SRCS) $(HEADERS)
 	@mkdir -p $(dir $@)
 	g++ $(CXXSTD) -O2 -Wall -Icsrc/include -I$(BUILD)/gen -DMIREDUCE_NO_HIP tests/native/host_unit.cpp \
-	    $(filter-out csrc/apps/reduce_mpi.cpp,$(MPI_SRCS)) -o $@
+	    $(UNIT_SRCS) -o $@
 
 $(BUILD)/bin/bootstrap_test: tests/native/bootstrap_test.cpp $(COMMLIB) $(LIB) $(HEADERS)
 	@mkdir -p $(dir $@)
@@ -146,7 +147,7 @@ asan: csrc/apps/reduce_mpi.cpp
 	    -I$(MPI_HOME)/include $(MPI_SRCS) -static-libstdc++ -static-libgcc $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,$(MPI_HOME)/lib \
 	    -o $(BUILD)/asan/reduce_mpi
 	g++ $(CXXSTD) -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -Icsrc/include -I$(BUILD)/gen -DMIREDUCE_NO_HIP \
-	    tests/native/host_unit.cpp $(filter-out csrc/apps/reduce_mpi.cpp,$(MPI_SRCS)) -o $(BUILD)/asan/host_unit
+	    tests/native/host_unit.cpp $(UNIT_SRCS) -o $(BUILD)/asan/host_unit
 
 # Race detection: the threaded host reference reducers / arg-reductions under
 # ThreadSanitizer (tests/native/race_unit.cpp; exits non-zero on any report).

@@ -42,19 +42,104 @@ import json
 from dataclasses import replace
 import math
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
-import torch
+LAUNCHER_ENV = "MIREDUCE_BENCH_LAUNCHER"  # set by _launch_ranks for its children: "self-spawned"
 
-from cuda_mpi_reductions_amd._native import native, native_path
-from cuda_mpi_reductions_amd.models import CONFIGS, LOC_OPS, NORTH_STAR, scalar_workload
-from cuda_mpi_reductions_amd.ops import KernelConfig
-from cuda_mpi_reductions_amd.parallel import dist as pdist
-from cuda_mpi_reductions_amd.utils.fault import FaultInjector
-from cuda_mpi_reductions_amd.utils.graphs import StepGraph
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch_ranks(argv: list) -> "int | None":
+    """Make ``--gpus N`` mean N ranks however bench.py is started. Runs before anything loads the
+    HIP runtime (no torch, no native extension): this process never touches a GPU.
+
+    * ``WORLD_SIZE`` set (torchrun / the driver started the ranks): it must equal ``--gpus``, else
+      rank 0 prints a diagnostic JSON line and every rank exits with 2 (a mis-launched job must not
+      report a 1-rank number as an N-GPU one). Returns None (run the bench in this process).
+    * ``WORLD_SIZE`` unset and ``--gpus N > 1``: start ``torch.distributed.run`` with N ranks of this
+      same command line as a CHILD process (never exec: a replaced process image is not allowed
+      on the GPU pool), relay nothing (the child inherits stdout / stderr), forward SIGTERM / SIGINT,
+      and return the child's exit status. Each rank records ``launcher: "self-spawned"``.
+    * otherwise (one rank): None.
+
+    Reference: reduce.c reports the rank count it ran with (NODES = commSize, mpi/reduce.c:81,95);
+    the job shape comes from the launcher (mpi/ccni_vn.sh:7)."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    known, _ = pre.parse_known_args(argv)
+    n = known.gpus
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != n:
+            if os.environ.get("RANK", "0") == "0":
+                print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": n, "verified": None,
+                                  "error": f"--gpus {n} but the launcher started WORLD_SIZE={ws} ranks; "
+                                           "refusing to report a measurement for the wrong number of GPUs"}),
+                      flush=True)
+            print(f"[bench] --gpus {n} != WORLD_SIZE {ws}: exiting with 2", file=sys.stderr, flush=True)
+            return 2
+        return None
+    if n <= 1:
+        return None
+    env = dict(os.environ)
+    env[LAUNCHER_ENV] = "self-spawned"
+    # the native TCP bootstrap defaults to MASTER_PORT + 17: give it a port known to be free
+    env.setdefault("MIREDUCE_BOOTSTRAP_PORT", str(_free_port()))
+    master = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(master), os.path.abspath(__file__)] + list(argv)
+    print(f"[bench] --gpus {n} without a launcher: starting {n} ranks under torch.distributed.run",
+          file=sys.stderr, flush=True)
+
+    def _die_with_parent():  # the child must not outlive a killed parent
+        try:
+            import ctypes
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except Exception:  # noqa: BLE001
+            pass
+
+    child = subprocess.Popen(cmd, env=env, preexec_fn=_die_with_parent)
+
+    def _forward(sig, _frame):
+        try:
+            child.send_signal(sig)
+        except ProcessLookupError:
+            pass
+
+    for s in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(s, _forward)
+    while True:
+        try:
+            rc = child.wait()
+            return rc if rc >= 0 else 128 - rc  # killed by a signal: the shell's convention
+        except KeyboardInterrupt:  # forwarded above; keep waiting for the child's status
+            continue
+
 
 METRIC = "reduction bandwidth (GB/s, whole node), 1B-double sum at 1/2/4/8 MI355X"
+
+if __name__ == "__main__":
+    _rc = _launch_ranks(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
+
+import torch  # noqa: E402  (after the launcher: the parent of self-spawned ranks never loads it)
+
+from cuda_mpi_reductions_amd._native import native, native_path  # noqa: E402
+from cuda_mpi_reductions_amd.models import CONFIGS, LOC_OPS, NORTH_STAR, scalar_workload  # noqa: E402
+from cuda_mpi_reductions_amd.ops import KernelConfig  # noqa: E402
+from cuda_mpi_reductions_amd.parallel import dist as pdist  # noqa: E402
+from cuda_mpi_reductions_amd.utils.fault import FaultInjector  # noqa: E402
+from cuda_mpi_reductions_amd.utils.graphs import StepGraph  # noqa: E402
+
 RELEASE_SETTLE_S = 0.5  # idle after handing GB-sized buffers back to the driver, before timing again
 
 
@@ -97,6 +182,9 @@ def parse_args(argv=None):
     p.add_argument("--teardown-deadline", type=float, default=120.0,
                    help="seconds the teardown after the printed line (device sync, process-group destruction) "
                         "may take; past it every rank exits with the headline's status")
+    p.add_argument("--no-decompose", dest="decompose", action="store_false",
+                   help="skip the after-headline decomposition (the same steps without the combine, per rank: "
+                        "local time, skew, exchange cost)")
     p.add_argument("--local-only", action="store_true",
                    help="single rank: skip the cross-rank combine (by default it is issued even at N=1)")
     p.add_argument("--streams", type=int, default=1,
@@ -114,6 +202,11 @@ def parse_args(argv=None):
     p.add_argument("--launch", choices=["auto", "graph", "eager"], default="auto",
                    help="graph: replay the timed steps as captured hipGraphs (chunks of --graph-chunk steps); "
                         "eager: issue every step from Python; auto: graph on GPUs when capturable")
+    p.add_argument("--replay-probe", choices=["auto", "on", "off"], default="auto",
+                   help="before replaying captured collective-issuing headline steps, replay 3 of them under "
+                        "--probe-deadline and fall back to eager issue if any rank fails (auto: when the RCCL "
+                        "combine is captured at N > 1)")
+    p.add_argument("--probe-deadline", type=float, default=20.0, help="seconds the replay probe may take")
     p.add_argument("--graph-chunk", type=int, default=0,
                    help="steps per captured graph (each graph ends by joining its lanes / last all-reduce, so "
                         "fewer, longer graphs leave fewer bubbles); 0 = auto: every timed step in one graph "
@@ -139,6 +232,22 @@ def parse_args(argv=None):
 def _sync(dev: torch.device) -> None:
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
+
+
+def _ranks_seen(ctx) -> int:
+    """How many ranks the job's collective backend actually joined: an all-reduce of a one from
+    every rank over the default process group (RCCL on GPUs; gloo in CPU rehearsals)."""
+    t = torch.ones(1, dtype=torch.int64, device=ctx.device if ctx.backend == "nccl" else "cpu")
+    if torch.distributed.is_initialized():
+        torch.distributed.all_reduce(t)
+    return int(t.item())
+
+
+def _launch_record(ctx, seen: int) -> dict:
+    """JSON fields that prove the job's shape: who started the ranks and how many the collective saw."""
+    launcher = os.environ.get(LAUNCHER_ENV) or ("external" if "WORLD_SIZE" in os.environ else "single process")
+    return {"launcher": launcher, "ranks_seen": seen, "ranks_seen_backend": ctx.backend,
+            "rccl_ranks_seen": seen if ctx.backend == "nccl" else None}
 
 
 def _time_torch_reduction(wl, K: int, W: int, ctx) -> float:
@@ -221,6 +330,9 @@ def run_vector(args, ctx, cfg, fault) -> int:
     dev = ctx.device
     elapsed, verified = _time_vector(wl, ctx, args.steps, args.warmup, fault, not args.no_verify)
     gib = wl.bytes_total * args.steps / elapsed / float(1 << 30)
+    seen = _ranks_seen(ctx)
+    if seen != ctx.world_size:
+        verified = False
     if ctx.is_root:
         print(json.dumps({
             "metric": f"MPI_Reduce-style element-wise {cfg.collective} bandwidth (GiB/s of total data, reduce.c units)",
@@ -236,6 +348,7 @@ def run_vector(args, ctx, cfg, fault) -> int:
             "baseline_value": cfg.baseline, "baseline_unit": cfg.baseline_unit if cfg.baseline else None,
             "baseline_source": cfg.baseline_source or None,
             "verified": verified,
+            **_launch_record(ctx, seen),
         }), flush=True)
     return 0 if verified in (None, True) else 1
 
@@ -445,13 +558,16 @@ def _graph_chunk(requested: int, steps: int, issues_collective: bool) -> int:
 
 
 def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph: bool = True,
-             steps: "int | None" = None, site: str = "step") -> dict:
-    """Time K steps (after ``warmup`` eager steps); returns elapsed (MAX over ranks), the launch
-    mode and how many slots the timed steps wrote (graph replays rewrite the first chunk). ``site``:
-    the fault-injection site of these steps (``step`` = the headline, ``extras`` = a candidate)."""
+             steps: "int | None" = None, site: str = "step", step_fn=None) -> dict:
+    """Time K steps (after ``warmup`` eager steps); returns elapsed (MAX over ranks; ``elapsed_min``:
+    the fastest rank's), the launch mode and how many slots the timed steps wrote (graph replays
+    rewrite the first chunk). ``site``: the fault-injection site of these steps (``step`` = the
+    headline, ``extras`` = a candidate). ``step_fn`` (default ``wl.step``): what one step enqueues."""
     C = native()
     dev = ctx.device
     K = args.steps if steps is None else steps
+    step = step_fn or wl.step
+    issues_collective = wl.issues_collective and step_fn is None
 
     def run(first: int, count: int):
         works = []
@@ -459,7 +575,7 @@ def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph
         for i in range(first, first + count):
             C.trace_push("bench.step")
             corrupt = fault.at(ctx.rank, i, site, f"bench {site}")
-            w = wl.step(slots[i:i + 1], async_op=True, corrupt=corrupt)
+            w = step(slots[i:i + 1], async_op=True, corrupt=corrupt)
             C.trace_pop()
             if w is not None:
                 if serial:
@@ -474,24 +590,40 @@ def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph
     launch, sg = "eager", None
     armed = fault.on(site)
     capturable = dev.type == "cuda" and not args.trace and not armed and \
-        (not wl.issues_collective or ctx.backend == "nccl")
+        (not issues_collective or ctx.backend == "nccl")
+    # The headline's captured collectives get a short replay probe first (--replay-probe)
+    probe = site == "step" and (args.replay_probe == "on" or (
+        args.replay_probe == "auto" and issues_collective and ctx.world_size > 1))
     if allow_graph and ((args.launch == "graph" and not armed) or (args.launch == "auto" and capturable)):
         # Capture the K timed steps as graph replays of --graph-chunk-step chunks (all ranks agree
         # on success or all fall back to eager issue); one untimed replay uploads the graphs.
         W = warmup
-        sg = StepGraph(lambda j: wl.step(slots[W + j:W + j + 1], async_op=True), K, dev,
-                       chunk=_graph_chunk(args.graph_chunk, K, wl.issues_collective), serial=serial,
+        sg = StepGraph(lambda j: step(slots[W + j:W + j + 1], async_op=True), K, dev,
+                       chunk=_graph_chunk(args.graph_chunk, K, issues_collective), serial=serial,
                        fork=wl.fork, join=wl.join)
         # (kernel-only steps keep the NCCL stream out of the capture: no watchdog settle needed)
-        if sg.capture(group_agree=ctx.world_size > 1, settle_s=None if wl.issues_collective else 0.0):
+        if sg.capture(group_agree=ctx.world_size > 1, settle_s=None if issues_collective else 0.0):
             launch = f"graph (chunk {sg.chunk}, {sg.reps} replays" + (f" + 1 of {sg.rem})" if sg.rem else ")")
-            for g in sg.graphs:
-                g.replay()
+            perr = _replay_probe(wl, ctx, args, fault, serial, step, capture=True) if probe else None
+            if perr is not None:
+                sg.reset()
+                sg = None
+                launch = f"eager (captured replay probe failed: {perr})"
+                if ctx.is_root:
+                    print(f"[bench] {launch}", file=sys.stderr)
+            else:
+                if probe:
+                    launch += "; replay probe ok"
+                for g in sg.graphs:
+                    g.replay()
         else:
             launch = f"eager (graph capture failed: {sg.error})"
             if ctx.is_root:
                 print(f"[bench] {launch}", file=sys.stderr)
             sg = None
+    elif probe:  # no graphs here (CPU rehearsal, --launch eager): the same probe over eager steps
+        perr = _replay_probe(wl, ctx, args, fault, serial, step, capture=False)
+        launch = f"eager (replay probe failed: {perr})" if perr else "eager; replay probe ok"
     _sync(dev)
     pdist.barrier(ctx)
     _sync(dev)
@@ -504,10 +636,68 @@ def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph
     t1 = time.perf_counter()
     pdist.barrier(ctx)
     elapsed = pdist.max_over_ranks(t1 - t0, ctx)
+    fastest = -pdist.max_over_ranks(-(t1 - t0), ctx)
     written = warmup + (sg.chunk if sg is not None else K)
     if sg is not None:
         sg.reset()  # captured RCCL work must not outlive the communicator
-    return {"elapsed": elapsed, "launch": launch, "written": written}
+    return {"elapsed": elapsed, "elapsed_min": fastest, "launch": launch, "written": written}
+
+
+def _replay_probe(wl, ctx, args, fault, serial: bool, step, capture: bool) -> "str | None":
+    """Before the headline replays captured collective-issuing steps (the RCCL combine at N > 1,
+    used when the fused finish was declined): capture 3 such steps, replay them once and poll for
+    completion for at most ``--probe-deadline`` seconds; the verdict is agreed over ranks. Any
+    failure (capture error, replay error, late completion on any rank) makes the headline issue its
+    steps eagerly, and the JSON's ``launch`` says why — a problem of the captured path must not cost
+    the number. A replay that NEVER completes cannot be recovered in-process (its stream is stuck
+    behind a spinning collective kernel): the headline deadline then ends the run with rc 2 and a
+    diagnostic line. Without graphs (``capture=False``: CPU rehearsals) 3 eager steps are probed
+    under the same rules. Fault site ``capture`` (STEP ignored) fires inside the probe's clock.
+    Reference: every reduction is timed to completion and none may be lost (reduction.cpp:319-374)."""
+    dev = ctx.device
+    deadline = args.probe_deadline
+    slots = wl.new_slots(3)
+    err, pg, done = None, None, True
+    try:
+        if capture:
+            pg = StepGraph(lambda j: step(slots[j:j + 1], async_op=True), 3, dev, chunk=3, serial=serial,
+                           fork=wl.fork, join=wl.join)
+            if not pg.capture(group_agree=ctx.world_size > 1):
+                err, pg = f"capture: {pg.error}", None
+        if err is None:
+            t0 = time.perf_counter()
+            fault.at(ctx.rank, fault.spec.step, "capture", "replay probe")
+            if pg is not None:
+                pg.run()
+                ev = torch.cuda.Event()
+                ev.record()
+                while not ev.query() and time.perf_counter() - t0 <= deadline:
+                    time.sleep(0.0005)
+                done = ev.query()
+            else:
+                for j in range(3):
+                    w = step(slots[j:j + 1], async_op=True)
+                    if w is not None:
+                        w.wait()
+                _sync(dev)
+            el = time.perf_counter() - t0
+            if not done:
+                err = f"3 replayed steps not complete after {deadline:g} s"
+            elif el > deadline:
+                err = f"3 steps took {el:.1f} s (deadline {deadline:g} s)"
+    except Exception as e:  # noqa: BLE001 - recorded; the headline falls back to eager issue
+        err = f"{type(e).__name__}: {e}"[:200]
+    failed = pdist.max_over_ranks(1.0 if err else 0.0, ctx) > 0.5  # (waits for a stuck rank's stream)
+    if pg is not None:
+        _sync(dev)
+        pg.reset()
+    if not failed:
+        return None
+    errs = [err]
+    if ctx.world_size > 1:
+        errs = [None] * ctx.world_size
+        torch.distributed.all_gather_object(errs, err)
+    return "; ".join(f"rank {r}: {m}" for r, m in enumerate(errs) if m)[:300] or "failed on another rank"
 
 
 def _try_fused(wl, ctx) -> "str | None":
@@ -689,6 +879,41 @@ def _candidates(wl, ctx, args, fault, fused_ok: bool, capture_failed: bool = Fal
     return out
 
 
+def _decompose(wl, ctx, args, fault, headline_ms: float) -> dict:
+    """Where the N-GPU step's time goes (an extra, measured after the line is final): the same
+    serial, graph-replayed steps with the combine removed (``wl.local_step``: the same kernel plan,
+    no channel, no collective), timed per rank.
+
+    * ``local_ms_per_step``: the slowest rank's local time per step (= ``local_ms_max``);
+      ``local_ms_min``: the fastest rank's; their difference is the inter-GPU skew of the local work;
+    * ``local_gbps``: bytes per step / slowest local time (the node rate if combining were free);
+    * ``exchange_us_per_step``: headline ms/step - slowest local ms/step: the cross-rank combine's
+      round trip plus the per-step skew it exposes (each combine waits for the slowest rank);
+    * ``scaling_efficiency_vs_local``: value / (N x the slowest rank's local rate) — how much of the
+      local reduction rate survives the combine (1.0 = combining is free). Not the N-vs-1 scaling
+      efficiency, which tools/scaling.py computes from the per-N headline values.
+
+    Reference shape: whole-node GB/s = bytes / max over ranks (t_local + t_combine) (SURVEY §5.8;
+    simpleMPI.cpp:92-98: local reduce, then the combine)."""
+    K, W = args.steps, min(args.warmup, 2)
+    slots = wl.new_slots(W + K)
+    m = _measure(wl, slots, ctx, args, fault, serial=True, warmup=W, site="extras", step_fn=wl.local_step)
+    written = slots[:m["written"]]
+    same = bool((written == written[-1]).all().item()) if written.numel() else True
+    same = -pdist.max_over_ranks(-float(same), ctx) > 0.5  # every slot holds this rank's partial
+    err = wl.check()
+    loc_max, loc_min = m["elapsed"] / K * 1e3, m["elapsed_min"] / K * 1e3
+    out = {"local_ms_per_step": round(loc_max, 5), "local_ms_min": round(loc_min, 5), "local_ms_max": round(loc_max, 5),
+           "local_gbps": round(wl.bytes_total / (loc_max * 1e-3) / 1e9, 3),
+           "skew_us_per_step": round((loc_max - loc_min) * 1e3, 3),
+           "exchange_us_per_step": round((headline_ms - loc_max) * 1e3, 3),
+           "scaling_efficiency_vs_local": round(loc_max / headline_ms, 5) if headline_ms > 0 else None,
+           "local_launch": m["launch"], "steps": K, "consistent": same and err is None}
+    if err:
+        out["error"] = err
+    return out
+
+
 def _tune_plan(wl, ctx, args, fault, kernel, cands) -> "tuple[KernelConfig, dict]":
     """Streaming-kernel plan for this shard: the tuned default against the runners-up
     (profiles/r2_plan/), each measured with the headline protocol (one lane, fused finish, serial,
@@ -718,6 +943,8 @@ def _topology(ctx) -> dict:
     """Where the ranks ran (parallel/topology.py peer_map): hosts, physical GPUs, ranks per GPU and
     the agreed peer-access verdict of the IPC-mapped paths (collective at N > 1)."""
     from cuda_mpi_reductions_amd.parallel.topology import peer_map
+    # (peer_map enters its gathers on every rank even when this rank's device query fails, so an
+    # exception here is raised on every rank alike, after the collectives)
     try:
         pm = peer_map(ctx.device.index if ctx.device.index is not None else torch.cuda.current_device())
     except Exception as e:  # noqa: BLE001 - a record field must never cost the headline
@@ -739,9 +966,12 @@ def main(argv=None) -> int:
     fault = FaultInjector.from_flag_or_env(args.inject_fault)
     ctx = pdist.init(backend=None if args.backend == "auto" else args.backend, device_type=device_type,
                      timeout_s=args.pg_timeout)
-    if args.gpus != ctx.world_size and ctx.is_root:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}; using {ctx.world_size}",
-              file=sys.stderr)
+    if args.gpus != ctx.world_size:  # (main() called directly; the __main__ launcher checks this first)
+        if ctx.is_root:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": args.gpus, "verified": None,
+                              "error": f"--gpus {args.gpus} but WORLD_SIZE={ctx.world_size}"}), flush=True)
+        pdist.shutdown(ctx)
+        return 2
     cfg = CONFIGS[args.config]
     if args.elements is not None:
         cfg = replace(cfg, n_total=args.elements)
@@ -807,6 +1037,9 @@ def main(argv=None) -> int:
     m_lanes = len(wl.lanes) if wl.lanes else 1
     m_issues = wl.issues_collective
     err = wl.check()  # device error words (fan-in, fused finish), agreed over ranks
+    seen = _ranks_seen(ctx)
+    if seen != ctx.world_size:
+        err = (err + "; " if err else "") + f"the process group joined {seen} ranks, not {ctx.world_size}"
     stage["now"] = "verification"
     verified = None
     if not args.no_verify:
@@ -877,6 +1110,7 @@ def main(argv=None) -> int:
             "verified": verified,
             "native_ext": os.path.basename(native_path()),
             "native_source_hash": C.source_hash(),
+            **_launch_record(ctx, seen),
         }
         if err is not None:
             line["device_error"] = err
@@ -901,6 +1135,12 @@ def main(argv=None) -> int:
     guard = _ExtrasWatchdog(line, args.extras_deadline, rc, partial=extras)
     run_cands = args.candidates and dev.type == "cuda" and hasattr(wl, "use_collective") and not args.pipelined
     cap_failed = m["launch"].startswith("eager (graph capture failed")
+    if args.decompose and not args.pipelined and hasattr(wl, "local_step"):  # kernels only: cheap, first
+        try:
+            extras["decomposition"] = _decompose(wl, ctx, args, fault, ms)
+        except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
+            extras["decomposition"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+            print(f"[bench] rank {ctx.rank}: decomposition failed: {e}", file=sys.stderr)
     if run_cands:  # the fused (kernel-only) candidate first: before the torch-heavy extras below
         extras["candidates"] = _candidates(wl, ctx, args, fault, collective == "fused", cap_failed, which="fused")
     if args.vector_extras and dev.type == "cuda" and cfg.name == NORTH_STAR:
@@ -918,7 +1158,7 @@ def main(argv=None) -> int:
             pipe = [v["gbps"] for k, v in cands.items() if k.endswith("pipelined") and v.get("gbps")]
             line["pipelined_gbps"] = max(pipe) if pipe else None
             line["rccl_serial_gbps"] = cands.get("rccl_serial", {}).get("gbps")
-        for k in ("torch_gbps", "reduce_c_vector"):
+        for k in ("torch_gbps", "reduce_c_vector", "decomposition"):
             if k in extras:
                 line[k] = extras[k]
         print(json.dumps(line), flush=True)

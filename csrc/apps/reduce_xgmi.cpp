@@ -36,6 +36,7 @@
 #include "mireduce/cpu_reference.hpp"
 #include "mireduce/device.hpp"
 #include "mireduce/direct.hpp"
+#include "mireduce/peer_access.hpp"
 #include "mireduce/fault.hpp"
 #include "mireduce/ladder.hpp"
 #include "mireduce/mt19937.hpp"
@@ -580,7 +581,8 @@ void usage() {
       "  --json=PATH  --noverify  --seed=N  --block= --unroll= --wg-per-cu= --policy=auto|nt|default\n"
       "  --timeout=S                  RCCL wait deadline / direct kernels' device-side wait bound (s);\n"
       "                               bootstrap: MIREDUCE_BOOTSTRAP_TIMEOUT\n"
-      "  --inject-fault=KIND[@RANK][:STEP]  exit|hang|corrupt|delay=<ms> at a timed collective (tests)\n"
+      "  --inject-fault=KIND[@RANK][:STEP]  exit|hang|corrupt|delay=<ms> at a timed collective (tests);\n"
+      "                               nopeer: RANK's peer-access preflight says no (fused/direct decline)\n"
       "launch: torchrun --nproc-per-node=8 --master-addr 127.0.0.1 ... | mpirun -np 8 ...\n");
 }
 
@@ -714,6 +716,13 @@ int main(int argc, char** argv) {
     if (!needs_no_rccl(c)) {  // direct / fused need no RCCL (and may share one GPU between ranks)
       c.comm = std::make_unique<RcclComm>(*c.boot, c.device);
       install_comm_abort_hook(c.comm.get());
+    } else {
+      // The IPC-mapped paths store to / load from peers' memory from inside kernels: agree that
+      // every pair of GPUs can map each other BEFORE any handle is opened, and decline on every
+      // rank together otherwise (simpleP2P.cu:250-275 checks the same before enabling anything).
+      const std::string why = peer_preflight(*c.boot, c.device, &c.fault);
+      if (!why.empty())
+        throw Error("--collective=" + c.collective + " needs peer access between every pair of GPUs: " + why);
     }
     if (c.env.rank == 0) {
       DeviceInfo di = device_info(c.device);

@@ -12,6 +12,8 @@
 //   hang     the rank stops making progress (sleeps; killed by the launcher or a deadline)
 //   corrupt  at() returns true once: the caller perturbs its local result (verification must fail)
 //   delay    the rank sleeps <ms> once (a straggler; results stay correct)
+//   nopeer   the rank's peer-access query answers "no" for every peer device (the IPC-mapped
+//            paths must then decline on every rank before mapping anything; STEP ignored)
 #pragma once
 
 #include <string>
@@ -19,7 +21,7 @@
 namespace mireduce {
 
 struct FaultSpec {
-  enum class Kind { None, Exit, Hang, Corrupt, Delay };
+  enum class Kind { None, Exit, Hang, Corrupt, Delay, NoPeer };
   Kind kind = Kind::None;
   int rank = 1;
   long step = 0;
@@ -40,6 +42,8 @@ class FaultInjector {
   // Call at each numbered step; fires once when (rank, step) match. Returns true iff the caller
   // must corrupt its local result now. `site` names the call site in the log line.
   bool at(int rank, long step, const char* site);
+  // Whether `rank` must report no peer access (Kind::NoPeer; every query, not once).
+  bool no_peer(int rank) const { return spec_.kind == FaultSpec::Kind::NoPeer && rank == spec_.rank; }
 
  private:
   FaultSpec spec_;

@@ -88,7 +88,8 @@ class Workspace {
   unsigned* fan() const { return fan_; }
   // Sticky error of the polled fan-in (synchronous read: call after the launches completed).
   // Non-zero: some launch's finisher reached its wait bound; that launch and every later one
-  // wrote a poisoned result (NaN, or the identity for integers) until reset().
+  // wrote a poisoned result (NaN, or the operator's identity for integers — for which this word,
+  // not the value, is the signal) until reset().
   unsigned error() const;
   // Re-zero the tickets, fan-in slots and the sticky error (after an error or an aborted launch;
   // stream-ordered: no launch on this workspace may be running on another stream).
@@ -116,8 +117,22 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
 // Enqueue a full reduction of n elements at device pointer `in` into out[0] (device pointer,
 // element type `acc`). Asynchronous on `stream`; safe to capture into a hipGraph.
 // Throws mireduce::Error on invalid arguments.
+// Error state: a launch whose fan-in (or fused cross-rank finish) failed writes a poisoned value —
+// NaN for floating accumulators, the operator's IDENTITY for integers (no in-range integer can
+// signal an error, and the identity stays neutral in a later cross-rank fold) — and sets a sticky
+// error word. The value therefore does not tell an integer caller anything: read the word
+// (Workspace::error() after the stream completed, XrankChannel::error() for the fused finish), or
+// use reduce_checked() below.
 LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
                   hipStream_t stream, const ReduceConfig& cfg = {});
+
+// Synchronous form: reduce(), wait for `stream`, and return the error state of this and every
+// earlier launch on `ws` since its last reset(): 0 = out[0] is valid; bit 0 = the polled fan-in
+// reached its wait bound; bits 8.. = the fused finish's channel error (<< 8: 1 a peer's partial
+// timed out, 2 a peer pushed a poisoned partial). Non-zero: out[0] is poisoned; reset() the
+// workspace (and XrankChannel::clear_error()) before relying on later launches.
+unsigned reduce_checked(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
+                        hipStream_t stream, const ReduceConfig& cfg = {}, LaunchPlan* plan = nullptr);
 
 // A reduction whose plan, kernel variant and arguments are resolved once. launch() is a single
 // kernel launch (plus the finalize launch in two-pass mode) with no planning or argument

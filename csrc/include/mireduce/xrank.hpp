@@ -20,7 +20,11 @@
 // without host involvement; the mailbox is double-buffered by epoch parity (a rank can run at
 // most one epoch ahead of the slowest peer: it needs that peer's partial to finish). A poll that
 // exceeds `timeout` sets a sticky error word instead of hanging (later launches then do not wait),
-// which XrankChannel::error() reports.
+// which XrankChannel::error() reports. A rank whose own fan-in failed pushes its partial with a
+// poison flag in the tag; its peers then set error bit 2 and poison their results too, so the
+// failure is visible on every rank (integers are poisoned to the operator's identity, so the
+// error word is their only signal). Epochs are 31 bits (the 32nd tag bit is the flag) and wrap
+// keeping their parity.
 //
 // Every rank must launch the bound reductions of a channel in the same order; one channel per
 // concurrently running reduction (stream lane).
@@ -44,7 +48,8 @@ struct XrankDesc {
   uint64_t* peer_mbox[kMaxXrankRanks];  // rank p's mailbox as mapped in this process ([rank] = own)
   uint64_t* own_mbox;
   unsigned* epoch;          // finished launches on this channel
-  unsigned* error;          // sticky: 1 = a peer's partial missed the timeout
+  unsigned* error;          // sticky bits: 1 = a peer's partial missed the timeout,
+                            // 2 = a peer pushed a poisoned partial (its own fan-in failed)
   int rank;
   int world;
   uint64_t timeout_ticks;   // wall_clock64() ticks

@@ -335,12 +335,30 @@ LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out
   a.flat = p.flat ? 1 : 0;
   a.slots = p.poll ? ws.slots() : nullptr;
   a.fan = ws.fan();
+  a.fan_slots = static_cast<unsigned>(ws.max_grid());
   a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
   const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][body_index(p)];
   fn(a, p.grid, stream);
   MIREDUCE_HIP_THROW(hipGetLastError());
   if (!p.single_pass) reduce_finalize(ws.partials(), p.grid, acc, op, out, stream);
   return p;
+}
+
+unsigned reduce_checked(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
+                        hipStream_t stream, const ReduceConfig& cfg, LaunchPlan* plan) {
+  const LaunchPlan p = reduce(in, n, t, op, acc, out, ws, stream, cfg);
+  if (plan) *plan = p;
+  MIREDUCE_HIP_THROW(hipStreamSynchronize(stream));
+  unsigned err = ws.error();
+  if (cfg.xrank) {  // the fused finish's own error word (a peer's partial late or poisoned)
+    unsigned xe = 0;
+    const auto* d = static_cast<const XrankDesc*>(cfg.xrank);
+    unsigned* word = nullptr;
+    MIREDUCE_HIP_THROW(hipMemcpy(&word, &d->error, sizeof word, hipMemcpyDeviceToHost));
+    MIREDUCE_HIP_THROW(hipMemcpy(&xe, word, sizeof xe, hipMemcpyDeviceToHost));
+    err |= xe << 8;
+  }
+  return err;
 }
 
 struct BoundReduce::Impl {
@@ -368,6 +386,7 @@ BoundReduce::BoundReduce(const void* in, size_t n, DType t, Op op, DType acc, vo
   a.flat = p.flat ? 1 : 0;
   a.slots = p.poll ? ws.slots() : nullptr;
   a.fan = ws.fan();
+  a.fan_slots = static_cast<unsigned>(ws.max_grid());
   a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
   impl_ = new Impl{a, table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][body_index(p)],
                    p, op, acc, &ws};

@@ -82,6 +82,7 @@ struct Args {
   uint64_t* slots;         // non-null: polled fan-in (no tickets), [gridDim.x][2] epoch-tagged words
   unsigned* fan;           // polled fan-in state (Workspace): [0] epoch = finished launches, [1] sticky error
   uint64_t fan_bound;      // polled fan-in: finisher's wait bound in wall-clock ticks
+  unsigned fan_slots;      // polled fan-in: slots in the workspace (all zeroed when the epoch wraps)
   int balance;             // 1 (interleaved split): whole rounds of tiles, then the leftover < grid
                            // tiles split evenly over ALL workgroups (no one-tile tail on a few)
   int delay_wg;            // test hook (ReduceConfig::debug_delay_wg): this workgroup sleeps
@@ -92,15 +93,21 @@ struct Args {
 // epoch is this launch's number (Workspace fan[0] + 1, read by every workgroup at its start and
 // advanced by the finisher after it has consumed every slot): a slot is valid for exactly one
 // launch, so nothing needs clearing, and a late store from an earlier (timed-out) launch never
-// matches. Reaching the bound sets the sticky error fan[1] and poisons the result (NaN / identity)
-// instead of folding unpublished slots; Workspace::error() reports it, Workspace::reset() clears it.
+// matches. Reaching the bound sets the sticky error fan[1] and poisons the result instead of
+// folding unpublished slots; Workspace::error() reports it, Workspace::reset() clears it.
+// The epoch is 32 bits: when it wraps (every 2^32 launches of one workspace) the finisher first
+// zeroes every slot of the workspace (Args::fan_slots), so a slot last written a whole cycle ago —
+// beyond the grid of the launches since — cannot carry the new cycle's tag.
 constexpr int kPollSlots = 4;  // slots one finisher lane polls per round (grid <= 4 x BLOCK)
 constexpr uint64_t kFanBoundTicks = 1ull << 30;  // ~10.7 s of the 100 MHz wall clock
 
-template <class AccT>
+// The value a launch writes when its fan-in or cross-rank finish failed: NaN for floating types;
+// for integers no in-range value can signal an error, so they get the operator's identity — neutral
+// in any later fold — and the error WORDS (Workspace::error(), XrankChannel::error()) are the signal.
+template <class OpT, class AccT>
 __device__ __forceinline__ AccT poisoned() {
   if constexpr (std::is_floating_point_v<AccT>) return __builtin_nan("");
-  else return AccT(0);
+  else return OpT::template identity<AccT>();
 }
 
 template <class T>
@@ -131,6 +138,22 @@ __device__ __forceinline__ T from_bits64(uint64_t b) {
 // The descriptor fields a lane needs are read by xrank_prefetch: in the polled fan-in the
 // finisher is known up front and issues these loads before it waits for the other workgroups'
 // partials, so their latency (a descriptor miss, ~0.5 us at N=1) is off the critical path.
+// Mailbox word tags: a 31-bit epoch plus the poison flag (bit 63 of the word): a rank whose own
+// result is poisoned pushes its (neutral) partial with the flag set, and every peer that folds it
+// sets error bit 2 on its own channel and poisons its result too — a failure on one rank is never
+// a plausible-looking value on another.
+constexpr unsigned kXrankEpochMask = 0x7fffffffu;
+constexpr uint64_t kXrankPoisonBit = 1ull << 63;
+constexpr unsigned kXrankErrTimeout = 1u;    // a peer's partial missed the timeout
+constexpr unsigned kXrankErrPeerPoison = 2u; // a peer pushed a poisoned partial
+
+// Next launch's epoch from the channel counter: 31 bits, 0 skipped (a zeroed mailbox word) and the
+// parity kept alternating across the wrap (0x7fffffff -> 2), which the double buffer relies on.
+__device__ __forceinline__ unsigned xrank_next_epoch(unsigned cur) {
+  const unsigned e = (cur + 1u) & kXrankEpochMask;
+  return e ? e : 2u;
+}
+
 struct XrankLane {
   uint64_t* peer;       // rank `lane`'s mailbox (lane < world, lane != rank)
   const uint64_t* own;  // this rank's mailbox
@@ -151,14 +174,19 @@ __device__ __forceinline__ XrankLane xrank_prefetch(const XrankDesc* d, unsigned
   return x;
 }
 
+// `poison`: this rank's partial `t` is already poisoned (its fan-in failed): it is pushed with the
+// poison flag. `failed` (wave-uniform) returns whether this launch's global value is unusable: a
+// peer's partial missed the timeout or arrived poisoned (the caller then writes poisoned<>()).
 template <class OpT, class AccT>
-__device__ __forceinline__ AccT xrank_finish(const XrankDesc* d, const XrankLane& x, AccT t) {
+__device__ __forceinline__ AccT xrank_finish(const XrankDesc* d, const XrankLane& x, AccT t, bool poison,
+                                             bool& failed) {
   const int lane = threadIdx.x & 63;
   const unsigned e = x.e;
   const uint64_t parity = static_cast<uint64_t>(e & 1u) * kMaxXrankRanks;
-  const uint64_t tag = static_cast<uint64_t>(e) << 32;
+  const uint64_t tag = (static_cast<uint64_t>(e) << 32) | (poison ? kXrankPoisonBit : 0ull);
   const uint64_t bits = to_bits64(t);
   AccT v = OpT::template identity<AccT>();
+  bool bad = false;
   if (lane < x.world && lane != x.rank) {
     uint64_t* dst = x.peer + (parity + x.rank) * 2;
     __hip_atomic_store(dst, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -168,12 +196,17 @@ __device__ __forceinline__ AccT xrank_finish(const XrankDesc* d, const XrankLane
     for (;;) {
       const uint64_t lo = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       const uint64_t hi = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if ((lo >> 32) == e && (hi >> 32) == e) {
+      if (((lo >> 32) & kXrankEpochMask) == e && ((hi >> 32) & kXrankEpochMask) == e) {
         v = from_bits64<AccT>((lo & 0xffffffffull) | (hi << 32));
+        if ((lo | hi) & kXrankPoisonBit) {
+          __hip_atomic_fetch_or(d->error, kXrankErrPeerPoison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          bad = true;
+        }
         break;
       }
       if (static_cast<uint64_t>(wall_clock64()) - t0 > x.limit) {
-        __hip_atomic_fetch_or(d->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_or(d->error, kXrankErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bad = true;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -182,6 +215,7 @@ __device__ __forceinline__ AccT xrank_finish(const XrankDesc* d, const XrankLane
     v = t;  // this rank's own partial never leaves the register file
   }
   if (lane == 0) __hip_atomic_store(d->epoch, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  failed = __ballot(bad) != 0;
   return wave_reduce<OpT>(v);
 }
 
@@ -375,7 +409,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   // body — 76 -> 60 VGPRs and 7.3 -> 5.1 TB/s at 512 x 16) so the finisher pays no atomic round trip.
   unsigned xr_epoch = 0, xr_err = 0;
   if (a.xrank) {
-    xr_epoch = __hip_atomic_load(a.xrank->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    xr_epoch = xrank_next_epoch(__hip_atomic_load(a.xrank->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     xr_err = __hip_atomic_load(a.xrank->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
@@ -390,8 +424,9 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   //      no tickets, no second load round.
   if (gridDim.x == 1) {
     if (threadIdx.x < 64) {
-      if (a.xrank) v = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), v);
-      if (threadIdx.x == 0) *static_cast<AccT*>(a.out) = v;
+      bool xf = false;
+      if (a.xrank) v = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), v, false, xf);
+      if (threadIdx.x == 0) *static_cast<AccT*>(a.out) = xf ? poisoned<OpT, AccT>() : v;
     }
     return;
   }
@@ -482,10 +517,17 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     // Any lane past the bound (or an earlier launch's sticky error) poisons this launch's result.
     const bool bad = __syncthreads_or(late) || fan_err != 0;
     t = block_reduce<OpT, AccT, BLOCK>(t, lds);
+    if (fan_e == 0xffffffffu) {  // the epoch wraps after this launch: invalidate every slot first
+      __syncthreads();
+      for (unsigned i = threadIdx.x; i < 2u * a.fan_slots; i += BLOCK)
+        __hip_atomic_store(a.slots + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+    }
     if (threadIdx.x < 64) {
-      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xl, bad ? poisoned<AccT>() : t);
+      bool xf = false;
+      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xl, bad ? poisoned<OpT, AccT>() : t, bad, xf);
       if (threadIdx.x == 0) {
-        *static_cast<AccT*>(a.out) = bad ? poisoned<AccT>() : t;
+        *static_cast<AccT*>(a.out) = (bad || xf) ? poisoned<OpT, AccT>() : t;
         if (bad) __hip_atomic_fetch_or(a.fan + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // every slot of this launch has been read (or abandoned): the next launch's epoch
         __hip_atomic_store(a.fan, fan_e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -535,9 +577,10 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     for (unsigned i = threadIdx.x; i < gridDim.x; i += BLOCK) t = OpT::apply(t, load_sc1(&partials[i]));
     t = block_reduce<OpT, AccT, BLOCK>(t, lds);
     if (threadIdx.x < 64) {
-      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), t);
+      bool xf = false;
+      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), t, false, xf);
       if (threadIdx.x == 0) {
-        *static_cast<AccT*>(a.out) = t;
+        *static_cast<AccT*>(a.out) = xf ? poisoned<OpT, AccT>() : t;
         // reset: the top counter, or (one group) the group counter itself
         __hip_atomic_store(&a.tickets[(G > 1 ? G : 0) * kTicketStride], 0u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -567,9 +610,10 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     const int lane = threadIdx.x;
     AccT t = lane < static_cast<int>(G) ? load_sc1(&gpart[lane]) : OpT::template identity<AccT>();
     t = wave_reduce<OpT>(t);
-    if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), t);
+    bool xf = false;
+    if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), t, false, xf);
     if (lane == 0) {
-      *static_cast<AccT*>(a.out) = t;
+      *static_cast<AccT*>(a.out) = xf ? poisoned<OpT, AccT>() : t;
       __hip_atomic_store(&a.tickets[G * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

@@ -40,11 +40,12 @@ FaultSpec parse_fault_spec(const std::string& spec) {
   if (kind == "exit") f.kind = FaultSpec::Kind::Exit;
   else if (kind == "hang") f.kind = FaultSpec::Kind::Hang;
   else if (kind == "corrupt") f.kind = FaultSpec::Kind::Corrupt;
+  else if (kind == "nopeer") f.kind = FaultSpec::Kind::NoPeer;
   else if (kind.rfind("delay=", 0) == 0) {
     f.kind = FaultSpec::Kind::Delay;
     f.delay_ms = static_cast<int>(to_long(kind.substr(6), spec));
   } else {
-    throw std::invalid_argument("bad fault spec '" + spec + "': kind must be exit, hang, corrupt or delay=<ms>");
+    throw std::invalid_argument("bad fault spec '" + spec + "': kind must be exit, hang, corrupt, delay=<ms> or nopeer");
   }
   if (at != std::string::npos) f.rank = static_cast<int>(to_long(rank, spec));
   if (colon != std::string::npos) f.step = to_long(step, spec);
@@ -58,7 +59,9 @@ FaultInjector FaultInjector::from_flag_or_env(const std::string& flag) {
 }
 
 bool FaultInjector::at(int rank, long step, const char* site) {
-  if (fired_ || spec_.kind == FaultSpec::Kind::None || rank != spec_.rank || step != spec_.step) return false;
+  if (fired_ || spec_.kind == FaultSpec::Kind::None || spec_.kind == FaultSpec::Kind::NoPeer || rank != spec_.rank ||
+      step != spec_.step)
+    return false;
   fired_ = true;
   switch (spec_.kind) {
     case FaultSpec::Kind::Exit:
@@ -77,6 +80,7 @@ bool FaultInjector::at(int rank, long step, const char* site) {
     case FaultSpec::Kind::Corrupt:
       std::fprintf(stderr, "[fault] rank %d corrupts its result at %s step %ld\n", rank, site, step);
       return true;
+    case FaultSpec::Kind::NoPeer:  // not a step fault (no_peer())
     case FaultSpec::Kind::None:
       break;
   }

@@ -168,6 +168,7 @@ class ScalarReduction:
         self._next = 0
         self._fork = None
         self.bound = None  # lane 0's prepared launch, set by setup()
+        self._local_bound = None  # lane 0's plan without a channel (local_step), made on first use
 
     # ------------------------------------------------------------------ setup
     def _size_for_hbm(self) -> int:
@@ -228,7 +229,7 @@ class ScalarReduction:
         old = [(st, red) for st, red, _, _ in self.lanes]  # keep streams and workspaces
         # Drop every reference to the old bound reductions and channels, then tear the channels
         # down collectively (a new mailbox may reuse an old one's address; see close_channels).
-        self.lanes, self.bound = [], None
+        self.lanes, self.bound, self._local_bound = [], None, None
         close_channels(self.channels, dev)
         lanes, channels = [], []
         for k in range(n):
@@ -275,6 +276,23 @@ class ScalarReduction:
         from ..ops import reduce as host_reduce
         return host_reduce(self.x, self.cfg.op, self.acc, out=out)
 
+    def local_step(self, out: torch.Tensor, async_op: bool = True, corrupt: bool = False):
+        """The step with the combine removed: the SAME kernel plan as :meth:`step` on lane 0's
+        workspace and stream, but bound without a channel (one prepared launch, capturable), so
+        ``step time - local_step time`` is what the cross-rank exchange costs (bench.py's
+        decomposition). Returns None (nothing to wait on)."""
+        if self.ctx.device.type != "cuda":
+            self.local(out)
+        else:
+            if self._local_bound is None:
+                keep = dict(self.reducer.last_plan)
+                self._local_bound = self.reducer.bind(self.x, self.cfg.op, self.acc, out=self._bound_out)
+                self.reducer.last_plan = keep  # the record describes the step's launch
+            self._local_bound.launch(_current_stream_handle(self.ctx.device), out.data_ptr())
+        if corrupt:
+            out.sub_(1) if self.cfg.op == "min" else out.add_(1)
+        return None
+
     def fork(self) -> None:
         """Multi-lane steps: make every lane's stream follow the caller's current stream (call
         before a batch of steps; inside a graph capture this is the fork of the captured DAG)."""
@@ -317,18 +335,21 @@ class ScalarReduction:
 
         * the polled fan-in's sticky error (a launch's finisher reached its wait bound: that launch
           and every later one on the workspace wrote a poisoned result; the workspaces are reset);
-        * the fused finish's error (a peer's partial never arrived)."""
+        * the fused finish's error words (a peer's partial never arrived, or arrived poisoned
+          because that peer's fan-in failed — then every rank's result is poisoned too)."""
         if self.ctx.device.type != "cuda":
             return None
         dev = self.ctx.device
         torch.cuda.synchronize(dev)
         fan = sum(int(red.ws.error() != 0) for _, red, _, _ in self.lanes)
-        xr = sum(int(ch.error() != 0) for ch in self.channels)
+        words = [int(ch.error()) for ch in self.channels]
+        late = sum(int(w & 1 != 0) for w in words)  # a peer's partial missed the timeout
+        pois = sum(int(w & 2 != 0) for w in words)  # a peer pushed a poisoned partial
         if self.ctx.world_size > 1:
-            t = torch.tensor([fan, xr], dtype=torch.int64,
+            t = torch.tensor([fan, late, pois], dtype=torch.int64,
                              device=dev if self.ctx.backend == "nccl" else "cpu")
             torch.distributed.all_reduce(t)
-            fan, xr = (int(v) for v in t.tolist())
+            fan, late, pois = (int(v) for v in t.tolist())
         if fan:
             for _, red, _, _ in self.lanes:
                 red.ws.reset(_current_stream_handle(dev))
@@ -336,8 +357,11 @@ class ScalarReduction:
         msgs = []
         if fan:
             msgs.append(f"polled fan-in: {fan} workspace(s) reached the wait bound (results poisoned; reset)")
-        if xr:
-            msgs.append(f"fused cross-rank finish: {xr} channel(s) timed out waiting for a peer")
+        if late:
+            msgs.append(f"fused cross-rank finish: {late} channel(s) timed out waiting for a peer")
+        if pois:
+            msgs.append(f"fused cross-rank finish: {pois} channel(s) received a peer's poisoned partial "
+                        "(its fan-in failed; results poisoned on every rank)")
         return "; ".join(msgs) or None
 
     # ------------------------------------------------------------------ verify

@@ -1,6 +1,6 @@
 """Tensor operations backed by the native gfx950 kernels (csrc/kernels)."""
 from .reduce import (  # noqa: F401
-    DTYPE_CODES, OP_CODES, KernelConfig, Reducer, cpu_reduce, default_acc_dtype, dtype_code,
+    DTYPE_CODES, OP_CODES, FaninError, KernelConfig, Reducer, cpu_reduce, default_acc_dtype, dtype_code,
     ladder_reduce, op_code, reduce, reduce_partials, sum_tolerance,
 )
 from .fill import PATTERNS, fill_, mt19937_fill_, synthetic  # noqa: F401

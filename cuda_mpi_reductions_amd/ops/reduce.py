@@ -30,7 +30,14 @@ __all__ = [
     "cpu_reduce",
     "sum_tolerance",
     "ladder_reduce",
+    "FaninError",
 ]
+
+
+class FaninError(RuntimeError):
+    """A device reduction's fan-in reached its wait bound: the result is poisoned (NaN for floating
+    accumulators, the operator's identity for integers — which no value check can tell apart from
+    a real result, so the workspace's error word is the signal)."""
 
 DTYPE_CODES = {torch.int32: 0, torch.int64: 1, torch.float32: 2, torch.float64: 3,
                torch.bfloat16: 4, torch.float16: 5}
@@ -128,8 +135,9 @@ class Reducer:
     def check(self, stream: Optional[torch.cuda.Stream] = None) -> Optional[str]:
         """None, or the polled fan-in's sticky error: some launch's finisher reached its wait bound
         (a workgroup never published), so that launch and every later one on this workspace wrote a
-        poisoned result (NaN, or the identity for integers) instead of a wrong-but-plausible one.
-        Synchronises the device; after an error the workspace is reset, so the next launch is good."""
+        poisoned result — NaN for floating accumulators, the operator's identity for integers, for
+        which only this error word tells the result is bad. Synchronises the device; after an error
+        the workspace is reset, so the next launch is good."""
         torch.cuda.synchronize(self.device)
         if self.ws.error() == 0:
             return None
@@ -145,7 +153,12 @@ class Reducer:
         out: Optional[torch.Tensor] = None,
         stream: Optional[torch.cuda.Stream] = None,
         config: Optional[KernelConfig] = None,
+        check: bool = False,
     ) -> torch.Tensor:
+        """Enqueue the reduction (asynchronous). ``check=True`` makes the call synchronous and raises
+        :class:`FaninError` when the workspace's sticky error is set (the result is poisoned; the
+        workspace is reset first, so the next call is good). Without it, call :meth:`check`
+        before trusting an integer result."""
         C = native()
         if x.device != self.device:
             raise ValueError(f"tensor on {x.device}, reducer on {self.device}")
@@ -168,6 +181,10 @@ class Reducer:
             _stream_handle(self.device, stream),
             **cfg.kwargs(),
         )
+        if check:
+            err = self.check(stream)
+            if err is not None:
+                raise FaninError(err)
         return out
 
     def bind(self, x: torch.Tensor, op: str = "sum", acc_dtype: Optional[torch.dtype] = None,
@@ -235,14 +252,17 @@ def reduce(
     acc_dtype: Optional[torch.dtype] = None,
     out: Optional[torch.Tensor] = None,
     config: Optional[KernelConfig] = None,
+    check: bool = False,
 ) -> torch.Tensor:
     """Reduce all elements of ``x`` with ``op`` into a 1-element tensor of the accumulator dtype.
 
     Device tensors run the native HIP kernel on the current stream (asynchronous). Host tensors
-    run the native CPU reference.
+    run the native CPU reference. ``check=True`` (device tensors): wait for the result and raise
+    :class:`FaninError` if the kernel's fan-in failed — the only way to tell for integer results,
+    whose poisoned value is the operator's identity.
     """
     if x.device.type == "cuda":
-        return _default_reducer(x.device)(x, op, acc_dtype, out, config=config)
+        return _default_reducer(x.device)(x, op, acc_dtype, out, config=config, check=check)
     acc = acc_dtype or default_acc_dtype(x.dtype, op)
     val = cpu_reduce(x, op, acc)
     res = torch.tensor([val], dtype=acc)

@@ -123,6 +123,8 @@ def init(backend: Optional[str] = None, device_type: Optional[str] = None,
 
 def shutdown(ctx: Optional[DistContext] = None) -> None:
     if dist.is_initialized() and (ctx is None or ctx.owns_group):
+        from .topology import forget
+        forget()  # answers remembered per process group go with the groups
         dist.destroy_process_group()
 
 

@@ -20,7 +20,7 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
-__all__ = ["PeerMap", "peer_map", "peer_verdict"]
+__all__ = ["PeerMap", "peer_map", "peer_verdict", "forget"]
 
 Key = Tuple[str, str, int]  # (host, device uuid or PCI id, local device index)
 
@@ -53,31 +53,49 @@ def _key(idx: int) -> Key:
     return (socket.gethostname(), str(getattr(props, "uuid", "")) or str(getattr(props, "pci_bus_id", idx)), idx)
 
 
-_cache: dict = {}
+# Answers per (group object, device). The group object itself is held (not its id(), which a later
+# group could reuse on some ranks only: those would skip the gathers the others enter and the job
+# would hang); forget() — called by parallel.dist.shutdown — drops them with the groups.
+_cache: list = []
+
+
+def forget() -> None:
+    """Drop every remembered answer (process groups are being destroyed)."""
+    _cache.clear()
 
 
 def peer_map(idx: int, group=None) -> PeerMap:
     """Collective over ``group``: every rank's (host, GPU, index), and one verdict agreed by all
     ranks (every rank gets the same ``error``). Remembered per (group, device): every rank asks
-    with the same arguments, so every rank takes the cached answer together."""
+    with the same arguments, so every rank takes the cached answer together. A rank whose own
+    (host, GPU) query fails still enters both gathers (with the failure as its key), so the
+    verdict is an error on every rank instead of a hang on the others."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return PeerMap((_key(idx),), 1, None)
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     pg = group if group is not None else dist.distributed_c10d._get_default_group()
-    ck = (id(pg), idx, world, rank)
-    if ck in _cache:
-        return _cache[ck]
-    keys: List = [None] * world
-    dist.all_gather_object(keys, _key(idx), group=group)
-    keys = [tuple(k) for k in keys]
+    for g, i, w, r, pm in _cache:
+        if g is pg and (i, w, r) == (idx, world, rank):
+            return pm
     try:
-        mine = peer_verdict(keys, rank, torch.cuda.can_device_access_peer)
+        key = _key(idx)
     except Exception as e:  # noqa: BLE001 - agreed on below, never raised mid-protocol
-        mine = f"{type(e).__name__}: {e}"
+        key = ("?", f"unknown ({type(e).__name__}: {e})"[:200], idx)
+        mine = f"cannot query device {idx}: {type(e).__name__}: {e}"
+    else:
+        mine = None
+    keys: List = [None] * world
+    dist.all_gather_object(keys, key, group=group)
+    keys = [tuple(k) for k in keys]
+    if mine is None:
+        try:
+            mine = peer_verdict(keys, rank, torch.cuda.can_device_access_peer)
+        except Exception as e:  # noqa: BLE001 - agreed on below, never raised mid-protocol
+            mine = f"{type(e).__name__}: {e}"
     verdicts: List = [None] * world
     dist.all_gather_object(verdicts, mine, group=group)
     bad = [f"rank {r}: {m}" for r, m in enumerate(verdicts) if m]
     gpus = [(h, u) for h, u, _ in keys]
     pm = PeerMap(tuple(keys), max(gpus.count(g) for g in gpus), "; ".join(bad)[:500] if bad else None)
-    _cache[ck] = pm
+    _cache.append((pg, idx, world, rank, pm))
     return pm

@@ -72,16 +72,18 @@ def open_channel(device: torch.device, group=None, timeout_s: float = 2.0, fault
 
 
 def check_channel(channels, group=None) -> Optional[str]:
-    """None if no channel's kernel ever timed out on any rank, else an error string (collective
-    when a process group is initialised: every rank gets the same verdict)."""
-    bad = sum(int(ch.error()) for ch in channels)
+    """None if no channel's kernel ever flagged an error on any rank (a peer's partial late, or
+    poisoned by that peer's failed fan-in), else an error string (collective when a process group
+    is initialised: every rank gets the same verdict)."""
+    bad = sum(int(ch.error() != 0) for ch in channels)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         t = torch.tensor([bad], dtype=torch.int64)
         if dist.get_backend(group) == "nccl":
             t = t.cuda()
         dist.all_reduce(t, group=group)
         bad = int(t.item())
-    return None if bad == 0 else f"fused cross-rank finish: {bad} channel(s) timed out waiting for a peer"
+    return None if bad == 0 else (f"fused cross-rank finish: {bad} channel(s) flagged an error (a peer's "
+                                  "partial timed out or arrived poisoned)")
 
 
 def close_channels(channels: list, device: torch.device, group=None) -> None:

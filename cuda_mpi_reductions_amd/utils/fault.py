@@ -12,7 +12,10 @@ RANK defaults to 1, STEP to 0, SITE to ``step`` (also read from ``MIREDUCE_INJEC
   ``extras``: the steps of bench.py's after-headline candidates (pipelined / RCCL measurements) —
   a hang there must still leave a printed, verified headline (the extras watchdog);
   ``teardown``: just before the process-group teardown that follows the printed line (STEP is
-  ignored) — a hang there must end within the teardown deadline with the headline's status.
+  ignored) — a hang there must end within the teardown deadline with the headline's status;
+  ``capture``: inside bench.py's replay probe of captured collective steps (STEP ignored) — a
+  probe that misses its deadline on one rank must send every rank to eager issue, and the
+  headline must still be measured and verified.
 * KIND ``mailbox``: rank RANK fails to create its fused-finish mailbox
   (:func:`parallel.xrank.open_channel`); every rank must then agree on the RCCL fallback.
 """
@@ -27,7 +30,7 @@ from typing import Optional
 __all__ = ["FaultSpec", "FaultInjector", "parse_fault_spec"]
 
 KINDS = ("none", "exit", "hang", "corrupt", "delay", "mailbox")
-SITES = ("step", "extras", "teardown")
+SITES = ("step", "extras", "teardown", "capture")
 
 
 @dataclass(frozen=True)
@@ -92,7 +95,7 @@ class FaultInjector:
         """Fire once at (rank, step) of ``site``. Returns True iff the caller must corrupt its local
         result."""
         s = self.spec
-        if self.fired or not self.on(site) or rank != s.rank or step != s.step:
+        if self.fired or not self.on(site) or rank != s.rank or (step != s.step and site != "capture"):
             return False
         self.fired = True
         print(f"[fault] rank {rank} {s.kind} at {label or site} {step}", file=sys.stderr, flush=True)

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Round 3, GPU pass B: r1-vs-r3 regression A/B, the HBM-fill investigation, and test_apps_gpu again.
 cd "$GRAFT_REPO_ROOT"
-bash tools/gpu/r3_regress.sh || exit $?
+bash tools/gpu/regress.sh || exit $?
 cd "$GRAFT_REPO_ROOT"
-bash tools/gpu/r3_hbmfill.sh || exit $?
+bash tools/gpu/hbmfill.sh || exit $?
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/r3b
 timeout -k 10 600 python -u -m pytest tests/test_apps_gpu.py -v --timeout 300 --timeout-method thread \

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Round 3, GPU pass C: r1-vs-r3 regression A/B, HBM-fill sizes + PMC, (XCD, residue) affinity sweep.
 cd "$GRAFT_REPO_ROOT"
-bash tools/gpu/r3_regress.sh || exit $?
+bash tools/gpu/regress.sh || exit $?
 cd "$GRAFT_REPO_ROOT"
-bash tools/gpu/r3_hbmfill.sh || exit $?
+bash tools/gpu/hbmfill.sh || exit $?
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r3_shift
 mkdir -p $O

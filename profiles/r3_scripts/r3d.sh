@@ -2,7 +2,7 @@
 # Round 3, GPU pass D: kernel-only fan-in / tree A/B against the round-1 tree, the per-wave dynamic
 # tail experiment (wg_timeline --set=wavetail) at 8 GB and 1 GB, HBM-fill sizes + PMC at 292 GB.
 cd "$GRAFT_REPO_ROOT"
-bash tools/gpu/r3_fanin_ab.sh || exit $?
+bash tools/gpu/fanin_ab.sh || exit $?
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r3_wavetail
 mkdir -p $O
@@ -12,5 +12,5 @@ for n in 1e9 1.25e8; do
   case $rc in 0) ;; *) exit $rc;; esac
 done
 cd "$GRAFT_REPO_ROOT"
-bash tools/gpu/r3_hbmfill.sh
+bash tools/gpu/hbmfill.sh
 du -sh gpurun_out

@@ -16,4 +16,4 @@ for r in 1 2; do
   step bench_f64_$r 300 python bench.py --steps 50 --warmup 10 --no-vector-extras --no-candidates
 done
 step pytest_xrank 600 python -u -m pytest tests/test_xrank_gpu.py -m gpu -q -x --timeout 300 --timeout-method thread
-bash tools/gpu/r3t.sh
+bash profiles/r3_scripts/r3t.sh

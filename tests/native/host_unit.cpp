@@ -10,6 +10,7 @@
 #include "mireduce/cli.hpp"
 #include "mireduce/fault.hpp"
 #include "mireduce/mt19937.hpp"
+#include "mireduce/peer_access.hpp"
 #include "mireduce/report.hpp"
 #include "mireduce/timer.hpp"
 #include "mireduce/types.hpp"
@@ -155,7 +156,37 @@ static void test_fault_spec() {
   CHECK(!d.at(0, 0, "unit"));
 }
 
+static void test_peer_verdict() {
+  // the native twin of parallel/topology.py peer_verdict
+  auto yes = [](int, int) { return true; };
+  auto no = [](int, int) { return false; };
+  const std::vector<PeerKey> node = {{"h", "g0", 0}, {"h", "g1", 1}, {"h", "g2", 2}};
+  for (int me = 0; me < 3; ++me) CHECK(peer_verdict(node, me, yes).empty());
+  CHECK(peer_verdict(node, 1, no) == "device 1 cannot access peer device 0 (rank 0)");
+  // a one-way link: 0 can map 2 but 2 cannot map 0 -> only rank 2 objects
+  auto oneway = [](int a, int b) { return !(a == 2 && b == 0); };
+  CHECK(peer_verdict(node, 0, oneway).empty());
+  CHECK(peer_verdict(node, 2, oneway).find("cannot access peer device 0") != std::string::npos);
+  // ranks sharing one physical GPU need no peer access (one-GPU rehearsals)
+  const std::vector<PeerKey> shared = {{"h", "g0", 0}, {"h", "g0", 0}, {"h", "g0", 0}};
+  CHECK(peer_verdict(shared, 2, no).empty());
+  // another host: IPC handles do not cross hosts
+  const std::vector<PeerKey> two_hosts = {{"a", "g0", 0}, {"b", "g0", 0}};
+  CHECK(peer_verdict(two_hosts, 0, yes).find("runs on host b") != std::string::npos);
+  // same index, different GPU (e.g. different visibility masks)
+  const std::vector<PeerKey> alias = {{"h", "g0", 0}, {"h", "g7", 0}};
+  CHECK(peer_verdict(alias, 1, yes).find("a different GPU") != std::string::npos);
+  CHECK(peer_verdict(node, 5, yes) == "rank index out of range");
+  // agreement: identical text on every rank, failing ranks only, in rank order
+  CHECK(agree_verdicts({"", "", ""}).empty());
+  CHECK(agree_verdicts({"", "x", "", "y"}) == "rank 1: x; rank 3: y");
+  // the injected fault kind parses and is not a step fault
+  FaultInjector f(parse_fault_spec("nopeer@1"));
+  CHECK(f.no_peer(1) && !f.no_peer(0) && !f.at(1, 0, "unit"));
+}
+
 int main() {
+  test_peer_verdict();
   test_cli();
   test_peer_plan();
   test_fault_spec();

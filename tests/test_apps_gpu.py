@@ -319,6 +319,21 @@ def test_reduce_xgmi_direct_corrupt_detected(collective):
     assert "verification FAILED" in r.stderr
 
 
+@pytest.mark.parametrize("mode,collective", [("scalar", "fused"), ("vector", "direct"), ("vector", "direct-reduce")])
+def test_reduce_xgmi_peer_preflight_declines_on_every_rank(mode, collective):
+    # the IPC-mapped paths agree on peer access BEFORE any hipIpcOpenMemHandle;
+    # rank 1 reporting "no peer access" (injected) makes every rank exit non-zero with the agreed
+    # message — no GPU fault, no hang, no collective started (no header row printed).
+    r = torchrun(2, ["--no-python", os.path.join(BIN, "reduce_xgmi"), f"--mode={mode}", f"--collective={collective}",
+                     "--ints=100003", "--doubles=100003", "--retries=1", "--iters=1", "--timeout=5",
+                     "--inject-fault=nopeer@1"], timeout=240)
+    assert r.returncode != 0
+    for k in range(2):
+        assert f"[rank {k}] error: --collective={collective} needs peer access" in r.stderr, r.stderr[-3000:]
+    assert "rank 1: device" in r.stderr and "injected" in r.stderr
+    assert "# DATATYPE" not in r.stdout
+
+
 # "hang" only: a peer that EXITS frees its registered buffers, and the survivor's kernel would
 # then store its barrier flag into unmapped peer memory — a GPU fault by construction, not a test.
 @pytest.mark.parametrize("kind", ["hang"])

@@ -2,12 +2,13 @@
 code paths bench.py runs over RCCL on GPUs."""
 import json
 import os
+import sys
 
 import pytest
 import torch
 import torch.multiprocessing as mp
 
-from helpers import ROOT, free_port, torchrun
+from helpers import ROOT, free_port, run, torchrun
 
 
 def _worker(rank, world, port, fn_name, q):
@@ -135,6 +136,44 @@ def test_bench_contract_on_cpu_ranks(tmp_path):
     assert d["metric"] == "reduction bandwidth (GB/s, whole node), 1B-double sum at 1/2/4/8 MI355X"
     assert d["scaling"] == "strong" and d["config"]["parallelism"] == "dp2"
     assert abs(d["value"] - d["config"]["bytes_per_step"] * 4 / (d["ms_per_step"] * 4e-3) / 1e9) / d["value"] < 0.01
+
+
+def test_bench_self_launches_n_ranks_without_torchrun(tmp_path):
+    # `python bench.py --gpus 2` with no launcher starts 2 ranks itself (a child
+    # torch.distributed.run; the parent never touches a GPU) and proves the shape in the JSON
+    r = run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "3",
+             "--warmup", "1", "--elements", "200003"], cwd=tmp_path, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["ranks_seen_backend"] == "gloo"
+    assert d["launcher"] == "self-spawned" and d["verified"] is True
+    assert d["rccl_ranks_seen"] is None  # gloo here; on GPUs the same all-reduce runs over RCCL
+    # the N>1 decomposition is present: local time, skew, exchange
+    dec = d["decomposition"]
+    for k in ("local_ms_per_step", "local_ms_min", "local_ms_max", "local_gbps", "skew_us_per_step",
+              "exchange_us_per_step", "scaling_efficiency_vs_local", "local_launch", "consistent"):
+        assert k in dec, k
+    assert dec["local_ms_min"] <= dec["local_ms_max"] == dec["local_ms_per_step"] and dec["consistent"] is True
+    assert abs(dec["exchange_us_per_step"] - (d["ms_per_step"] - dec["local_ms_max"]) * 1e3) < 0.01
+
+
+def test_bench_refuses_world_size_mismatch(tmp_path):
+    # a launcher that started a different number of ranks than --gpus asks for: diagnostic line, rc 2
+    r = run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "3"],
+            cwd=tmp_path, timeout=300, env={"WORLD_SIZE": "1", "RANK": "0"})
+    assert r.returncode == 2
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["value"] is None and "WORLD_SIZE=1" in d["error"]
+
+
+def test_bench_external_launcher_recorded(tmp_path):
+    r = torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                     "--device", "cpu", "--elements", "100003", "--no-decompose"], cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["launcher"] == "external" and d["ranks_seen"] == 2 and "decomposition" not in d
 
 
 def test_bench_vector_config1_two_cpu_ranks(tmp_path):

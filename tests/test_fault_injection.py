@@ -33,6 +33,7 @@ def test_parse_fault_spec():
     assert parse_fault_spec("delay=250@0:2") == FaultSpec("delay", 0, 2, 250)
     assert parse_fault_spec("corrupt:5") == FaultSpec("corrupt", 1, 5, 0)
     assert parse_fault_spec("hang@1/teardown") == FaultSpec("hang", 1, 0, 0, "teardown")
+    assert parse_fault_spec("delay=500@0/capture") == FaultSpec("delay", 0, 0, 500, "capture")
     for bad in ("boom", "exit@", "exit@x", "hang:-1", "delay=", "corrupt@1:2x"):
         with pytest.raises(ValueError):
             parse_fault_spec(bad)
@@ -116,3 +117,17 @@ def test_reduce_mpi_crashed_rank_ends_job():
              "--inject-fault=exit@1:2"], timeout=120)
     assert r.returncode != 0
     assert time.time() - t0 < 60
+
+
+def test_replay_probe_miss_on_one_rank_goes_eager_and_still_measures(tmp_path):
+    # rank 1 misses the replay probe's deadline (injected delay past it); every
+    # rank must agree to issue the headline eagerly, and the headline is still measured and
+    # verified with rc 0 — the JSON names the rank and the reason.
+    r = torchrun(2, [BENCH, *SCALAR, "--replay-probe", "on", "--probe-deadline", "1",
+                     "--inject-fault", "delay=2500@1/capture"], cwd=tmp_path, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json(r)
+    assert d["verified"] is True and d["value"] > 0
+    launch = d["config"]["launch"]
+    assert launch.startswith("eager (replay probe failed: ") and "rank 1: 3 steps took" in launch, launch
+    assert "[fault] rank 1 delay at replay probe" in r.stderr

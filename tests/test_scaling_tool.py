@@ -49,6 +49,23 @@ def test_cli_writes_results_files_readable_by_plot_and_getavgs(tmp_path):
     assert [n for n, _ in plot.read_results(str(out / "DOUBLE_SUM.txt"))] == [1, 2, 4, 8]
 
 
+def test_decomposition_columns(tmp_path):
+    # bench.py's per-N decomposition (local / exchange / skew) reaches the table
+    a = _line(8, 50000.0, 0.16)
+    a["decomposition"] = {"local_ms_per_step": 0.14, "exchange_us_per_step": 20.0, "skew_us_per_step": 1.5,
+                          "scaling_efficiency_vs_local": 0.875}
+    b = _line(8, 52000.0, 0.154)
+    b["decomposition"] = {"local_ms_per_step": 0.142, "exchange_us_per_step": 12.0, "skew_us_per_step": 2.5,
+                          "scaling_efficiency_vs_local": 0.922}
+    c = _line(1, 7300.0, 1.0959)  # an older line without the field
+    per_n = scaling.summarise([a, b, c])[("xgmi_1b_double_sum", "DOUBLE", "SUM")]
+    assert abs(per_n[8]["local_ms"] - 0.141) < 1e-12 and per_n[8]["exchange_us"] == 16.0
+    assert per_n[8]["skew_us"] == 2.0 and abs(per_n[8]["vs_local"] - 0.8985) < 1e-12
+    assert per_n[1]["local_ms"] is None
+    text = scaling.write({("xgmi_1b_double_sum", "DOUBLE", "SUM"): per_n}, str(tmp_path))
+    assert "exchange us/step" in text and "| 0.1410 | 16.00 | 2.00 | 0.899 |" in text
+
+
 def test_cli_without_results_fails(tmp_path):
     empty = tmp_path / "e.txt"
     empty.write_text("nothing here\n")

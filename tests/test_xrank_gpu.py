@@ -104,6 +104,54 @@ def test_bench_fused_ranks_share_one_gpu(tmp_path, nproc, monkeypatch):
     assert d["config"]["launch"].startswith("graph")
 
 
+@pytest.mark.parametrize("dt,op", [(torch.int64, "min"), (torch.float64, "sum")])
+def test_fused_poison_reaches_every_rank(tmp_path, dt, op):
+    # rank 1's polled fan-in misses its bound, so its partial is poisoned (the
+    # MIN identity for int64, NaN for fp64) and pushed with the poison flag: rank 0 must flag its own
+    # channel (bit 2) and poison its result too — never fold a neutral partial into a plausible
+    # value with a clean error word. Then, after resets, a clean launch is exact on both ranks.
+    script = tmp_path / "xp.py"
+    script.write_text(
+        "import math, os, sys, torch\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import torch.distributed as dist\n"
+        "from cuda_mpi_reductions_amd._native import native\n"
+        "from cuda_mpi_reductions_amd.ops import Reducer, default_acc_dtype, dtype_code, op_code\n"
+        "from cuda_mpi_reductions_amd.parallel.xrank import open_channel\n"
+        "dist.init_process_group('gloo')\n"
+        "r = dist.get_rank(); C = native()\n"
+        "dev = torch.device('cuda', 0); torch.cuda.set_device(dev)\n"
+        f"dt, op = {dt}, {op!r}\n"
+        "x = torch.full((1 << 22,), 3 + r, dtype=dt, device=dev)\n"
+        "acc = default_acc_dtype(dt, op)\n"
+        "out = torch.zeros(1, dtype=acc, device=dev)\n"
+        "ch = open_channel(dev, timeout_s=5.0)\n"
+        "red = Reducer(dev)\n"
+        "s = torch.cuda.current_stream().cuda_stream\n"
+        "def launch(**kw):\n"
+        "    return C.reduce(red.ws, x.data_ptr(), x.numel(), dtype_code(dt), op_code(op), dtype_code(acc),\n"
+        "                    out.data_ptr(), s, xrank=ch.desc_ptr, **kw)\n"
+        "kw = dict(fanin_bound_ticks=100_000, debug_delay_wg=0, debug_delay_ticks=5_000_000) if r == 1 else {}\n"
+        "launch(**kw); torch.cuda.synchronize()\n"
+        "v = out.item(); fan, xr = red.ws.error(), ch.error()\n"
+        "dist.barrier()\n"
+        "red.ws.reset(s); ch.clear_error(); torch.cuda.synchronize(); dist.barrier()\n"
+        "launch(); torch.cuda.synchronize()\n"
+        f"open(os.path.join({str(tmp_path)!r}, 'r%d' % r), 'w').write(repr((v, fan, xr, out.item(), ch.error())))\n"
+        "dist.destroy_process_group()\n")
+    r = torchrun(2, [str(script)], timeout=240, env={"MIREDUCE_FORCE_DEVICE": "0"})
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    import math
+    ident = torch.iinfo(dt).max if op == "min" else 0
+    clean = 3 if op == "min" else (3.0 + 4.0) * (1 << 22)
+    res = {k: eval((tmp_path / f"r{k}").read_text()) for k in range(2)}  # noqa: S307 - our own repr
+    for k, (v, fan, xr, v2, xr2) in res.items():
+        assert (math.isnan(v) if dt.is_floating_point else v == ident), (k, v)
+        assert v2 == clean and xr2 == 0, (k, v2, xr2)
+    assert res[1][1] != 0 and res[1][2] == 0   # rank 1: its own fan-in failed; its channel saw clean peers
+    assert res[0][1] == 0 and res[0][2] == 2   # rank 0: clean fan-in, a poisoned partial from rank 1
+
+
 def test_fused_missing_peer_times_out_not_hangs(tmp_path):
     # Rank 1 never launches: rank 0's kernel must give up after its timeout, flag the channel
     # (sticky: the next launch does not wait again) and the collective check must report it.
@@ -353,3 +401,33 @@ def test_bench_maxloc_config_skips_plan_tuning(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["verified"] is True and "plan_tuning" not in d
+
+
+# ---------------------------------------------------------------- bench: replay probe, decomposition
+
+def test_bench_replay_probe_and_decomposition_one_gpu(tmp_path):
+    # VERDICT r3 items 2 and 4 on the GPU path: the RCCL combine captured at world 1 runs the replay
+    # probe (forced on) and passes it; the decomposition's local time is the same kernel without
+    # the combine, so at world 1 the exchange costs little.
+    r = run([sys.executable, BENCH, "--no-vector-extras", "--no-candidates", "--steps", "40", "--warmup", "2",
+             "--elements", "50000017", "--collective", "rccl", "--replay-probe", "on"], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r)
+    assert d["verified"] is True and d["config"]["launch"].startswith("graph") and "replay probe ok" in d["config"]["launch"]
+    dec = d["decomposition"]
+    assert dec["consistent"] is True and dec["local_launch"].startswith("graph")
+    assert 0 < dec["local_ms_per_step"] <= d["ms_per_step"] * 1.5
+    assert dec["local_ms_min"] <= dec["local_ms_max"] and dec["skew_us_per_step"] == 0.0  # one rank
+    assert d["launcher"] == "single process" and d["rccl_ranks_seen"] == 1
+
+
+def test_bench_replay_probe_failure_goes_eager_one_gpu(tmp_path):
+    # a probe that misses its deadline (injected 3 s delay vs a 1 s deadline) sends the headline to
+    # eager issue; it is still measured and verified (rc 0)
+    r = run([sys.executable, BENCH, "--no-vector-extras", "--no-candidates", "--steps", "10", "--warmup", "2",
+             "--elements", "50000017", "--collective", "rccl", "--replay-probe", "on", "--probe-deadline", "1",
+             "--inject-fault", "delay=3000@0/capture"], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r)
+    assert d["verified"] is True
+    assert d["config"]["launch"].startswith("eager (captured replay probe failed: rank 0: "), d["config"]["launch"]

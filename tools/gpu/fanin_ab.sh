@@ -2,7 +2,7 @@
 # Same-box kernel-only A/B (reduction app, hipEvent per iteration, 100 iterations, 8 GB float64 SUM):
 # the round-1 tree (.ab/r1, ticketed tree fan-in) against this tree with the polled fan-in (default)
 # and with MIREDUCE_FANIN=tree (round 1's fan-in), for the round-1 and round-3 8 GB plans.
-O=gpurun_out/r3_fanin_ab
+O=${O:-gpurun_out/fanin_ab}
 mkdir -p $O
 cd "$GRAFT_REPO_ROOT"
 run() {  # run <tag> <binary> <B> <U> <W>

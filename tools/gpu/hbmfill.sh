@@ -3,7 +3,7 @@
 #  1. GB/s vs array size (8 GB .. 292 GB), interleaved split (default) and contiguous split
 #  2. PMC at 8 GB vs 292 GB: UTCL1 translation misses / stalls, UTCL2 busy, EA read requests & stalls
 # Every GPU step has its own time limit; a timeout / crash ends the script.
-O=gpurun_out/r3_hbmfill2
+O=${O:-gpurun_out/hbmfill}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 B=./build/bin/reduction

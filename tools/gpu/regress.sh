@@ -1,7 +1,7 @@
 #!/bin/bash
 # same-box A/B of the round-1 tree (4cc6ac6, built in .ab/r1) against this tree on
 # the driver's exact command, interleaved, 3 runs each, under rocprofv3 --kernel-trace --stats.
-O=$GRAFT_REPO_ROOT/gpurun_out/r3_regress
+O=${O:-$GRAFT_REPO_ROOT/gpurun_out/regress}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 for i in 1 2 3; do

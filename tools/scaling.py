@@ -22,6 +22,12 @@ or any JSON document holding such objects, e.g. the driver's scaling file), grou
 Efficiency = value(N) / (N * value(1)): the whole-node bandwidth of N GPUs against N copies of the
 1-GPU run (bench.py's headline is strong scaling, so this is also t(1) / (N * t(N))).
 
+Where an N-GPU step's time goes (bench.py's ``decomposition``, averaged like the headline): the
+slowest rank's local reduce (ms/step, the same kernel without the combine), the cross-rank
+exchange (us/step = headline - local), the inter-GPU skew of the local work (us/step) and
+``vs local`` = local time / step time (1.0 = the combine is free). So a loss of efficiency at N=8
+splits into the per-GPU rate at the smaller shard (local ms vs N=1), the exchange and the skew.
+
     python tools/scaling.py SCALE_r01.json bench_*.json --out results/scaling
 """
 from __future__ import annotations
@@ -88,6 +94,21 @@ def summarise(results):
             ms = [float(r["ms_per_step"]) for r in rs if r.get("ms_per_step") is not None]
             out[k][n] = {"gbps": sum(float(r["value"]) for r in rs) / len(rs),
                          "ms": sum(ms) / len(ms) if ms else None, "runs": len(rs)}
+            out[k][n].update(_decomposition(rs))
+    return out
+
+
+DECOMP = (("local_ms", "local_ms_per_step"), ("exchange_us", "exchange_us_per_step"),
+          ("skew_us", "skew_us_per_step"), ("vs_local", "scaling_efficiency_vs_local"))
+
+
+def _decomposition(rs) -> dict:
+    """Mean of each bench.py ``decomposition`` field over the runs that carry it (None if none do)."""
+    out = {}
+    for name, field in DECOMP:
+        vals = [float(d[field]) for d in (r.get("decomposition") or {} for r in rs)
+                if isinstance(d, dict) and d.get(field) is not None]
+        out[name] = sum(vals) / len(vals) if vals else None
     return out
 
 
@@ -158,8 +179,9 @@ def efficiency(per_n):
 
 def write(summary, out_dir):
     os.makedirs(out_dir, exist_ok=True)
-    md = ["| config | dtype | op | N | GB/s (whole node) | ms/step | speed-up | efficiency | runs |",
-          "|---|---|---|---|---|---|---|---|---|"]
+    md = ["| config | dtype | op | N | GB/s (whole node) | ms/step | speed-up | efficiency | runs "
+          "| local ms/step | exchange us/step | skew us/step | vs local |",
+          "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for (model, dt, op), per_n in sorted(summary.items()):
         with open(os.path.join(out_dir, f"{dt}_{op}.txt"), "w") as f:
             f.write("\n")  # getAvgs.sh:5-6 starts each results file with a blank line
@@ -171,7 +193,10 @@ def write(summary, out_dir):
             ms = "" if v["ms"] is None else "%.4f" % v["ms"]
             sp = "" if s is None else "%.2fx" % s
             ef = "" if e is None else "%.1f %%" % (100 * e)
-            md.append(f"| {model} | {dt} | {op} | {n} | {v['gbps']:.1f} | {ms} | {sp} | {ef} | {v['runs']} |")
+            dec = ["" if v.get(f) is None else fmt % v[f] for f, fmt in
+                   (("local_ms", "%.4f"), ("exchange_us", "%.2f"), ("skew_us", "%.2f"), ("vs_local", "%.3f"))]
+            md.append(f"| {model} | {dt} | {op} | {n} | {v['gbps']:.1f} | {ms} | {sp} | {ef} | {v['runs']} | "
+                      + " | ".join(dec) + " |")
     text = "\n".join(md) + "\n"
     with open(os.path.join(out_dir, "scaling.md"), "w") as f:
         f.write(text)

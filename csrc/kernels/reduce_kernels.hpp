@@ -334,6 +334,29 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   const uint64_t t0 = a.contig ? blockIdx.x * ntiles / grid : blockIdx.x;
   const uint64_t t1 = a.contig ? (blockIdx.x + 1) * ntiles / grid : full;
   const uint64_t step = a.contig ? 1 : grid;
+  // Balanced mode: the leftover after the whole rounds (< grid tiles + the sub-tile remainder) is
+  // split into one even, contiguous piece per workgroup (< one tile each, so <= UNROLL loads per
+  // thread, their count `nl` uniform over the workgroup). With an explicit window the piece is
+  // loaded BEFORE the body and consumed after it: it costs no extra memory round trip at the end,
+  // where the kernel's last workgroups decide its duration.
+  V pre_v[WIN > 0 ? UNROLL : 1];
+  uint64_t pre_s0 = 0, pre_s1 = 0;
+  int pre_n = 0;
+  if constexpr (WIN > 0) {
+    if (balanced) {
+      const uint64_t l0 = full * kTile, left = a.nvec - l0;
+      pre_s0 = l0 + left * blockIdx.x / grid;
+      pre_s1 = l0 + left * (blockIdx.x + 1) / grid;
+      pre_n = static_cast<int>((pre_s1 - pre_s0 + BLOCK - 1) / BLOCK);
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        if (u < pre_n) {
+          const uint64_t idx = pre_s0 + threadIdx.x + static_cast<uint64_t>(u) * BLOCK;
+          pre_v[u] = __builtin_nontemporal_load(vin + (idx < pre_s1 ? idx : pre_s0));
+        }
+      }
+    }
+  }
   if constexpr (PIPE) {
     if (t0 < t1) {
       V cur[UNROLL];
@@ -358,7 +381,15 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, v);
     }
   }
-  if (balanced) {
+  if (WIN > 0 && balanced) {  // the piece prefetched before the body
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      if (u < pre_n && pre_s0 + threadIdx.x + static_cast<uint64_t>(u) * BLOCK < pre_s1) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(pre_v[u], k)));
+      }
+    }
+  } else if (balanced) {
     // The leftover after the whole rounds (< grid tiles + the sub-tile remainder) as one even,
     // contiguous piece per workgroup (< one tile each): every load issued unconditionally (an
     // out-of-piece lane re-reads its piece's first vector and discards it), so no per-load branch

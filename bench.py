@@ -243,6 +243,20 @@ def _ranks_seen(ctx) -> int:
     return int(t.item())
 
 
+def _emit(line: dict) -> bool:
+    """Print THE result line (rank 0) through the native once-guard: if a signal handler already
+    printed the armed line (the process is being killed), nothing more is printed."""
+    sys.stdout.flush()
+    return native().emit_final_line(json.dumps(line))
+
+
+def _arm(line: "dict | None") -> None:
+    """The line to print if the process is killed (torchrun SIGTERMs every rank when one fails; a GPU
+    fault aborts): csrc/include/mireduce/final_line.hpp. Only rank 0 arms (others pass None)."""
+    if line is not None:
+        native().arm_final_line(json.dumps(line))
+
+
 def _launch_record(ctx, seen: int) -> dict:
     """JSON fields that prove the job's shape: who started the ranks and how many the collective saw."""
     launcher = os.environ.get(LAUNCHER_ENV) or ("external" if "WORLD_SIZE" in os.environ else "single process")
@@ -334,7 +348,7 @@ def run_vector(args, ctx, cfg, fault) -> int:
     if seen != ctx.world_size:
         verified = False
     if ctx.is_root:
-        print(json.dumps({
+        _emit(({
             "metric": f"MPI_Reduce-style element-wise {cfg.collective} bandwidth (GiB/s of total data, reduce.c units)",
             "value": round(gib, 3), "unit": "GiB/s", "n_gpus": ctx.world_size if dev.type == "cuda" else 0,
             "n_ranks": ctx.world_size, "steps": args.steps, "warmup": args.warmup,
@@ -349,7 +363,7 @@ def run_vector(args, ctx, cfg, fault) -> int:
             "baseline_source": cfg.baseline_source or None,
             "verified": verified,
             **_launch_record(ctx, seen),
-        }), flush=True)
+        }))
     return 0 if verified in (None, True) else 1
 
 
@@ -378,7 +392,7 @@ def _checksum(wl, holder: bool) -> float:
     return float(wl.result().to(torch.float64).sum().item()) if holder else 0.0
 
 
-def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES, out: "dict | None" = None) -> dict:
+def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES, out: "dict | None" = None, progress=None) -> dict:
     """reduce.c's own measurement on this job's GPUs, next to the scalar headline, in reduce.c's
     shape: element-wise INT and DOUBLE MAX / MIN / SUM of 2 GiB of total data each (NUM_INTS /
     NUM_DOUBLES, mpi/constants.h:1-2) to root 0 (MPI_Reduce, reduce.c:76,90), one warm-up SUM per
@@ -445,6 +459,8 @@ def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES, out: "dict | None" = No
                         if dev_err:
                             table[-1]["device_error"] = dev_err
                         lines.append("%s %s %d %10.3lf" % (dt, op.upper(), ctx.world_size, gib))
+                        if progress is not None:
+                            progress()  # the rows so far survive a kill of the process
             for kind, coll in (("reduce", "reduce"), ("allreduce", "allreduce")):  # DOUBLE SUM summaries
                 wl = wls["DOUBLE"]
                 wl.cfg = replace(_C["xgmi_2g_double_sum_reduce"], op="sum", collective=coll)
@@ -786,7 +802,7 @@ class _PhaseWatchdog:
             self._done = True
             line = self._make_line()
             if line is not None:
-                print(json.dumps(line), flush=True)
+                _emit(line)
             print(f"[bench] {self._what} exceeded {self._deadline:.0f} s: exiting with {self._rc}",
                   file=sys.stderr, flush=True)
             os._exit(self._rc)
@@ -968,8 +984,8 @@ def main(argv=None) -> int:
                      timeout_s=args.pg_timeout)
     if args.gpus != ctx.world_size:  # (main() called directly; the __main__ launcher checks this first)
         if ctx.is_root:
-            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": args.gpus, "verified": None,
-                              "error": f"--gpus {args.gpus} but WORLD_SIZE={ctx.world_size}"}), flush=True)
+            _emit({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": args.gpus, "verified": None,
+                   "error": f"--gpus {args.gpus} but WORLD_SIZE={ctx.world_size}"})
         pdist.shutdown(ctx)
         return 2
     cfg = CONFIGS[args.config]
@@ -986,13 +1002,18 @@ def main(argv=None) -> int:
     # ------------------------------------------------------------------ headline phase (deadline)
     stage = {"now": "setup"}
 
-    def diag():
+    def diag(why: "str | None" = None):
         if not ctx.is_root:
             return None
         return {"metric": metric, "value": None, "unit": "GB/s", "n_gpus": ctx.world_size, "steps": K,
                 "warmup": W, "higher_is_better": True, "scaling": "strong", "verified": None,
-                "error": f"headline phase did not finish within {args.headline_deadline:.0f} s "
-                         f"(stage: {stage['now']}); no measurement", "native_source_hash": C.source_hash()}
+                "error": (why or f"headline phase did not finish within {args.headline_deadline:.0f} s") +
+                         f" (stage: {stage['now']}); no measurement", "native_source_hash": C.source_hash()}
+
+    def at_stage(name: str) -> None:
+        stage["now"] = name
+        _arm(diag("the process was terminated (signal) during the headline phase"))
+    at_stage("setup")
     watch = _PhaseWatchdog("headline phase", args.headline_deadline, 2, diag)
 
     kernel = KernelConfig(block=args.block, unroll=args.unroll, wg_per_cu=args.wg_per_cu,
@@ -1013,7 +1034,7 @@ def main(argv=None) -> int:
     if collective == "auto":
         collective = "rccl"
         if fused_ok:
-            stage["now"] = "fused self-check"
+            at_stage("fused self-check")
             collective_note = _try_fused(wl, ctx)
             collective = "fused" if collective_note is None else "rccl"
             if collective_note and ctx.is_root:
@@ -1028,10 +1049,10 @@ def main(argv=None) -> int:
         cands = _plan_candidates(wl.bytes_total / ctx.world_size, torch.empty((), dtype=cfg.dtype).element_size())
         if len(cands) > 1:
             # kernel-only steps with bounded device waits: this cannot hang on a collective
-            stage["now"] = "plan tuning"
+            at_stage("plan tuning")
             kernel, plan_tuning = _tune_plan(wl, ctx, args, fault, kernel, cands)
 
-    stage["now"] = "timed steps"
+    at_stage("timed steps")
     slots = wl.new_slots(W + K)
     m = _measure(wl, slots, ctx, args, fault, serial=not args.pipelined, warmup=W)
     m_lanes = len(wl.lanes) if wl.lanes else 1
@@ -1040,7 +1061,7 @@ def main(argv=None) -> int:
     seen = _ranks_seen(ctx)
     if seen != ctx.world_size:
         err = (err + "; " if err else "") + f"the process group joined {seen} ranks, not {ctx.world_size}"
-    stage["now"] = "verification"
+    at_stage("verification")
     verified = None
     if not args.no_verify:
         ok, ref = _verify_slots(wl, slots[:m["written"]], ctx)
@@ -1133,6 +1154,15 @@ def main(argv=None) -> int:
     # what has completed.
     extras = {}
     guard = _ExtrasWatchdog(line, args.extras_deadline, rc, partial=extras)
+
+    def rearm() -> None:  # the finished headline + the extras so far, should the process be killed now
+        if line is not None:
+            out = dict(line)
+            out.update(json.loads(json.dumps(extras)))
+            out["extras_error"] = "the process was terminated (signal) during the extras; headline measured and " \
+                                  "verified before them"
+            _arm(out)
+    rearm()
     run_cands = args.candidates and dev.type == "cuda" and hasattr(wl, "use_collective") and not args.pipelined
     cap_failed = m["launch"].startswith("eager (graph capture failed")
     if args.decompose and not args.pipelined and hasattr(wl, "local_step"):  # kernels only: cheap, first
@@ -1141,13 +1171,17 @@ def main(argv=None) -> int:
         except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
             extras["decomposition"] = {"error": f"{type(e).__name__}: {e}"[:300]}
             print(f"[bench] rank {ctx.rank}: decomposition failed: {e}", file=sys.stderr)
+        rearm()
     if run_cands:  # the fused (kernel-only) candidate first: before the torch-heavy extras below
         extras["candidates"] = _candidates(wl, ctx, args, fault, collective == "fused", cap_failed, which="fused")
+        rearm()
     if args.vector_extras and dev.type == "cuda" and cfg.name == NORTH_STAR:
         extras["reduce_c_vector"] = {}
-        _vector_extras(ctx, out=extras["reduce_c_vector"])
+        _vector_extras(ctx, out=extras["reduce_c_vector"], progress=rearm)
+        rearm()
     if args.compare_torch and dev.type == "cuda":
         extras["torch_gbps"] = round(_time_torch_reduction(wl, K, W, ctx), 3)
+        rearm()
     if run_cands:  # the RCCL candidates last: a hang there costs the fewest extras
         extras["candidates"].update(_candidates(wl, ctx, args, fault, collective == "fused", cap_failed,
                                                 which="rccl"))
@@ -1161,7 +1195,7 @@ def main(argv=None) -> int:
         for k in ("torch_gbps", "reduce_c_vector", "decomposition"):
             if k in extras:
                 line[k] = extras[k]
-        print(json.dumps(line), flush=True)
+        _emit(line)
     elif line is not None:  # the watchdog printed it
         pass
     # The line is out: a teardown stuck in a collective (communicator destruction) must not hold

@@ -16,6 +16,7 @@
 #include "mireduce/check.hpp"
 #include "mireduce/cpu_reference.hpp"
 #include "mireduce/direct.hpp"
+#include "mireduce/final_line.hpp"
 #include "mireduce/ladder.hpp"
 #include "mireduce/moments.hpp"
 #include "mireduce/mt19937.hpp"
@@ -217,6 +218,15 @@ PYBIND11_MODULE(_C, m) {
       .def("epoch", &XrankChannel::epoch)
       .def("clear_error", &XrankChannel::clear_error);
   m.attr("XRANK_MAX_RANKS") = kMaxXrankRanks;
+
+  // bench.py's one result line, printed exactly once even if the process is killed (final_line.hpp).
+  m.def("arm_final_line", [](const std::string& line) { arm_final_line(line); }, py::arg("line"));
+  m.def("disarm_final_line", &disarm_final_line);
+  m.def("emit_final_line", [](const std::string& line) {
+    py::gil_scoped_release nogil;
+    return emit_final_line(line);
+  }, py::arg("line"));
+  m.def("final_line_emitted", &final_line_emitted);
 
   // Stream-ordered device copy between raw pointers (registered IPC buffers <-> torch tensors).
   m.def("memcpy_d2d", [](uintptr_t dst, uintptr_t src, uint64_t bytes, uintptr_t stream) {

@@ -164,6 +164,10 @@ def parse_args(argv=None):
                    help="cross-rank combine: rccl = 1-element RCCL all-reduce after the local kernel; "
                         "fused = the kernel's last workgroup folds all ranks' partials via IPC mailboxes; "
                         "auto = fused if its self-check passes on every rank, else rccl (GPU scalar configs)")
+    p.add_argument("--no-canary", dest="canary", action="store_false",
+                   help="at N > 1, skip the fused finish's canary (the same exchange run first in throw-away "
+                        "helper processes, so a fault of the peer mapping cannot take the benchmark down)")
+    p.add_argument("--canary-timeout", type=float, default=90.0, help="seconds each canary helper may take")
     p.add_argument("--xrank-timeout", type=float, default=30.0,
                    help="fused finish: seconds a kernel waits for a peer's partial before flagging the channel")
     p.add_argument("--tune-steps", type=int, default=0,
@@ -716,10 +720,17 @@ def _replay_probe(wl, ctx, args, fault, serial: bool, step, capture: bool) -> "s
     return "; ".join(f"rank {r}: {m}" for r, m in enumerate(errs) if m)[:300] or "failed on another rank"
 
 
-def _try_fused(wl, ctx) -> "str | None":
+def _try_fused(wl, ctx, canary: bool = True, canary_timeout: float = 90.0) -> "str | None":
     """Switch the workload to the fused in-kernel finish and check it on every rank: 3 steps, no
     channel timeout or fan-in error, results equal to torch's reference. On any failure (agreed over
-    ranks) switch back to RCCL and return the reason."""
+    ranks) switch back to RCCL and return the reason. At N > 1 a canary runs the same exchange in
+    throw-away helper processes first (parallel/canary.py): a fault of the peer mapping there
+    cannot take this process — and the headline — down with it."""
+    if canary and ctx.world_size > 1:
+        from cuda_mpi_reductions_amd.parallel.canary import fused_canary
+        err = fused_canary(ctx, timeout_s=canary_timeout, dry=ctx.device.type != "cuda")
+        if err is not None:
+            return f"canary: {err}"[:300]
     try:
         wl.use_collective("fused", streams=1)  # collective; raises on every rank if any rank cannot map
     except Exception as e:  # noqa: BLE001
@@ -1035,7 +1046,7 @@ def main(argv=None) -> int:
         collective = "rccl"
         if fused_ok:
             at_stage("fused self-check")
-            collective_note = _try_fused(wl, ctx)
+            collective_note = _try_fused(wl, ctx, canary=args.canary, canary_timeout=args.canary_timeout)
             collective = "fused" if collective_note is None else "rccl"
             if collective_note and ctx.is_root:
                 print(f"[bench] fused finish unavailable, using RCCL: {collective_note}", file=sys.stderr)

@@ -1,0 +1,147 @@
+"""Canary run of the fused cross-rank finish in throw-away child processes.
+
+The fused finish (:mod:`.xrank`) stores into and polls peers' IPC-mapped GPU memory from inside the
+reduction kernel. Every rank agrees on peer access before mapping (:mod:`.topology`), device waits
+are bounded and results are self-checked — but a fault of the mapping itself (a GPU memory-access
+fault) would abort the process, and with it the measurement it was meant to serve. So before a
+benchmark process touches a peer's memory, :func:`fused_canary` has one helper process per rank
+run the same exchange end to end: a private gloo group over the job's rendezvous store (a fresh
+key prefix), a channel, three fused launches of a 1-element-per-rank-distinguishable array, and a
+check of every result, the error words and a final barrier (nobody unmaps while a peer still
+polls). Each rank waits for its helper (bounded), and the verdicts are agreed over the real
+process group: any failure — a crash, a timeout, a wrong value — makes every rank decline the
+fused finish together (bench.py then combines over RCCL). The helpers never share a process with
+the benchmark, so whatever faults in them cannot take the benchmark down.
+
+Reference: the vendored simpleP2P checks peer access and then actually exercises the peer path
+(a kernel reading the other GPU's buffer, verified) before reporting bandwidth
+(cuda/C/src/simpleP2P/simpleP2P.cu:250-275,330-350).
+
+``python -m cuda_mpi_reductions_amd.parallel.canary`` is the helper (its parameters come from
+``MIREDUCE_CANARY_*`` environment variables set by :func:`fused_canary`).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import secrets
+import subprocess
+import sys
+from typing import Optional
+
+__all__ = ["fused_canary"]
+
+_ENV = "MIREDUCE_CANARY_"
+
+
+def _helper_fault(rank: int) -> None:
+    """Test hook: MIREDUCE_CANARY_FAULT = abort@R | hang@R | wrong@R (the helper of rank R)."""
+    spec = os.environ.get(_ENV + "FAULT", "")
+    if not spec or "@" not in spec:
+        return
+    kind, r = spec.split("@", 1)
+    if int(r) != rank:
+        return
+    if kind == "abort":
+        print(f"[canary] rank {rank}: injected abort", file=sys.stderr, flush=True)
+        os.abort()
+    if kind == "hang":
+        import time
+        while True:
+            time.sleep(1)
+
+
+def _helper() -> int:
+    rank, world = int(os.environ[_ENV + "RANK"]), int(os.environ[_ENV + "WORLD"])
+    host, port = os.environ[_ENV + "ADDR"], int(os.environ[_ENV + "PORT"])
+    prefix, dry = os.environ[_ENV + "PREFIX"], os.environ.get(_ENV + "DRY") == "1"
+    timeout = datetime.timedelta(seconds=float(os.environ.get(_ENV + "TIMEOUT", "60")))
+    import torch
+    import torch.distributed as dist
+    store = dist.PrefixStore(prefix, dist.TCPStore(host, port, is_master=False, timeout=timeout,
+                                                   wait_for_workers=False))
+    dist.init_process_group("gloo", store=store, rank=rank, world_size=world, timeout=timeout)
+    _helper_fault(rank)
+    wrong = os.environ.get(_ENV + "FAULT", "") == f"wrong@{rank}"
+    if dry:  # no GPU: the orchestration only (CPU tests)
+        t = torch.tensor([float(rank + 1) + (1.0 if wrong else 0.0)], dtype=torch.float64)
+        dist.all_reduce(t)
+        ok = t.item() == world * (world + 1) / 2
+        msg = None if ok else f"gloo all-reduce gave {t.item()}"
+    else:
+        from ..ops import Reducer
+        from .xrank import close_channels, open_channel
+        idx = int(os.environ[_ENV + "DEVICE"])
+        dev = torch.device("cuda", idx)
+        torch.cuda.set_device(dev)
+        n = int(os.environ.get(_ENV + "ELEMENTS", str(1 << 20)))
+        x = torch.full((n,), float(rank + 1), dtype=torch.float64, device=dev)
+        if wrong:
+            x[0] += 1.0
+        out = torch.zeros(3, dtype=torch.float64, device=dev)
+        ch = open_channel(dev, timeout_s=5.0)  # collective over the helpers' group
+        red = Reducer(dev)
+        b = red.bind(x, "sum", torch.float64, out=out[:1], xrank=ch)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        for i in range(3):  # epochs 1..3: both mailbox parities
+            b.launch(s, out[i:i + 1].data_ptr())
+        torch.cuda.synchronize(dev)
+        expect = float(n) * world * (world + 1) / 2
+        got = out.tolist()
+        errs = (int(ch.error()), int(red.ws.error()))
+        ok = errs == (0, 0) and all(v == expect for v in got)
+        msg = None if ok else f"results {got} (expected {expect}), channel / fan-in error words {errs}"
+        del b
+        close_channels([ch], dev)  # collective: nobody unmaps a mailbox a peer still polls
+    dist.barrier()
+    dist.destroy_process_group()
+    if msg:
+        print(f"[canary] rank {rank}: {msg}", file=sys.stderr, flush=True)
+    return 0 if ok else 1
+
+
+def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int = 1 << 20) -> Optional[str]:
+    """Collective over the default process group: None if every rank's helper ran the fused
+    exchange correctly, else the agreed reason ("rank r: ..." for each failing rank). World 1 maps
+    no peer memory: None without a helper. ``dry`` (CPU tests): helpers rendezvous and all-reduce
+    over gloo only."""
+    import torch.distributed as dist
+    if ctx.world_size == 1 or not dist.is_initialized():
+        return None
+    token = [secrets.token_hex(8) if ctx.rank == 0 else None]
+    dist.broadcast_object_list(token, src=0)
+    env = dict(os.environ)
+    env.update({_ENV + "RANK": str(ctx.rank), _ENV + "WORLD": str(ctx.world_size),
+                _ENV + "ADDR": os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                _ENV + "PORT": os.environ.get("MASTER_PORT", ""), _ENV + "PREFIX": f"mireduce_canary/{token[0]}/",
+                _ENV + "DEVICE": str(ctx.device.index if ctx.device.index is not None else 0),
+                _ENV + "TIMEOUT": str(max(10.0, timeout_s - 10.0)), _ENV + "ELEMENTS": str(elements)})
+    if dry:
+        env[_ENV + "DRY"] = "1"
+    mine = None
+    if not env[_ENV + "PORT"]:
+        mine = "no rendezvous store address (MASTER_PORT unset)"
+    else:
+        try:
+            p = subprocess.Popen([sys.executable, "-m", "cuda_mpi_reductions_amd.parallel.canary"], env=env,
+                                 stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                                 cwd=os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+            try:
+                _, err = p.communicate(timeout=timeout_s)
+                if p.returncode != 0:
+                    tail = " | ".join(ln for ln in (err or "").strip().splitlines()[-2:])
+                    mine = f"helper exited with {p.returncode}: {tail}"[:300]
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.communicate()
+                mine = f"helper did not finish within {timeout_s:g} s"
+        except OSError as e:
+            mine = f"could not start the helper: {e}"[:300]
+    verdicts = [None] * ctx.world_size
+    dist.all_gather_object(verdicts, mine)
+    bad = [f"rank {r}: {m}" for r, m in enumerate(verdicts) if m]
+    return "; ".join(bad)[:600] if bad else None
+
+
+if __name__ == "__main__":
+    sys.exit(_helper())

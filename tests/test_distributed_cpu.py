@@ -176,6 +176,35 @@ def test_bench_external_launcher_recorded(tmp_path):
     assert d["launcher"] == "external" and d["ranks_seen"] == 2 and "decomposition" not in d
 
 
+def canary_case(rank, world):
+    from cuda_mpi_reductions_amd.parallel import dist as pdist
+    from cuda_mpi_reductions_amd.parallel.canary import fused_canary
+    ctx = pdist.init(device_type="cpu")
+    res = {"ok": fused_canary(ctx, timeout_s=60, dry=True)}
+    os.environ["MIREDUCE_CANARY_FAULT"] = "abort@1"
+    res["abort"] = fused_canary(ctx, timeout_s=25, dry=True)
+    os.environ["MIREDUCE_CANARY_FAULT"] = "wrong@0"
+    res["wrong"] = fused_canary(ctx, timeout_s=60, dry=True)
+    os.environ.pop("MIREDUCE_CANARY_FAULT")
+    res["again"] = fused_canary(ctx, timeout_s=60, dry=True)  # a fresh key prefix per call
+    pdist.shutdown(ctx)
+    return res
+
+
+def test_fused_canary_orchestration_three_ranks():
+    # parallel/canary.py on CPU ranks (dry helpers: rendezvous over the job's store + a gloo
+    # all-reduce): a helper that aborts or computes a wrong value makes EVERY rank get the same
+    # failure verdict naming it, and the benchmark processes themselves carry on
+    out = _spawn("canary_case", 3)
+    verdicts = list(out.values())
+    assert all(isinstance(v, dict) for v in verdicts), verdicts
+    assert all(v == verdicts[0] for v in verdicts)  # agreed
+    v = verdicts[0]
+    assert v["ok"] is None and v["again"] is None
+    assert v["abort"] is not None and "rank 1: helper exited with" in v["abort"], v["abort"]
+    assert v["wrong"] is not None and "gloo all-reduce gave" in v["wrong"], v["wrong"]
+
+
 def test_bench_vector_config1_two_cpu_ranks(tmp_path):
     # BASELINE config 1 through bench.py: 1M int32 SUM, element-wise reduce to root, 2 CPU ranks.
     r = torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "1",

@@ -431,3 +431,23 @@ def test_bench_replay_probe_failure_goes_eager_one_gpu(tmp_path):
     d = _json(r)
     assert d["verified"] is True
     assert d["config"]["launch"].startswith("eager (captured replay probe failed: rank 0: "), d["config"]["launch"]
+
+
+@pytest.mark.parametrize("fault", [None, "abort@1"])
+def test_bench_fused_canary_two_ranks_one_gpu(tmp_path, monkeypatch, fault):
+    # the fused finish's canary (parallel/canary.py) with real GPU helpers (two ranks sharing the
+    # GPU): clean -> fused chosen; a helper that aborts -> every rank declines the fused finish and
+    # the headline is still measured and verified over the other combine
+    monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    if fault:
+        monkeypatch.setenv("MIREDUCE_CANARY_FAULT", fault)
+    r = torchrun(2, [BENCH, "--no-vector-extras", "--no-candidates", "--gpus", "2", "--backend", "gloo", "--steps", "6",
+                     "--warmup", "2", "--elements", "20000003", "--canary-timeout", "40"], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json(r)
+    assert d["verified"] is True and d["n_gpus"] == 2
+    if fault:
+        assert d["config"]["collective"] == "rccl"
+        assert "canary: rank 1: helper exited with" in d["config"]["collective_choice"], d["config"]["collective_choice"]
+    else:
+        assert d["config"]["collective"] == "fused", d["config"]["collective_choice"]

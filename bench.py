@@ -396,7 +396,8 @@ def _checksum(wl, holder: bool) -> float:
     return float(wl.result().to(torch.float64).sum().item()) if holder else 0.0
 
 
-def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES, out: "dict | None" = None, progress=None) -> dict:
+def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES, out: "dict | None" = None, progress=None,
+                   canary: bool = True, canary_timeout: float = 90.0) -> dict:
     """reduce.c's own measurement on this job's GPUs, next to the scalar headline, in reduce.c's
     shape: element-wise INT and DOUBLE MAX / MIN / SUM of 2 GiB of total data each (NUM_INTS /
     NUM_DOUBLES, mpi/constants.h:1-2) to root 0 (MPI_Reduce, reduce.c:76,90), one warm-up SUM per
@@ -425,6 +426,15 @@ def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES, out: "dict | None" = No
     table, rows = [], {}
     out["table"], out["rows"] = table, rows
     holder = ctx.rank == 0
+    direct_ok = True
+    if ctx.world_size > 1 and canary:  # the peer mapping runs in throw-away helpers first
+        from cuda_mpi_reductions_amd.parallel.canary import direct_canary
+        why = direct_canary(ctx, timeout_s=canary_timeout)
+        if why is not None:
+            direct_ok = False
+            out["direct_canary"] = why
+            impls = tuple(i for i in impls if i != "direct")
+            table.append({"impl": "direct", "error": f"canary: {why}"[:300]})
     for impl in impls:
         if impl == "rccl" and ctx.world_size == 1:
             table += [{"dtype": dt, "op": op.upper(), "impl": impl, "gibps": None, "note": WORLD1_RCCL}
@@ -494,7 +504,7 @@ def _vector_extras(ctx, retries: int = REDUCE_C_RETRIES, out: "dict | None" = No
         out["note"] = ("world 1: RCCL rows are null (no work); direct is one local send -> receive pass (what "
                        "MPI_Reduce does on one rank); tools/scaling.py keeps N=1 out of the results files")
     if ctx.world_size > 1:
-        out["peer_read"] = _peer_read_extra(ctx)
+        out["peer_read"] = _peer_read_extra(ctx) if direct_ok else {"error": "skipped: the direct canary failed"}
     return out
 
 
@@ -1188,7 +1198,8 @@ def main(argv=None) -> int:
         rearm()
     if args.vector_extras and dev.type == "cuda" and cfg.name == NORTH_STAR:
         extras["reduce_c_vector"] = {}
-        _vector_extras(ctx, out=extras["reduce_c_vector"], progress=rearm)
+        _vector_extras(ctx, out=extras["reduce_c_vector"], progress=rearm, canary=args.canary,
+                       canary_timeout=args.canary_timeout)
         rearm()
     if args.compare_torch and dev.type == "cuda":
         extras["torch_gbps"] = round(_time_torch_reduction(wl, K, W, ctx), 3)

@@ -29,7 +29,7 @@ import subprocess
 import sys
 from typing import Optional
 
-__all__ = ["fused_canary"]
+__all__ = ["fused_canary", "direct_canary"]
 
 _ENV = "MIREDUCE_CANARY_"
 
@@ -68,6 +68,27 @@ def _helper() -> int:
         dist.all_reduce(t)
         ok = t.item() == world * (world + 1) / 2
         msg = None if ok else f"gloo all-reduce gave {t.item()}"
+    elif os.environ.get(_ENV + "KIND", "fused") == "direct":
+        # the direct one-kernel collective (parallel/direct.py): registered buffers mapped by every
+        # rank, an all-reduce and a reduce to root 0, a peer-read pass, error words, close
+        from .direct import DirectComm
+        idx = int(os.environ[_ENV + "DEVICE"])
+        dev = torch.device("cuda", idx)
+        torch.cuda.set_device(dev)
+        n = int(os.environ.get(_ENV + "ELEMENTS", str(1 << 20)))
+        t = torch.full((n,), float(rank + 1), dtype=torch.float64, device=dev)
+        if wrong:
+            t[0] += 1.0
+        comm = DirectComm(dev, n * 8, timeout_s=5.0)
+        expect = world * (world + 1) / 2
+        a = comm.allreduce(t.clone(), "sum")
+        r0 = comm.reduce(t.clone(), "sum", root=0)
+        comm.read_peers(n * 8)
+        torch.cuda.synchronize(dev)
+        err = comm.check()  # collective
+        ok = err is None and bool((a == expect).all().item()) and (rank != 0 or bool((r0 == expect).all().item()))
+        msg = None if ok else f"direct all-reduce / reduce wrong or device error ({err})"
+        comm.close()  # collective
     else:
         from ..ops import Reducer
         from .xrank import close_channels, open_channel
@@ -100,11 +121,13 @@ def _helper() -> int:
     return 0 if ok else 1
 
 
-def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int = 1 << 20) -> Optional[str]:
-    """Collective over the default process group: None if every rank's helper ran the fused
-    exchange correctly, else the agreed reason ("rank r: ..." for each failing rank). World 1 maps
-    no peer memory: None without a helper. ``dry`` (CPU tests): helpers rendezvous and all-reduce
-    over gloo only."""
+def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int = 1 << 20,
+                 kind: str = "fused") -> Optional[str]:
+    """Collective over the default process group: None if every rank's helper ran the exchange
+    correctly, else the agreed reason ("rank r: ..." for each failing rank). ``kind``: ``fused``
+    (the fused cross-rank finish) or ``direct`` (the direct one-kernel collective and the peer-read
+    probe, parallel/direct.py). World 1 maps no peer memory: None without a helper. ``dry`` (CPU
+    tests): helpers rendezvous and all-reduce over gloo only."""
     import torch.distributed as dist
     if ctx.world_size == 1 or not dist.is_initialized():
         return None
@@ -115,7 +138,8 @@ def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int 
                 _ENV + "ADDR": os.environ.get("MASTER_ADDR", "127.0.0.1"),
                 _ENV + "PORT": os.environ.get("MASTER_PORT", ""), _ENV + "PREFIX": f"mireduce_canary/{token[0]}/",
                 _ENV + "DEVICE": str(ctx.device.index if ctx.device.index is not None else 0),
-                _ENV + "TIMEOUT": str(max(10.0, timeout_s - 10.0)), _ENV + "ELEMENTS": str(elements)})
+                _ENV + "TIMEOUT": str(max(10.0, timeout_s - 10.0)), _ENV + "ELEMENTS": str(elements),
+                _ENV + "KIND": kind})
     if dry:
         env[_ENV + "DRY"] = "1"
     mine = None
@@ -141,6 +165,12 @@ def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int 
     dist.all_gather_object(verdicts, mine)
     bad = [f"rank {r}: {m}" for r, m in enumerate(verdicts) if m]
     return "; ".join(bad)[:600] if bad else None
+
+
+def direct_canary(ctx, timeout_s: float = 90.0, dry: bool = False) -> Optional[str]:
+    """:func:`fused_canary` for the direct one-kernel collective (bench.py runs it before its
+    reduce.c table's direct rows and the xGMI peer-read probe)."""
+    return fused_canary(ctx, timeout_s=timeout_s, dry=dry, kind="direct")
 
 
 if __name__ == "__main__":

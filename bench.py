@@ -939,6 +939,7 @@ def _decompose(wl, ctx, args, fault, headline_ms: float) -> dict:
     same = bool((written == written[-1]).all().item()) if written.numel() else True
     same = -pdist.max_over_ranks(-float(same), ctx) > 0.5  # every slot holds this rank's partial
     err = wl.check()
+    wait = _exchange_wait(wl, ctx, args, fault) if getattr(wl, "collective", None) == "fused" and wl.channels else None
     loc_max, loc_min = m["elapsed"] / K * 1e3, m["elapsed_min"] / K * 1e3
     out = {"local_ms_per_step": round(loc_max, 5), "local_ms_min": round(loc_min, 5), "local_ms_max": round(loc_max, 5),
            "local_gbps": round(wl.bytes_total / (loc_max * 1e-3) / 1e9, 3),
@@ -946,9 +947,47 @@ def _decompose(wl, ctx, args, fault, headline_ms: float) -> dict:
            "exchange_us_per_step": round((headline_ms - loc_max) * 1e3, 3),
            "scaling_efficiency_vs_local": round(loc_max / headline_ms, 5) if headline_ms > 0 else None,
            "local_launch": m["launch"], "steps": K, "consistent": same and err is None}
+    if wait is not None:
+        out["exchange_wait_us"] = wait
     if err:
         out["error"] = err
     return out
+
+
+def _exchange_wait(wl, ctx, args, fault, cap: int = 4096) -> "dict | None":
+    """Device-side timing of the fused exchange (XrankChannel.set_stamps): for every step of a
+    short serial graph-replayed run, the finisher's wall clock at its first push and when every
+    peer's partial had landed. Per rank the median / p90 of that wait (us); the rank that waits least
+    arrived last (its wait is the local poll of already-landed partials), the one that waits most
+    pays the skew of the local reductions plus the xGMI latency. None if unsupported."""
+    ch = wl.channels[0]
+    if not hasattr(ch, "set_stamps"):
+        return None
+    K, W = min(args.steps, cap - 8), 2
+    st = torch.zeros(2 * cap, dtype=torch.int64, device=ctx.device)
+    err = None
+    try:
+        ch.set_stamps(st.data_ptr(), cap)
+        _measure(wl, wl.new_slots(W + K), ctx, args, fault, serial=True, warmup=W, site="extras")
+    except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
+        err = f"{type(e).__name__}: {e}"[:200]
+    finally:
+        ch.set_stamps(0, 1)
+    s = st.view(-1, 2).cpu()
+    s = s[s[:, 0] > 0]
+    us = ((s[:, 1] - s[:, 0]).to(torch.float64) / ch.ticks_per_us).sort().values
+    med = float(us[len(us) // 2]) if len(us) else float("nan")
+    p90 = float(us[int(0.9 * (len(us) - 1))]) if len(us) else float("nan")
+    rows = [None] * ctx.world_size
+    mine = {"median": round(med, 3), "p90": round(p90, 3), "launches": int(len(us)), "error": err}
+    if ctx.world_size > 1:
+        torch.distributed.all_gather_object(rows, mine)
+    else:
+        rows = [mine]
+    meds = [r["median"] for r in rows]
+    return {"median_by_rank": meds, "p90_by_rank": [r["p90"] for r in rows], "min_rank_median": min(meds),
+            "max_rank_median": max(meds), "launches": min(r["launches"] for r in rows),
+            "errors": [r["error"] for r in rows if r["error"]] or None}
 
 
 def _tune_plan(wl, ctx, args, fault, kernel, cands) -> "tuple[KernelConfig, dict]":

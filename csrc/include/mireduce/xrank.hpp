@@ -53,6 +53,10 @@ struct XrankDesc {
   int rank;
   int world;
   uint64_t timeout_ticks;   // wall_clock64() ticks
+  // Exchange timing (set_stamps; null = off): the finisher records, per launch e, the wall clock
+  // at its first push and when every peer's partial had landed, at stamps[2 * (e & stamp_mask)].
+  uint64_t* stamps;
+  unsigned stamp_mask;
 };
 
 using IpcHandleBytes = std::array<char, sizeof(hipIpcMemHandle_t)>;
@@ -78,12 +82,19 @@ class XrankChannel {
   unsigned error() const;
   unsigned epoch() const;
   void clear_error();
+  // Exchange timing: `stamps` (device, 2 * cap uint64, cap a power of two; nullptr = off) receives
+  // (push, all peers landed) wall-clock ticks of launch e at [2 * (e % cap)]. Synchronous; no launch
+  // on this channel may be running.
+  void set_stamps(uint64_t* stamps, unsigned cap);
+  // Ticks per microsecond of the device wall clock (wall_clock64()).
+  double ticks_per_us() const { return ticks_per_us_; }
 
  private:
   int device_ = 0;
   int rank_ = 0, world_ = 1;
   bool connected_ = false;
   double timeout_s_ = 2.0;
+  double ticks_per_us_ = 100.0;
   uint64_t* mbox_ = nullptr;     // own mailbox (uncached)
   unsigned* counters_ = nullptr; // [0] epoch, [1] error
   XrankDesc* desc_dev_ = nullptr;

@@ -158,6 +158,8 @@ struct XrankLane {
   uint64_t* peer;       // rank `lane`'s mailbox (lane < world, lane != rank)
   const uint64_t* own;  // this rank's mailbox
   uint64_t limit;       // wait bound in wall-clock ticks (0 after a sticky error: look once)
+  uint64_t* stamps;     // exchange timing (XrankDesc::stamps; null: off)
+  unsigned stamp_mask;
   unsigned e;           // this launch's epoch
   int world, rank;
 };
@@ -170,6 +172,8 @@ __device__ __forceinline__ XrankLane xrank_prefetch(const XrankDesc* d, unsigned
   x.peer = d->peer_mbox[lane < kMaxXrankRanks ? lane : 0];
   x.own = d->own_mbox;
   x.limit = err ? 0 : d->timeout_ticks;  // a sticky error means a peer is gone: do not wait
+  x.stamps = d->stamps;
+  x.stamp_mask = d->stamp_mask;
   x.e = e;
   return x;
 }
@@ -187,6 +191,7 @@ __device__ __forceinline__ AccT xrank_finish(const XrankDesc* d, const XrankLane
   const uint64_t bits = to_bits64(t);
   AccT v = OpT::template identity<AccT>();
   bool bad = false;
+  const uint64_t t_push = x.stamps ? static_cast<uint64_t>(wall_clock64()) : 0;
   if (lane < x.world && lane != x.rank) {
     uint64_t* dst = x.peer + (parity + x.rank) * 2;
     __hip_atomic_store(dst, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -215,7 +220,12 @@ __device__ __forceinline__ AccT xrank_finish(const XrankDesc* d, const XrankLane
     v = t;  // this rank's own partial never leaves the register file
   }
   if (lane == 0) __hip_atomic_store(d->epoch, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  failed = __ballot(bad) != 0;
+  failed = __ballot(bad) != 0;  // (also: every lane's poll has ended)
+  if (x.stamps && lane == 0) {
+    uint64_t* st = x.stamps + 2 * static_cast<uint64_t>(e & x.stamp_mask);
+    st[0] = t_push;
+    st[1] = static_cast<uint64_t>(wall_clock64());
+  }
   return wave_reduce<OpT>(v);
 }
 

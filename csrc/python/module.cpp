@@ -216,7 +216,10 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("world", &XrankChannel::world)
       .def("error", &XrankChannel::error)
       .def("epoch", &XrankChannel::epoch)
-      .def("clear_error", &XrankChannel::clear_error);
+      .def("clear_error", &XrankChannel::clear_error)
+      .def("set_stamps", [](XrankChannel& c, uintptr_t p, unsigned cap) { c.set_stamps(as_ptr<uint64_t>(p), cap); },
+           py::arg("stamps_ptr"), py::arg("cap"))
+      .def_property_readonly("ticks_per_us", &XrankChannel::ticks_per_us);
   m.attr("XRANK_MAX_RANKS") = kMaxXrankRanks;
 
   // bench.py's one result line, printed exactly once even if the process is killed (final_line.hpp).

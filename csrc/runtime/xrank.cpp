@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <cstddef>
 #include <cstring>
 
 #include "mireduce/check.hpp"
@@ -82,6 +83,9 @@ void XrankChannel::connect(int rank, int world, const std::vector<IpcHandleBytes
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) != hipSuccess || khz <= 0)
     khz = 100000;  // gfx950: 100 MHz
   d.timeout_ticks = static_cast<uint64_t>(timeout_s_ * 1e3 * khz);
+  ticks_per_us_ = khz * 1e-3;
+  d.stamps = nullptr;
+  d.stamp_mask = 0;
   MIREDUCE_HIP_THROW(hipMemcpy(desc_dev_, &d, sizeof d, hipMemcpyHostToDevice));
   MIREDUCE_HIP_THROW(hipDeviceSynchronize());
   rank_ = rank;
@@ -101,6 +105,23 @@ unsigned XrankChannel::epoch() const {
   DeviceGuard g(device_);
   MIREDUCE_HIP_THROW(hipMemcpy(&v, counters_, sizeof v, hipMemcpyDeviceToHost));
   return v;
+}
+
+void XrankChannel::set_stamps(uint64_t* stamps, unsigned cap) {
+  MIREDUCE_REQUIRE(connected_, "XrankChannel::set_stamps: not connected");
+  MIREDUCE_REQUIRE(stamps == nullptr || (cap > 0 && (cap & (cap - 1)) == 0),
+                   "XrankChannel::set_stamps: capacity must be a power of two");
+  DeviceGuard g(device_);
+  struct {
+    uint64_t* p;
+    unsigned m;
+  } f{stamps, stamps ? cap - 1 : 0u};
+  static_assert(offsetof(XrankDesc, stamp_mask) == offsetof(XrankDesc, stamps) + sizeof(uint64_t*),
+                "stamp fields must be adjacent");
+  MIREDUCE_HIP_THROW(hipDeviceSynchronize());
+  MIREDUCE_HIP_THROW(hipMemcpy(reinterpret_cast<char*>(desc_dev_) + offsetof(XrankDesc, stamps), &f,
+                               sizeof(uint64_t*) + sizeof(unsigned), hipMemcpyHostToDevice));
+  MIREDUCE_HIP_THROW(hipDeviceSynchronize());
 }
 
 void XrankChannel::clear_error() {

@@ -10,6 +10,9 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method threa
   tests/test_xrank_gpu.py::test_bench_replay_probe_and_decomposition_one_gpu \
   tests/test_xrank_gpu.py::test_bench_replay_probe_failure_goes_eager_one_gpu \
   tests/test_xrank_gpu.py::test_fused_world1_matches_torch \
+  tests/test_xrank_gpu.py::test_bench_torchrun_one_rank_graphs_both_modes \
+  tests/test_xrank_gpu.py::test_bench_fused_canary_two_ranks_one_gpu \
+  tests/test_xrank_gpu.py::test_bench_fused_ranks_share_one_gpu \
   tests/test_apps_gpu.py::test_reduce_xgmi_peer_preflight_declines_on_every_rank \
   tests/test_apps_gpu.py::test_reduce_xgmi_scalar_fused > $O/pytest.txt 2>&1 &&
 timeout -k 10 240 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&

@@ -80,6 +80,13 @@ def test_bench_torchrun_one_rank_graphs_both_modes(tmp_path, collective):
     assert ("RCCL" in combine) if collective == "rccl" else ("fused" in combine)
     assert d["native_source_hash"] and d["native_source_hash"] != "unknown"
     assert d["config"]["topology"] == {"hosts": 1, "gpus": 1, "ranks_per_gpu": 1, "peer_access": "n/a (one GPU)"}
+    dec = d["decomposition"]  # round 4: the step without its combine, and (fused) the device-timed exchange
+    assert dec["consistent"] is True and dec["local_ms_per_step"] > 0
+    if collective == "fused":
+        w = dec["exchange_wait_us"]
+        assert w["launches"] >= 8 and w["errors"] is None and 0 <= w["min_rank_median"] < 50, w
+    else:
+        assert "exchange_wait_us" not in dec
 
 
 def test_bench_fused_two_lanes(tmp_path):

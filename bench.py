@@ -73,10 +73,10 @@ def _launch_ranks(argv: list) -> "int | None":
     Reference: reduce.c reports the rank count it ran with (NODES = commSize, mpi/reduce.c:81,95);
     the job shape comes from the launcher (mpi/ccni_vn.sh:7)."""
     pre = argparse.ArgumentParser(add_help=False)
-    pre.add_argument("--gpus", type=int, default=1)
+    pre.add_argument("--gpus", type=int, default=None)
     known, _ = pre.parse_known_args(argv)
-    n = known.gpus
     ws = os.environ.get("WORLD_SIZE")
+    n = known.gpus if known.gpus is not None else int(ws or 1)  # no --gpus: the launcher's shape
     if ws is not None:
         if int(ws) != n:
             if os.environ.get("RANK", "0") == "0":
@@ -145,7 +145,9 @@ RELEASE_SETTLE_S = 0.5  # idle after handing GB-sized buffers back to the driver
 
 def parse_args(argv=None):
     p = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (ranks) of the job; default: WORLD_SIZE under a launcher, else 1. Without a "
+                        "launcher, N > 1 starts N ranks (a child torch.distributed.run)")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default=NORTH_STAR, choices=sorted(CONFIGS))
@@ -1042,6 +1044,8 @@ def main(argv=None) -> int:
     fault = FaultInjector.from_flag_or_env(args.inject_fault)
     ctx = pdist.init(backend=None if args.backend == "auto" else args.backend, device_type=device_type,
                      timeout_s=args.pg_timeout)
+    if args.gpus is None:
+        args.gpus = ctx.world_size
     if args.gpus != ctx.world_size:  # (main() called directly; the __main__ launcher checks this first)
         if ctx.is_root:
             _emit({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": args.gpus, "verified": None,

@@ -63,7 +63,7 @@ def test_decomposition_columns(tmp_path):
     assert per_n[8]["skew_us"] == 2.0 and abs(per_n[8]["vs_local"] - 0.8985) < 1e-12
     assert per_n[1]["local_ms"] is None
     text = scaling.write({("xgmi_1b_double_sum", "DOUBLE", "SUM"): per_n}, str(tmp_path))
-    assert "exchange us/step" in text and "| 0.1410 | 16.00 | 2.00 | 0.899 |" in text
+    assert "exchange us/step" in text and "| 0.1410 | 16.00 | 2.00 | 0.899 |  |" in text
 
 
 def test_cli_without_results_fails(tmp_path):

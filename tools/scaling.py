@@ -25,7 +25,9 @@ Efficiency = value(N) / (N * value(1)): the whole-node bandwidth of N GPUs again
 Where an N-GPU step's time goes (bench.py's ``decomposition``, averaged like the headline): the
 slowest rank's local reduce (ms/step, the same kernel without the combine), the cross-rank
 exchange (us/step = headline - local), the inter-GPU skew of the local work (us/step) and
-``vs local`` = local time / step time (1.0 = the combine is free). So a loss of efficiency at N=8
+``vs local`` = local time / step time (1.0 = the combine is free) and, for the fused finish, the
+device-timed wait from a rank's push to all partials landed (the least waiting rank ~ the local
+poll, the most waiting ~ skew + xGMI latency). So a loss of efficiency at N=8
 splits into the per-GPU rate at the smaller shard (local ms vs N=1), the exchange and the skew.
 
     python tools/scaling.py SCALE_r01.json bench_*.json --out results/scaling
@@ -103,11 +105,16 @@ DECOMP = (("local_ms", "local_ms_per_step"), ("exchange_us", "exchange_us_per_st
 
 
 def _decomposition(rs) -> dict:
-    """Mean of each bench.py ``decomposition`` field over the runs that carry it (None if none do)."""
+    """Mean of each bench.py ``decomposition`` field over the runs that carry it (None if none do),
+    plus the device-timed fused exchange wait (``exchange_wait_us``: least / most waiting rank)."""
     out = {}
+    decs = [d for d in (r.get("decomposition") or {} for r in rs) if isinstance(d, dict)]
     for name, field in DECOMP:
-        vals = [float(d[field]) for d in (r.get("decomposition") or {} for r in rs)
-                if isinstance(d, dict) and d.get(field) is not None]
+        vals = [float(d[field]) for d in decs if d.get(field) is not None]
+        out[name] = sum(vals) / len(vals) if vals else None
+    for name, field in (("wait_min_us", "min_rank_median"), ("wait_max_us", "max_rank_median")):
+        vals = [float(d["exchange_wait_us"][field]) for d in decs
+                if isinstance(d.get("exchange_wait_us"), dict) and d["exchange_wait_us"].get(field) is not None]
         out[name] = sum(vals) / len(vals) if vals else None
     return out
 
@@ -180,8 +187,8 @@ def efficiency(per_n):
 def write(summary, out_dir):
     os.makedirs(out_dir, exist_ok=True)
     md = ["| config | dtype | op | N | GB/s (whole node) | ms/step | speed-up | efficiency | runs "
-          "| local ms/step | exchange us/step | skew us/step | vs local |",
-          "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
+          "| local ms/step | exchange us/step | skew us/step | vs local | fused wait us (min-max rank) |",
+          "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for (model, dt, op), per_n in sorted(summary.items()):
         with open(os.path.join(out_dir, f"{dt}_{op}.txt"), "w") as f:
             f.write("\n")  # getAvgs.sh:5-6 starts each results file with a blank line
@@ -195,8 +202,9 @@ def write(summary, out_dir):
             ef = "" if e is None else "%.1f %%" % (100 * e)
             dec = ["" if v.get(f) is None else fmt % v[f] for f, fmt in
                    (("local_ms", "%.4f"), ("exchange_us", "%.2f"), ("skew_us", "%.2f"), ("vs_local", "%.3f"))]
+            wait = "" if v.get("wait_min_us") is None else "%.2f-%.2f" % (v["wait_min_us"], v["wait_max_us"])
             md.append(f"| {model} | {dt} | {op} | {n} | {v['gbps']:.1f} | {ms} | {sp} | {ef} | {v['runs']} | "
-                      + " | ".join(dec) + " |")
+                      + " | ".join(dec) + f" | {wait} |")
     text = "\n".join(md) + "\n"
     with open(os.path.join(out_dir, "scaling.md"), "w") as f:
         f.write(text)

@@ -445,14 +445,20 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   for (int u = 1; u < UNROLL; ++u) acc[0] = OpT::apply(acc[0], acc[u]);
 
   // Fused cross-rank finish: this launch's epoch (counter + 1; only the finishing workgroup bumps
-  // the counter, and it runs last) and the sticky error word, loaded by every workgroup after its
-  // streaming body (not before: extra live values there change hipcc's load scheduling of the
-  // body — 76 -> 60 VGPRs and 7.3 -> 5.1 TB/s at 512 x 16) so the finisher pays no atomic round trip.
+  // the counter, and it runs last) and the sticky error word. Only the finisher needs them, and it
+  // loads them where their latency hides: the polled fan-in's finisher (known up front) right after
+  // publishing its own partial, under its poll of the others'; a one-workgroup launch just before
+  // the exchange. Only the ticketed fan-ins, whose finisher is whoever arrives last, load them in
+  // every workgroup — after the streaming body (not before: extra live values there change hipcc's
+  // load scheduling of the body — 76 -> 60 VGPRs and 7.3 -> 5.1 TB/s at 512 x 16). Loading them in
+  // every workgroup of the polled fan-in cost each workgroup the loads' round trip before its
+  // block barrier, i.e. ~1.4 us per fused step (bench.py decomposition, round 4).
   unsigned xr_epoch = 0, xr_err = 0;
-  if (a.xrank) {
+  auto load_xr = [&]() {
     xr_epoch = xrank_next_epoch(__hip_atomic_load(a.xrank->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     xr_err = __hip_atomic_load(a.xrank->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  };
+  if (a.xrank && !a.slots && gridDim.x > 1) load_xr();  // ticketed fan-in
 
   AccT v = block_reduce<OpT, AccT, BLOCK>(acc[0], lds);
   AccT* partials = static_cast<AccT*>(a.partials);
@@ -466,6 +472,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   if (gridDim.x == 1) {
     if (threadIdx.x < 64) {
       bool xf = false;
+      if (a.xrank) load_xr();
       if (a.xrank) v = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), v, false, xf);
       if (threadIdx.x == 0) *static_cast<AccT*>(a.out) = xf ? poisoned<OpT, AccT>() : v;
     }
@@ -497,7 +504,10 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     // The finisher: start the cross-rank descriptor loads and the sticky-error load now, they land
     // while it polls.
     XrankLane xl{};
-    if (a.xrank && threadIdx.x < 64) xl = xrank_prefetch(a.xrank, xr_epoch, xr_err);
+    if (a.xrank && threadIdx.x < 64) {
+      load_xr();
+      xl = xrank_prefetch(a.xrank, xr_epoch, xr_err);
+    }
     const unsigned fan_err = __hip_atomic_load(a.fan + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     AccT t = OpT::template identity<AccT>();
     // Bounded like every device-side wait here (all workgroups of this launch always publish, so

@@ -153,8 +153,11 @@ def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int 
             try:
                 _, err = p.communicate(timeout=timeout_s)
                 if p.returncode != 0:
-                    tail = " | ".join(ln for ln in (err or "").strip().splitlines()[-2:])
-                    mine = f"helper exited with {p.returncode}: {tail}"[:300]
+                    lines = [ln for ln in (err or "").strip().splitlines() if ln and not ln.startswith("[W")]
+                    tail = " | ".join(lines[-2:])
+                    how = (f"crashed (signal {-p.returncode})" if p.returncode < 0 else
+                           f"exited with {p.returncode}")
+                    mine = f"helper {how}: {tail}"[:300]
             except subprocess.TimeoutExpired:
                 p.kill()
                 p.communicate()
@@ -163,7 +166,10 @@ def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int 
             mine = f"could not start the helper: {e}"[:300]
     verdicts = [None] * ctx.world_size
     dist.all_gather_object(verdicts, mine)
-    bad = [f"rank {r}: {m}" for r, m in enumerate(verdicts) if m]
+    # the root causes first: helpers that crashed or hung, then the ones that only lost a peer
+    first = [f"rank {r}: {m}" for r, m in enumerate(verdicts) if m and ("crashed" in m or "did not finish" in m)]
+    rest = [f"rank {r}: {m}" for r, m in enumerate(verdicts) if m and not ("crashed" in m or "did not finish" in m)]
+    bad = first + rest
     return "; ".join(bad)[:600] if bad else None
 
 

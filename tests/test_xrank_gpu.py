@@ -144,14 +144,15 @@ def test_fused_poison_reaches_every_rank(tmp_path, dt, op):
         "dist.barrier()\n"
         "red.ws.reset(s); ch.clear_error(); torch.cuda.synchronize(); dist.barrier()\n"
         "launch(); torch.cuda.synchronize()\n"
-        f"open(os.path.join({str(tmp_path)!r}, 'r%d' % r), 'w').write(repr((v, fan, xr, out.item(), ch.error())))\n"
+        "import json\n"
+        f"open(os.path.join({str(tmp_path)!r}, 'r%d' % r), 'w').write(json.dumps((v, fan, xr, out.item(), ch.error())))\n"
         "dist.destroy_process_group()\n")
     r = torchrun(2, [str(script)], timeout=240, env={"MIREDUCE_FORCE_DEVICE": "0"})
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     import math
     ident = torch.iinfo(dt).max if op == "min" else 0
     clean = 3 if op == "min" else (3.0 + 4.0) * (1 << 22)
-    res = {k: eval((tmp_path / f"r{k}").read_text()) for k in range(2)}  # noqa: S307 - our own repr
+    res = {k: json.loads((tmp_path / f"r{k}").read_text()) for k in range(2)}
     for k, (v, fan, xr, v2, xr2) in res.items():
         assert (math.isnan(v) if dt.is_floating_point else v == ident), (k, v)
         assert v2 == clean and xr2 == 0, (k, v2, xr2)
@@ -455,6 +456,7 @@ def test_bench_fused_canary_two_ranks_one_gpu(tmp_path, monkeypatch, fault):
     assert d["verified"] is True and d["n_gpus"] == 2
     if fault:
         assert d["config"]["collective"] == "rccl"
-        assert "canary: rank 1: helper exited with" in d["config"]["collective_choice"], d["config"]["collective_choice"]
+        assert "canary: rank 1: helper crashed (signal 6)" in d["config"]["collective_choice"], \
+            d["config"]["collective_choice"]
     else:
         assert d["config"]["collective"] == "fused", d["config"]["collective_choice"]

@@ -46,6 +46,9 @@ struct ReduceConfig {
   // wall-clock ticks before publishing its partial (-1: none).
   int debug_delay_wg = -1;
   uint64_t debug_delay_ticks = 0;
+  // Diagnostic hook (tools/xcd_balance.py): workgroup b writes [3b] the wall clock after its last
+  // streamed tile was consumed, [3b+1] its XCC id, [3b+2] its tile count (device pointer; null: off).
+  uint64_t* debug_wg_stamps = nullptr;
 };
 
 // What the planner chose (printed by the apps, recorded in JSON sidecars).

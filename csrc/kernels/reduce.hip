@@ -310,6 +310,7 @@ static kern::Args make_args(const void* in, const LaunchPlan& p, DType t, const 
   a.fan_bound = cfg.fanin_bound_ticks ? cfg.fanin_bound_ticks : kern::kFanBoundTicks;
   a.delay_wg = cfg.debug_delay_wg;
   a.delay_ticks = cfg.debug_delay_ticks;
+  a.wg_stamps = cfg.debug_wg_stamps;
   a.head_ptr = in;
   a.body = static_cast<const char*>(in) + p.head * dtype_size(t);
   a.head = p.head;

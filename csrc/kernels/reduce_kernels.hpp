@@ -87,6 +87,7 @@ struct Args {
                            // tiles split evenly over ALL workgroups (no one-tile tail on a few)
   int delay_wg;            // test hook (ReduceConfig::debug_delay_wg): this workgroup sleeps
   uint64_t delay_ticks;    // delay_ticks before publishing its partial; -1 = none
+  uint64_t* wg_stamps;     // diagnostic (ReduceConfig::debug_wg_stamps): per-workgroup end stamps
 };
 
 // Polled fan-in: a published partial is two 8-byte words (epoch << 32 | 32 data bits), where the
@@ -443,6 +444,16 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   }
 #pragma unroll
   for (int u = 1; u < UNROLL; ++u) acc[0] = OpT::apply(acc[0], acc[u]);
+  if (a.wg_stamps && threadIdx.x == 0) {  // diagnostic: when this workgroup's streaming ended
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t t_end = static_cast<uint64_t>(wall_clock64());
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uint64_t* st = a.wg_stamps + 3 * static_cast<uint64_t>(blockIdx.x);
+    st[0] = t_end;
+    st[1] = xcc & 0xfu;
+    st[2] = a.contig ? t1 - t0 : (t1 > t0 ? (t1 - t0 + step - 1) / step : 0);
+  }
 
   // Fused cross-rank finish: this launch's epoch (counter + 1; only the finishing workgroup bumps
   // the counter, and it runs last) and the sticky error word. Only the finisher needs them, and it

@@ -276,9 +276,10 @@ PYBIND11_MODULE(_C, m) {
       [](Workspace& ws, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out,
          uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks, int groups,
          int policy, bool single_pass, int pipeline, uint64_t fanin_bound_ticks, int debug_delay_wg,
-         uint64_t debug_delay_ticks, int window, uintptr_t xrank) {
+         uint64_t debug_delay_ticks, int window, uintptr_t xrank, uintptr_t wg_stamps) {
         ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline, window);
         cfg.xrank = as_ptr<const void>(xrank);
+        cfg.debug_wg_stamps = as_ptr<uint64_t>(wg_stamps);
         cfg.fanin_bound_ticks = fanin_bound_ticks;
         cfg.debug_delay_wg = debug_delay_wg;
         cfg.debug_delay_ticks = debug_delay_ticks;
@@ -292,7 +293,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("unroll") = 0, py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0,
       py::arg("groups") = 0, py::arg("policy") = -1, py::arg("single_pass") = true,
       py::arg("pipeline") = -1, py::arg("fanin_bound_ticks") = 0, py::arg("debug_delay_wg") = -1,
-      py::arg("debug_delay_ticks") = 0, py::arg("window") = -1, py::arg("xrank") = 0);
+      py::arg("debug_delay_ticks") = 0, py::arg("window") = -1, py::arg("xrank") = 0, py::arg("wg_stamps") = 0);
 
   m.def(
       "plan",

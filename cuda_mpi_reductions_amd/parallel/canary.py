@@ -18,7 +18,8 @@ Reference: the vendored simpleP2P checks peer access and then actually exercises
 (cuda/C/src/simpleP2P/simpleP2P.cu:250-275,330-350).
 
 ``python -m cuda_mpi_reductions_amd.parallel.canary`` is the helper (its parameters come from
-``MIREDUCE_CANARY_*`` environment variables set by :func:`fused_canary`).
+``MIREDUCE_CANARY_*`` environment variables set by :func:`fused_canary`). Ranks sharing one GPU map
+no other GPU's memory, so there the canary is skipped unless ``MIREDUCE_CANARY_FORCE=1``.
 """
 from __future__ import annotations
 
@@ -131,6 +132,15 @@ def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int 
     import torch.distributed as dist
     if ctx.world_size == 1 or not dist.is_initialized():
         return None
+    if not dry and os.environ.get(_ENV + "FORCE") != "1":
+        # The canary guards the mapping of ANOTHER GPU's memory. Ranks that share one GPU (the
+        # one-GPU rehearsals) map their own device's memory only — and a helper per rank would
+        # double the processes holding that GPU (the pool allows 16 per GPU; 8 ranks + 8 helpers
+        # + the test runner is 17). MIREDUCE_CANARY_FORCE=1 runs it anyway (its GPU tests).
+        from .topology import peer_map  # collective; cached, open_channel asks the same
+        idx = ctx.device.index if ctx.device.index is not None else 0
+        if peer_map(idx).ranks_per_gpu > 1:
+            return None
     token = [secrets.token_hex(8) if ctx.rank == 0 else None]
     dist.broadcast_object_list(token, src=0)
     env = dict(os.environ)

@@ -23,3 +23,5 @@ rc=$?; echo "prof rc=$rc" >> $O/status.txt
 python3 tools/kernel_gaps.py $O/prof --match reduce_stream --bytes 1e9 --skip 200 > $O/kernel_gaps.txt 2>&1
 find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
 rm -rf $O/prof
+timeout -k 10 240 python -u tools/xcd_balance.py --sizes 125000000,1000000000 --rounds 5 --json $O/xcd_balance.jsonl > $O/xcd_balance.txt 2>&1
+echo "xcd rc=$?" >> $O/status.txt

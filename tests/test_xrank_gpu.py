@@ -447,6 +447,7 @@ def test_bench_fused_canary_two_ranks_one_gpu(tmp_path, monkeypatch, fault):
     # GPU): clean -> fused chosen; a helper that aborts -> every rank declines the fused finish and
     # the headline is still measured and verified over the other combine
     monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    monkeypatch.setenv("MIREDUCE_CANARY_FORCE", "1")  # ranks share the GPU: the canary would be skipped
     if fault:
         monkeypatch.setenv("MIREDUCE_CANARY_FAULT", fault)
     r = torchrun(2, [BENCH, "--no-vector-extras", "--no-candidates", "--gpus", "2", "--backend", "gloo", "--steps", "6",

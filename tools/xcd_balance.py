@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Per-XCD end times of the PRODUCTION streaming kernel (ReduceConfig::debug_wg_stamps).
+
+tools/wg_timeline.hip times re-implementations of the body; this asks the shipped kernel itself:
+every workgroup stamps the wall clock after its last streamed tile was consumed, plus its XCC id
+and tile count. For each size, ``--launches`` back-to-back launches run on one stream and the last
+one's stamps are read; repeated ``--rounds`` times. Printed per round: the spread of workgroup end
+times (min / p50 / p99 / max, us relative to the earliest end) and the mean end per XCC — a
+systematic per-XCD pattern would be the case for an XCD-weighted static split; a random one is
+not. The stamped launch is not timed (the kernel-only time per launch is, from hipEvents).
+
+    python tools/xcd_balance.py --sizes 125000000,1000000000 --rounds 5
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from cuda_mpi_reductions_amd._native import native  # noqa: E402
+from cuda_mpi_reductions_amd.ops import Reducer, dtype_code, fill_, op_code  # noqa: E402
+
+TICKS_PER_US = 100.0  # gfx950 wall clock: 100 MHz
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--sizes", default="125000000,1000000000", help="float64 element counts")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--json", default=None, help="append one JSON object per (size, round)")
+    a = ap.parse_args(argv)
+    C = native()
+    dev = torch.device("cuda", 0)
+    red = Reducer(dev)
+    out = torch.zeros(1, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    for n in (int(float(x)) for x in a.sizes.split(",")):
+        x = torch.empty(n, dtype=torch.float64, device=dev)
+        fill_(x, "uniform", seed=11)
+        stamps = torch.zeros(3 * red.ws.max_grid, dtype=torch.int64, device=dev)
+
+        def launch(st=0):
+            return C.reduce(red.ws, x.data_ptr(), n, dtype_code(x.dtype), op_code("sum"), dtype_code(torch.float64),
+                            out.data_ptr(), stream.cuda_stream, wg_stamps=st)
+        plan = launch()
+        grid = plan["grid"]
+        for r in range(a.rounds):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.launches):
+                launch()
+            e1.record()
+            launch(stamps.data_ptr())
+            torch.cuda.synchronize()
+            us_per = e0.elapsed_time(e1) * 1e3 / a.launches
+            st = stamps[: 3 * grid].view(grid, 3).cpu()
+            end = (st[:, 0] - st[:, 0].min()).double() / TICKS_PER_US
+            xcc = st[:, 1]
+            srt = end.sort().values
+            per = {int(k): round(float(end[xcc == k].mean()), 2) for k in sorted(set(xcc.tolist()))}
+            row = {"n": n, "round": r, "grid": grid, "us_per_launch": round(us_per, 2),
+                   "end_spread_us": {"p50": round(float(srt[grid // 2]), 2),
+                                     "p99": round(float(srt[int(0.99 * (grid - 1))]), 2),
+                                     "max": round(float(srt[-1]), 2)},
+                   "mean_end_by_xcc_us": per, "tiles": sorted(set(st[:, 2].tolist())),
+                   "plan": {k: plan[k] for k in ("block", "unroll", "window", "nontemporal")}}
+            print(json.dumps(row), flush=True)
+            if a.json:
+                with open(a.json, "a") as f:
+                    f.write(json.dumps(row) + "\n")
+        del x
+        torch.cuda.empty_cache()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -918,7 +918,7 @@ def _candidates(wl, ctx, args, fault, fused_ok: bool, capture_failed: bool = Fal
     return out
 
 
-def _decompose(wl, ctx, args, fault, headline_ms: float) -> dict:
+def _decompose(wl, ctx, args, fault, headline_ms: float, allow_graph: bool = True) -> dict:
     """Where the N-GPU step's time goes (an extra, measured after the line is final): the same
     serial, graph-replayed steps with the combine removed (``wl.local_step``: the same kernel plan,
     no channel, no collective), timed per rank.
@@ -936,12 +936,14 @@ def _decompose(wl, ctx, args, fault, headline_ms: float) -> dict:
     simpleMPI.cpp:92-98: local reduce, then the combine)."""
     K, W = args.steps, min(args.warmup, 2)
     slots = wl.new_slots(W + K)
-    m = _measure(wl, slots, ctx, args, fault, serial=True, warmup=W, site="extras", step_fn=wl.local_step)
+    m = _measure(wl, slots, ctx, args, fault, serial=True, warmup=W, site="extras", step_fn=wl.local_step,
+                 allow_graph=allow_graph)
     written = slots[:m["written"]]
     same = bool((written == written[-1]).all().item()) if written.numel() else True
     same = -pdist.max_over_ranks(-float(same), ctx) > 0.5  # every slot holds this rank's partial
     err = wl.check()
-    wait = _exchange_wait(wl, ctx, args, fault) if getattr(wl, "collective", None) == "fused" and wl.channels else None
+    wait = _exchange_wait(wl, ctx, args, fault, allow_graph=allow_graph) \
+        if getattr(wl, "collective", None) == "fused" and wl.channels else None
     loc_max, loc_min = m["elapsed"] / K * 1e3, m["elapsed_min"] / K * 1e3
     out = {"local_ms_per_step": round(loc_max, 5), "local_ms_min": round(loc_min, 5), "local_ms_max": round(loc_max, 5),
            "local_gbps": round(wl.bytes_total / (loc_max * 1e-3) / 1e9, 3),
@@ -956,7 +958,7 @@ def _decompose(wl, ctx, args, fault, headline_ms: float) -> dict:
     return out
 
 
-def _exchange_wait(wl, ctx, args, fault, cap: int = 4096) -> "dict | None":
+def _exchange_wait(wl, ctx, args, fault, cap: int = 4096, allow_graph: bool = True) -> "dict | None":
     """Device-side timing of the fused exchange (XrankChannel.set_stamps): for every step of a
     short serial graph-replayed run, the finisher's wall clock at its first push and when every
     peer's partial had landed. Per rank the median / p90 of that wait (us); the rank that waits least
@@ -970,7 +972,8 @@ def _exchange_wait(wl, ctx, args, fault, cap: int = 4096) -> "dict | None":
     err = None
     try:
         ch.set_stamps(st.data_ptr(), cap)
-        _measure(wl, wl.new_slots(W + K), ctx, args, fault, serial=True, warmup=W, site="extras")
+        _measure(wl, wl.new_slots(W + K), ctx, args, fault, serial=True, warmup=W, site="extras",
+                 allow_graph=allow_graph)
     except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
         err = f"{type(e).__name__}: {e}"[:200]
     finally:
@@ -1231,7 +1234,9 @@ def main(argv=None) -> int:
     cap_failed = m["launch"].startswith("eager (graph capture failed")
     if args.decompose and not args.pipelined and hasattr(wl, "local_step"):  # kernels only: cheap, first
         try:
-            extras["decomposition"] = _decompose(wl, ctx, args, fault, ms)
+            # (after a failed capture of the headline's collective steps another capture in this process
+            # can abort it: profiles/r2_full/; the decomposition then issues its steps eagerly)
+            extras["decomposition"] = _decompose(wl, ctx, args, fault, ms, allow_graph=not cap_failed)
         except Exception as e:  # noqa: BLE001 - an extra must never cost the headline
             extras["decomposition"] = {"error": f"{type(e).__name__}: {e}"[:300]}
             print(f"[bench] rank {ctx.rank}: decomposition failed: {e}", file=sys.stderr)

@@ -20,8 +20,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --elements 125000000 --steps 300 \
     --warmup 20 --no-vector-extras > $O/shard_prof.json 2> $O/shard_prof.err
 rc=$?; echo "prof rc=$rc" >> $O/status.txt
-python3 tools/kernel_gaps.py $O/prof --match reduce_stream --bytes 1e9 --skip 200 > $O/kernel_gaps.txt 2>&1
-find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
+python3 tools/prof_db.py $O/prof/run_results.db --steady reduce_stream > $O/kernel_stats.txt 2>&1
 rm -rf $O/prof
 timeout -k 10 240 python -u tools/xcd_balance.py --sizes 125000000,1000000000 --rounds 5 --json $O/xcd_balance.jsonl > $O/xcd_balance.txt 2>&1
 echo "xcd rc=$?" >> $O/status.txt

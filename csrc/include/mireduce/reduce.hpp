@@ -35,6 +35,10 @@ struct ReduceConfig {
   // (non-temporal policy, 256/512 threads, unroll 2..8 divisible by it; otherwise hipcc's).
   // profiles/r3_window/.
   int window = -1;
+  // XCD-weighted split of the interleaved window body, in permille of the rounds per workgroup:
+  // > 0 gives the odd workgroups (odd XCDs) that many more rounds, < 0 the even ones; 0 equal
+  // rounds; INT_MIN = tuned default. (profiles/r4_xcd/)
+  int xcd_skew = -2147483647 - 1;
   bool single_pass = true;   // last-arriver finalisation vs a second finalize launch
   // Fused cross-rank finish: XrankChannel::device_desc() (xrank.hpp). The launch then writes the
   // fold over every rank's partial into out (single-pass only).
@@ -65,6 +69,7 @@ struct LaunchPlan {
   bool flat = false;   // ticketed fan-in: flat (final arriver folds every partial) vs two-level
   bool contiguous = false;  // body split: one contiguous run of tiles per workgroup vs interleaved
   bool balanced = false;    // interleaved: leftover tiles split evenly over all workgroups
+  int xskew = 0;            // window body: extra rounds for odd (> 0) / even (< 0) workgroups
   uint64_t head = 0;   // scalar elements before the first 16-B aligned vector
   uint64_t nvec = 0;   // 16-byte vectors in the streaming body
   uint64_t tail = 0;   // scalar elements after the body

@@ -147,6 +147,9 @@ bool balance_leftover() {
   return e && std::strcmp(e, "1") == 0;
 }
 
+// XCD-weighted split default (permille; see plan_reduce): 0 until measured across boxes.
+int tuned_xcd_skew(DType, uint64_t) { return 0; }
+
 // Work split of the streaming body; MIREDUCE_SPLIT=stride|contig overrides (A/B runs; read per
 // plan so one process can compare both).
 bool split_contiguous() {
@@ -302,6 +305,16 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   p.flat = p.single_pass && fanin_mode() == 1;
   p.contiguous = split_contiguous();
   p.balanced = !p.contiguous && balance_leftover();
+  // XCD-weighted split (window bodies, interleaved, even grids): permille of the rounds per
+  // workgroup -> extra rounds for one parity. MIREDUCE_XCD_SKEW=<permille> overrides (A/B runs).
+  if (p.window > 0 && !p.contiguous && !p.balanced && p.grid % 2 == 0) {
+    int permille = cfg.xcd_skew == (-2147483647 - 1) ? tuned_xcd_skew(t, n) : cfg.xcd_skew;
+    if (const char* e = std::getenv("MIREDUCE_XCD_SKEW")) permille = std::atoi(e);
+    const uint64_t tile = static_cast<uint64_t>(p.block) * static_cast<uint64_t>(p.unroll);
+    const uint64_t rounds = tile ? p.nvec / tile / static_cast<uint64_t>(p.grid) : 0;
+    const int64_t d = (static_cast<int64_t>(rounds) * permille + (permille >= 0 ? 500 : -500)) / 1000;
+    p.xskew = static_cast<int>(d);
+  }
   return p;
 }
 
@@ -318,6 +331,23 @@ static kern::Args make_args(const void* in, const LaunchPlan& p, DType t, const 
   a.tail = p.tail;
   a.contig = p.contiguous ? 1 : 0;
   a.balance = p.balanced ? 1 : 0;
+  a.xskew = p.xskew;
+  {  // the weighted split's common / extra rounds (weighted_tiles), precomputed here
+    const uint64_t tile = static_cast<uint64_t>(p.block) * static_cast<uint64_t>(p.unroll);
+    const uint64_t ntiles = tile ? p.nvec / tile : 0, grid = static_cast<uint64_t>(p.grid > 0 ? p.grid : 1);
+    const uint64_t half = grid / 2, d = static_cast<uint64_t>(p.xskew < 0 ? -static_cast<int64_t>(p.xskew) : p.xskew);
+    if (p.xskew == 0 || half == 0) {
+      a.xskew = 0;
+      a.x_ra = ntiles / grid;
+      a.x_dd = 0;
+    } else if (ntiles >= d * half) {
+      a.x_ra = (ntiles - d * half) / grid;
+      a.x_dd = d;
+    } else {
+      a.x_ra = 0;
+      a.x_dd = ntiles / half;
+    }
+  }
   return a;
 }
 

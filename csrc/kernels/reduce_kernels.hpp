@@ -88,6 +88,10 @@ struct Args {
   int delay_wg;            // test hook (ReduceConfig::debug_delay_wg): this workgroup sleeps
   uint64_t delay_ticks;    // delay_ticks before publishing its partial; -1 = none
   uint64_t* wg_stamps;     // diagnostic (ReduceConfig::debug_wg_stamps): per-workgroup end stamps
+  int xskew;               // XCD-weighted split (window bodies, interleaved): |xskew| extra rounds of
+                           // tiles for the odd (xskew > 0) or even (< 0) workgroups; 0 = equal rounds
+  uint64_t x_ra;           // weighted split, precomputed on the host: common rounds (ntiles / grid at 0)
+  uint64_t x_dd;           // extra rounds actually given to the favoured parity
 };
 
 // Polled fan-in: a published partial is two 8-byte words (epoch << 32 | 32 data bits), where the
@@ -313,6 +317,87 @@ __device__ __forceinline__ void stream_window(AccT (&acc)[UNROLL], const V* __re
   }
 }
 
+// The tiles one workgroup streams as up to three arithmetic runs (the XCD-weighted split): run 0
+// `n0` tiles from `s0` by `st0`, run 1 `n1` tiles from `s1` by `st1`, run 2 `n2` tiles from `s2`
+// by `st0`. Workgroups are dispatched to the 8 XCDs round-robin (XCD = blockIdx % 8), and the
+// XCDs do not stream equally fast: with equal tiles, the even XCDs' workgroups end ~1.5-2 % later
+// than the odd ones' in every run (tools/xcd_balance.py, profiles/r4_suite/), and the kernel ends
+// with the slowest. The weighted split gives one parity a few more rounds so both end together.
+struct TileSeq {
+  uint64_t s0, st0, n0, s1, st1, n1, s2, n2;
+  __device__ __forceinline__ uint64_t count() const { return n0 + n1 + n2; }
+  __device__ __forceinline__ uint64_t at(uint64_t i) const {
+    if (i < n0) return s0 + i * st0;
+    i -= n0;
+    if (i < n1) return s1 + i * st1;
+    return s2 + (i - n1) * st0;
+  }
+};
+
+// Workgroup b's tiles of the interleaved split of `ntiles` over `grid` workgroups. Without skew:
+// tiles b, b + grid, ... (run 0 over the ra = ntiles / grid whole rounds, run 2 = the leftover
+// tile of the first ntiles % grid workgroups). With skew (even grid): every workgroup takes the
+// `ra` common rounds interleaved, the favoured parity then `dd` more rounds interleaved among
+// themselves, and the leftover (< grid tiles) goes one tile each to the favoured workgroups first.
+// `ra` and `dd` come precomputed from the host (no 64-bit division on the device). A bijection
+// onto [0, ntiles) for any skew (GPU test: tests/test_kernels_gpu.py::test_xcd_weighted_split).
+__device__ __forceinline__ TileSeq weighted_tiles(uint64_t ntiles, uint64_t grid, int xskew, uint64_t ra,
+                                                  uint64_t dd, uint64_t b) {
+  TileSeq q{};
+  q.s0 = b;
+  q.st0 = grid;
+  q.n0 = ra;
+  const uint64_t base1 = ra * grid;
+  if (xskew == 0) {
+    q.s2 = base1 + b;
+    q.n2 = b < ntiles - base1 ? 1 : 0;
+    return q;
+  }
+  const uint64_t half = grid >> 1;
+  const bool favoured = (b & 1u) == (xskew > 0 ? 1u : 0u);
+  q.s1 = base1 + (b >> 1);
+  q.st1 = half;
+  q.n1 = favoured ? dd : 0;
+  const uint64_t base2 = base1 + dd * half, left = ntiles - base2;  // < grid
+  const uint64_t rank2 = favoured ? (b >> 1) : half + (b >> 1);   // favoured workgroups first
+  q.s2 = base2 + rank2;
+  q.n2 = rank2 < left ? 1 : 0;
+  return q;
+}
+
+template <class OpT, class T, class AccT, class V, int N, int BLOCK, int UNROLL, int WIN>
+__device__ __forceinline__ void stream_window_seq(AccT (&acc)[UNROLL], const V* __restrict__ vin, const TileSeq& q) {
+  static_assert(UNROLL % WIN == 0, "the window must divide the unroll");
+  constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
+  constexpr uint32_t kStride = BLOCK * 16;
+  const uint64_t n = q.count();
+  if (n == 0) return;
+  const uint32_t voff = threadIdx.x * 16;
+  __amdgpu_buffer_rsrc_t rp = tile_rsrc(vin + q.at(0) * kTile);
+  V buf[WIN];
+#pragma unroll
+  for (int j = 0; j < WIN; ++j) buf[j] = ld_buf_nt<V>(rp, voff, j * kStride);
+  for (uint64_t i = 0; i + 1 < n; ++i) {  // the same loose window as stream_window
+    const __amdgpu_buffer_rsrc_t rq = tile_rsrc(vin + q.at(i + 1) * kTile);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(buf[u % WIN], k)));
+      const int j = u + WIN;
+      buf[u % WIN] = j < UNROLL ? ld_buf_nt<V>(rp, voff, j * kStride) : ld_buf_nt<V>(rq, voff, (j - UNROLL) * kStride);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    rp = rq;
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(buf[u % WIN], k)));
+    const int j = u + WIN;
+    if (j < UNROLL) buf[u % WIN] = ld_buf_nt<V>(rp, voff, j * kStride);
+  }
+}
+
 // PIPE: software-pipelined body — tile t+grid's loads are issued before tile t is consumed, so
 // a wave always has UNROLL loads in flight while it computes (two register sets). The loop has
 // no per-load condition (the last tile is peeled), see cdna_hip_programming.md §5 trap (c).
@@ -382,7 +467,16 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, cur);
     }
   } else if constexpr (WIN > 0) {
-    stream_window<OpT, T, AccT, V, N, BLOCK, UNROLL, WIN, false>(acc, vin, t0, t1, step);
+    // one window body for every split: contiguous runs, whole rounds (balanced), or interleaved
+    TileSeq q{};
+    if (a.contig || balanced) {
+      q.s0 = t0;
+      q.st0 = step;
+      q.n0 = t1 > t0 ? (t1 - t0 + step - 1) / step : 0;
+    } else {
+      q = weighted_tiles(ntiles, grid, a.xskew, a.x_ra, a.x_dd, blockIdx.x);
+    }
+    stream_window_seq<OpT, T, AccT, V, N, BLOCK, UNROLL, WIN>(acc, vin, q);
   } else if constexpr (WIN < 0) {  // strict window (experiments only: tools/window_ab.hip)
     stream_window<OpT, T, AccT, V, N, BLOCK, UNROLL, -WIN, true>(acc, vin, t0, t1, step);
   } else {
@@ -452,7 +546,8 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     uint64_t* st = a.wg_stamps + 3 * static_cast<uint64_t>(blockIdx.x);
     st[0] = t_end;
     st[1] = xcc & 0xfu;
-    st[2] = a.contig ? t1 - t0 : (t1 > t0 ? (t1 - t0 + step - 1) / step : 0);
+    st[2] = (WIN > 0 && !a.contig && !balanced) ? weighted_tiles(ntiles, grid, a.xskew, a.x_ra, a.x_dd, blockIdx.x).count()
+            : a.contig ? t1 - t0 : (t1 > t0 ? (t1 - t0 + step - 1) / step : 0);
   }
 
   // Fused cross-rank finish: this launch's epoch (counter + 1; only the finishing workgroup bumps

@@ -52,6 +52,7 @@ py::dict plan_dict(const LaunchPlan& p) {
   d["poll"] = p.poll;
   d["balanced"] = p.balanced;
   d["contiguous"] = p.contiguous;
+  d["xskew"] = p.xskew;
   d["head"] = p.head;
   d["nvec"] = p.nvec;
   d["tail"] = p.tail;

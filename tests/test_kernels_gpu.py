@@ -412,3 +412,31 @@ def test_default_plan_above_192mb_narrow_types(dt, op, want):
     acc = torch.float32 if half else (wide[dt] if op == "sum" else dt)
     check(got, x, op, acc, n)
 
+
+
+@pytest.mark.parametrize("permille", [-300, -16, 0, 9, 16, 400, 5000])
+@pytest.mark.parametrize("n", [25_000_003, 31_457_280 + 17])
+@pytest.mark.parametrize("op", ["sum", "max"])
+def test_xcd_weighted_split(monkeypatch, permille, n, op):
+    # round 4: the XCD-weighted split of the window body (reduce_kernels.hpp weighted_tiles) gives
+    # one blockIdx parity more rounds; every tile must still be streamed exactly once, for any skew
+    # (also skews larger than the array, which leave the other parity without tiles). int64 data:
+    # exact SUM / MAX against torch.
+    monkeypatch.setenv("MIREDUCE_XCD_SKEW", str(permille))
+    C = native()
+    g = torch.Generator(device="cpu").manual_seed(n + permille)
+    x = torch.randint(-(1 << 40), 1 << 40, (n,), generator=g, dtype=torch.int64).to(DEV)
+    if op == "max":
+        x[(n * 7) // 11] = 1 << 50  # the extreme sits in one tile
+    red = Reducer(torch.device(DEV))
+    out = torch.zeros(1, dtype=torch.int64, device=DEV)
+    from cuda_mpi_reductions_amd.ops import dtype_code, op_code
+    plan = C.reduce(red.ws, x.data_ptr(), n, dtype_code(x.dtype), op_code(op), dtype_code(torch.int64),
+                    out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert plan["window"] > 0 and plan["grid"] % 2 == 0, plan
+    rounds = n // 2 // (plan["block"] * plan["unroll"]) // plan["grid"]
+    q = rounds * permille + (500 if permille >= 0 else -500)  # the planner's rounding (half away from 0)
+    assert plan["xskew"] == (abs(q) // 1000) * (1 if q >= 0 else -1), plan
+    exp = x.sum().item() if op == "sum" else x.max().item()
+    assert out.item() == exp and red.check() is None

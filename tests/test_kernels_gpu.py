@@ -415,7 +415,7 @@ def test_default_plan_above_192mb_narrow_types(dt, op, want):
 
 
 @pytest.mark.parametrize("permille", [-300, -16, 0, 9, 16, 400, 5000])
-@pytest.mark.parametrize("n", [25_000_003, 31_457_280 + 17])
+@pytest.mark.parametrize("n", [26_000_003, 31_457_280 + 17])  # 8-byte window plans: > 192 MiB
 @pytest.mark.parametrize("op", ["sum", "max"])
 def test_xcd_weighted_split(monkeypatch, permille, n, op):
     # round 4: the XCD-weighted split of the window body (reduce_kernels.hpp weighted_tiles) gives

@@ -559,24 +559,24 @@ def _peer_read_extra(ctx, nbytes: int = 256 << 20, steps: int = 5) -> dict:
 
 
 def _plan_candidates(bytes_per_gpu: float, esize: int) -> list:
-    """Streaming-kernel plans (block, unroll, workgroups per CU, load window) worth measuring on the
-    node for a shard of this size: (0, 0, 0, -1) = the tuned default (256x8x1 with an explicit
-    load window of 4 for 8-byte types above 192 MB, profiles/r3_window/). The ranking of the top
-    plans moves by 1-2 % between boxes, so for the headline's 8-byte shards the bench measures the
-    default against the runners-up of the round-3 window sweep and the round-2 defaults (hipcc's
-    own schedule) instead of trusting one box's table."""
-    if esize == 8 and bytes_per_gpu >= 3 * (1 << 30):
-        return [(0, 0, 0, -1), (256, 4, 2, 2), (256, 8, 1, 0)]
+    """Streaming-kernel plans (block, unroll, workgroups per CU, load window, XCD skew) worth
+    measuring on the node for a shard of this size: (0, 0, 0, -1, None) = the tuned default
+    (256x8x1 with an explicit load window of 4 and the XCD-weighted split for 8-byte types above
+    192 MB, profiles/r3_window/, profiles/r4_xcd/). The ranking of the top plans moves by 1-2 %
+    between boxes, so for the headline's 8-byte shards the bench measures the default against the
+    same plan with equal rounds per XCD (skew 0) and with twice the skew, and against the runner-up
+    of the round-3 window sweep, instead of trusting one box's table."""
     if esize == 8 and bytes_per_gpu >= 768 * (1 << 20):
-        return [(0, 0, 0, -1), (256, 4, 2, 2), (256, 2, 3, 0)]
-    return [(0, 0, 0, -1)]
+        return [(0, 0, 0, -1, None), (0, 0, 0, -1, 0), (0, 0, 0, -1, 40), (256, 4, 2, 2, None)]
+    return [(0, 0, 0, -1, None)]
 
 
 def _plan_key(c) -> str:
-    b, u, w, win = c
+    b, u, w, win, skew = c
     if b == 0:
-        return "tuned default"
-    return f"{b}x{u}x{w}" + (f" window {win}" if win > 0 else " hipcc schedule")
+        return "tuned default" + ("" if skew is None else f", XCD skew {skew}")
+    return f"{b}x{u}x{w}" + (f" window {win}" if win > 0 else " hipcc schedule") + \
+        ("" if skew is None else f", XCD skew {skew}")
 
 
 def _graph_chunk(requested: int, steps: int, issues_collective: bool) -> int:
@@ -1008,14 +1008,15 @@ def _tune_plan(wl, ctx, args, fault, kernel, cands) -> "tuple[KernelConfig, dict
             key = _plan_key(c)
             if res.get(key, 0.0) < 0:
                 continue
-            b, u, w, win = c
-            wl.use_kernel(replace(kernel, block=b, unroll=u, wg_per_cu=w, window=None if win < 0 else win), streams=1)
+            b, u, w, win, skew = c
+            wl.use_kernel(replace(kernel, block=b, unroll=u, wg_per_cu=w, window=None if win < 0 else win,
+                                  xcd_skew=skew), streams=1)
             mt = _measure(wl, wl.new_slots(2 + T), ctx, args, fault, serial=True, warmup=2, steps=T)
             g = round(_gbps(wl, T, mt["elapsed"]), 3)
             res[key] = -1.0 if wl.check() is not None else max(res.get(key, 0.0), g)
     best = max(res, key=res.get)
-    b, u, w, win = next(c for c in cands if _plan_key(c) == best)
-    kernel = replace(kernel, block=b, unroll=u, wg_per_cu=w, window=None if win < 0 else win)
+    b, u, w, win, skew = next(c for c in cands if _plan_key(c) == best)
+    kernel = replace(kernel, block=b, unroll=u, wg_per_cu=w, window=None if win < 0 else win, xcd_skew=skew)
     wl.use_kernel(kernel, streams=1)
     return kernel, {"steps": T, "gbps": res, "chosen": best}
 

@@ -147,8 +147,12 @@ bool balance_leftover() {
   return e && std::strcmp(e, "1") == 0;
 }
 
-// XCD-weighted split default (permille; see plan_reduce): 0 until measured across boxes.
-int tuned_xcd_skew(DType, uint64_t) { return 0; }
+// XCD-weighted split default (permille of the rounds per workgroup given extra to the odd
+// workgroups; see plan_reduce and weighted_tiles). Measured for the 8-byte window plan on two boxes
+// (profiles/r4_xcd/): 0 -> 16 -> 24 permille take the 1 GB shard from 138.0-138.6 to 137.2-137.8 us
+// and 8 GB from 1092.1-1092.7 to 1086.3-1089.7 us, the even XCDs' late end gone from the stamps.
+// Other element types: 0 until measured. bench.py re-measures 0 / default / 2x on the node.
+int tuned_xcd_skew(DType t, uint64_t) { return dtype_size(t) == 8 ? 20 : 0; }
 
 // Work split of the streaming body; MIREDUCE_SPLIT=stride|contig overrides (A/B runs; read per
 // plan so one process can compare both).

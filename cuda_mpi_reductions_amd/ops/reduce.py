@@ -45,6 +45,7 @@ CODE_DTYPES = {v: k for k, v in DTYPE_CODES.items()}
 # sum / min / max are the reference's operators; sumsq (fused sum of squares) and amax (fused
 # max |x|) transform each element once as it is loaded (floating dtypes only).
 OP_CODES = {"sum": 0, "min": 1, "max": 2, "sumsq": 3, "amax": 4}
+XCD_SKEW_AUTO = -(2 ** 31)  # ReduceConfig::xcd_skew's "tuned default"
 FUSED_OPS = ("sumsq", "amax")
 
 
@@ -84,6 +85,7 @@ class KernelConfig:
     single_pass: bool = True
     pipelined: Optional[bool] = None    # None: tuned choice
     window: Optional[int] = None        # loads in flight per thread: None tuned, 0 hipcc's schedule, 2 | 4
+    xcd_skew: Optional[int] = None      # XCD-weighted split, permille of rounds (+: odd XCDs more); None tuned
 
     @property
     def policy(self) -> int:
@@ -100,6 +102,7 @@ class KernelConfig:
             single_pass=self.single_pass,
             pipeline=-1 if self.pipelined is None else int(bool(self.pipelined)),
             window=-1 if self.window is None else int(self.window),
+            xcd_skew=XCD_SKEW_AUTO if self.xcd_skew is None else int(self.xcd_skew),
         )
 
 

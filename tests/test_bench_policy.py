@@ -59,11 +59,15 @@ def test_extras_watchdog_stays_quiet_when_extras_finish():
 def test_plan_candidates_only_for_the_headline_shards():
     b = _bench()
     GB = 1 << 30
-    assert b._plan_candidates(8e9, 8) == [(0, 0, 0, -1), (256, 4, 2, 2), (256, 8, 1, 0)]  # N=1 / N=2 shards
-    assert b._plan_candidates(1e9, 8) == [(0, 0, 0, -1), (256, 4, 2, 2), (256, 2, 3, 0)]  # N=8 shard
-    assert b._plan_candidates(0.5 * GB, 8) == [(0, 0, 0, -1)]
-    assert b._plan_candidates(8e9, 4) == [(0, 0, 0, -1)] and b._plan_candidates(8e9, 2) == [(0, 0, 0, -1)]
-    assert b._plan_key((256, 4, 2, 2)) == "256x4x2 window 2" and b._plan_key((256, 8, 1, 0)) == "256x8x1 hipcc schedule"
+    # the tuned default (its XCD skew), equal rounds per XCD, twice the skew, the window runner-up
+    cands = [(0, 0, 0, -1, None), (0, 0, 0, -1, 0), (0, 0, 0, -1, 40), (256, 4, 2, 2, None)]
+    assert b._plan_candidates(8e9, 8) == cands  # N=1 / N=2 shards
+    assert b._plan_candidates(1e9, 8) == cands  # N=8 shard
+    assert b._plan_candidates(0.5 * GB, 8) == [(0, 0, 0, -1, None)]
+    assert b._plan_candidates(8e9, 4) == [(0, 0, 0, -1, None)] and b._plan_candidates(8e9, 2) == [(0, 0, 0, -1, None)]
+    assert b._plan_key((256, 4, 2, 2, None)) == "256x4x2 window 2"
+    assert b._plan_key((256, 8, 1, 0, None)) == "256x8x1 hipcc schedule"
+    assert b._plan_key((0, 0, 0, -1, None)) == "tuned default" and b._plan_key((0, 0, 0, -1, 0)) == "tuned default, XCD skew 0"
 
 
 def test_extras_watchdog_reports_the_extras_completed_so_far():

@@ -151,8 +151,14 @@ bool balance_leftover() {
 // workgroups; see plan_reduce and weighted_tiles). Measured for the 8-byte window plan on two boxes
 // (profiles/r4_xcd/): 0 -> 16 -> 24 permille take the 1 GB shard from 138.0-138.6 to 137.2-137.8 us
 // and 8 GB from 1092.1-1092.7 to 1086.3-1089.7 us, the even XCDs' late end gone from the stamps.
-// Other element types: 0 until measured. bench.py re-measures 0 / default / 2x on the node.
-int tuned_xcd_skew(DType t, uint64_t) { return dtype_size(t) == 8 ? 20 : 0; }
+// The fp32 window-4 plan wants the same (8 GB: 1106.5 -> 1099.1 us at 20, 1114.2 at -20;
+// profiles/r4_shard/); the bf16 one does not (1084.4 -> 1088.8 us at 20, profiles/r4_xcd/), and the
+// window-2 plans (int32 SUM, 16-bit MIN/MAX) are unmeasured: 0 there. bench.py re-measures
+// 0 / default / 2x on the node for the headline's shards.
+int tuned_xcd_skew(DType t, const LaunchPlan& p) {
+  const size_t es = dtype_size(t);
+  return (es == 8 || es == 4) && p.window == 4 ? 20 : 0;
+}
 
 // Work split of the streaming body; MIREDUCE_SPLIT=stride|contig overrides (A/B runs; read per
 // plan so one process can compare both).
@@ -312,7 +318,7 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   // XCD-weighted split (window bodies, interleaved, even grids): permille of the rounds per
   // workgroup -> extra rounds for one parity. MIREDUCE_XCD_SKEW=<permille> overrides (A/B runs).
   if (p.window > 0 && !p.contiguous && !p.balanced && p.grid % 2 == 0) {
-    int permille = cfg.xcd_skew == (-2147483647 - 1) ? tuned_xcd_skew(t, n) : cfg.xcd_skew;
+    int permille = cfg.xcd_skew == (-2147483647 - 1) ? tuned_xcd_skew(t, p) : cfg.xcd_skew;
     if (const char* e = std::getenv("MIREDUCE_XCD_SKEW")) permille = std::atoi(e);
     const uint64_t tile = static_cast<uint64_t>(p.block) * static_cast<uint64_t>(p.unroll);
     const uint64_t rounds = tile ? p.nvec / tile / static_cast<uint64_t>(p.grid) : 0;

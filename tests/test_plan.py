@@ -57,7 +57,13 @@ def test_tuned_defaults_by_size():
     # of 8-byte window plans; explicit values override; no window -> no skew; 4-byte: 0 until measured
     assert big["xskew"] == 19 and mid["xskew"] == 2     # 953 and 119 rounds per workgroup
     assert C.plan(0, 10**9, F64, xcd_skew=0)["xskew"] == 0 and C.plan(0, 10**9, F64, xcd_skew=-40)["xskew"] == -38
-    assert small["xskew"] == 0 and C.plan(0, 2 * 10**9, 2)["xskew"] == 0
+    assert small["xskew"] == 0
+    f32 = C.plan(0, 2 * 10**9, 2)          # fp32 SUM 8 GB: window 4, the same skew (profiles/r4_shard/)
+    assert f32["window"] == 4 and f32["xskew"] == 19
+    bf16 = C.plan(0, 4 * 10**9, 4)         # bf16 SUM 8 GB: window 4 but no skew (profiles/r4_xcd/)
+    assert bf16["window"] == 4 and bf16["xskew"] == 0
+    i32 = C.plan(0, 2 * 10**9, 0)          # int32 SUM: the window-2 plan, unmeasured: no skew
+    assert i32["window"] == 2 and i32["xskew"] == 0
 
 
 # op codes: SUM 0, MIN 1, MAX 2, SUMSQ 3, AMAX 4; dtypes: int32 0, int64 1, f32 2, f64 3, bf16 4, f16 5

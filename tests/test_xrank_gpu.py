@@ -395,11 +395,14 @@ def test_bench_plan_tuning_at_the_eight_gpu_shard(tmp_path):
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["verified"] is True
     pt = d["plan_tuning"]
-    assert set(pt["gbps"]) == {"tuned default", "256x4x2 window 2", "256x2x3 hipcc schedule"}
+    assert set(pt["gbps"]) == {"tuned default", "tuned default, XCD skew 0", "tuned default, XCD skew 40",
+                               "256x4x2 window 2"}
     assert pt["chosen"] == max(pt["gbps"], key=pt["gbps"].get)
     plan = d["config"]["kernel_plan"]
-    want = {"tuned default": (256, 8, 4), "256x4x2 window 2": (256, 4, 2), "256x2x3 hipcc schedule": (256, 2, 0)}
-    assert (plan["block"], plan["unroll"], plan["window"]) == want[pt["chosen"]]
+    # (block, unroll, window, xskew): 119 rounds per workgroup at the 1 GB shard
+    want = {"tuned default": (256, 8, 4, 2), "tuned default, XCD skew 0": (256, 8, 4, 0),
+            "tuned default, XCD skew 40": (256, 8, 4, 5), "256x4x2 window 2": (256, 4, 2, 0)}
+    assert (plan["block"], plan["unroll"], plan["window"], plan["xskew"]) == want[pt["chosen"]]
 
 
 def test_bench_maxloc_config_skips_plan_tuning(tmp_path):

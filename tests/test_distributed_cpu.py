@@ -205,6 +205,30 @@ def test_fused_canary_orchestration_three_ranks():
     assert v["wrong"] is not None and "gloo all-reduce gave" in v["wrong"], v["wrong"]
 
 
+def canary_hang_case(rank, world):
+    from cuda_mpi_reductions_amd.parallel import dist as pdist
+    from cuda_mpi_reductions_amd.parallel.canary import fused_canary
+    ctx = pdist.init(device_type="cpu")
+    os.environ["MIREDUCE_CANARY_FAULT"] = "hang@1"
+    import time
+    t0 = time.time()
+    res = {"hang": fused_canary(ctx, timeout_s=12, dry=True), "s": time.time() - t0}
+    os.environ.pop("MIREDUCE_CANARY_FAULT")
+    res["after"] = fused_canary(ctx, timeout_s=60, dry=True)  # the job goes on: a fresh canary passes
+    pdist.shutdown(ctx)
+    return res
+
+
+def test_fused_canary_hung_helper_is_bounded():
+    # a helper that hangs is killed at the canary's deadline and named in the agreed verdict (the
+    # peer's helper, stuck in a collective with it, fails by its gloo timeout or the same deadline)
+    out = _spawn("canary_hang_case", 2)
+    for res in out.values():
+        assert isinstance(res, dict), res
+        assert res["hang"] is not None and "rank 1: helper did not finish within 12 s" in res["hang"], res
+        assert res["s"] < 40 and res["after"] is None
+
+
 def test_bench_vector_config1_two_cpu_ranks(tmp_path):
     # BASELINE config 1 through bench.py: 1M int32 SUM, element-wise reduce to root, 2 CPU ranks.
     r = torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "1",

@@ -159,6 +159,19 @@ def test_bench_self_launches_n_ranks_without_torchrun(tmp_path):
     assert abs(dec["exchange_us_per_step"] - (d["ms_per_step"] - dec["local_ms_max"]) * 1e3) < 0.01
 
 
+def test_bench_four_cpu_ranks_probe_and_decomposition(tmp_path):
+    # the N > 1 headline flow with 4 ranks: the replay probe runs (auto: the combine issues a
+    # collective at N > 1; eager here) and passes, the decomposition covers every rank
+    r = torchrun(4, [os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "5", "--warmup", "1",
+                     "--device", "cpu", "--elements", "400007"], cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["verified"] is True and d["n_gpus"] == 4 and d["ranks_seen"] == 4 and d["launcher"] == "external"
+    assert d["config"]["launch"] == "eager; replay probe ok", d["config"]["launch"]
+    dec = d["decomposition"]
+    assert dec["consistent"] is True and dec["local_ms_min"] <= dec["local_ms_max"]
+
+
 def test_bench_refuses_world_size_mismatch(tmp_path):
     # a launcher that started a different number of ranks than --gpus asks for: diagnostic line, rc 2
     r = run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "3"],

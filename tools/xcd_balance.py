@@ -34,23 +34,35 @@ def main(argv=None) -> int:
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--json", default=None, help="append one JSON object per (size, round)")
+    ap.add_argument("--skews", default=None,
+                    help="comma list of XCD skews (permille, MIREDUCE_XCD_SKEW) measured interleaved in every "
+                         "round on the same array (default: the plan's own)")
+    ap.add_argument("--offset-tiles", type=int, default=0,
+                    help="start the array this many 32 KB tiles into its allocation (address-residue test)")
     a = ap.parse_args(argv)
     C = native()
     dev = torch.device("cuda", 0)
     red = Reducer(dev)
     out = torch.zeros(1, dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
+    skews = [None] if a.skews is None else [int(v) for v in a.skews.split(",")]
+    off = a.offset_tiles * 4096  # 32 KB tiles of float64
     for n in (int(float(x)) for x in a.sizes.split(",")):
-        x = torch.empty(n, dtype=torch.float64, device=dev)
+        base = torch.empty(n + off, dtype=torch.float64, device=dev)
+        x = base[off:]
         fill_(x, "uniform", seed=11)
         stamps = torch.zeros(3 * red.ws.max_grid, dtype=torch.int64, device=dev)
 
         def launch(st=0):
             return C.reduce(red.ws, x.data_ptr(), n, dtype_code(x.dtype), op_code("sum"), dtype_code(torch.float64),
                             out.data_ptr(), stream.cuda_stream, wg_stamps=st)
-        plan = launch()
-        grid = plan["grid"]
-        for r in range(a.rounds):
+        for r, sk in ((r, sk) for r in range(a.rounds) for sk in skews):
+            if sk is None:
+                os.environ.pop("MIREDUCE_XCD_SKEW", None)
+            else:
+                os.environ["MIREDUCE_XCD_SKEW"] = str(sk)
+            plan = launch()
+            grid = plan["grid"]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.launches):
@@ -64,7 +76,8 @@ def main(argv=None) -> int:
             xcc = st[:, 1]
             srt = end.sort().values
             per = {int(k): round(float(end[xcc == k].mean()), 2) for k in sorted(set(xcc.tolist()))}
-            row = {"n": n, "round": r, "grid": grid, "us_per_launch": round(us_per, 2),
+            row = {"n": n, "round": r, "skew": sk, "xskew": plan.get("xskew"), "offset_tiles": a.offset_tiles,
+                   "base_mod_2mb": int(x.data_ptr() % (2 << 20)), "grid": grid, "us_per_launch": round(us_per, 2),
                    "end_spread_us": {"p50": round(float(srt[grid // 2]), 2),
                                      "p99": round(float(srt[int(0.99 * (grid - 1))]), 2),
                                      "max": round(float(srt[-1]), 2)},
@@ -74,7 +87,7 @@ def main(argv=None) -> int:
             if a.json:
                 with open(a.json, "a") as f:
                     f.write(json.dumps(row) + "\n")
-        del x
+        del x, base
         torch.cuda.empty_cache()
     return 0
 

@@ -147,8 +147,8 @@ bool balance_leftover() {
   return e && std::strcmp(e, "1") == 0;
 }
 
-// XCD-weighted split default (permille of the rounds per workgroup given extra to the odd
-// workgroups; see plan_reduce and weighted_tiles). Measured for the 8-byte window plan on two boxes
+// XCD-weighted split default (permille of the rounds per workgroup given extra to the workgroups
+// on odd XCCs; see plan_reduce, weighted_tiles and XcdAnchor). Measured for the 8-byte window plan on two boxes
 // (profiles/r4_xcd/): 0 -> 16 -> 24 permille take the 1 GB shard from 138.0-138.6 to 137.2-137.8 us
 // and 8 GB from 1092.1-1092.7 to 1086.3-1089.7 us, the even XCDs' late end gone from the stamps.
 // The fp32 window-4 plan wants the same (8 GB: 1106.5 -> 1099.1 us at 20, 1114.2 at -20;
@@ -317,13 +317,17 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   p.balanced = !p.contiguous && balance_leftover();
   // XCD-weighted split (window bodies, interleaved, even grids): permille of the rounds per
   // workgroup -> extra rounds for one parity. MIREDUCE_XCD_SKEW=<permille> overrides (A/B runs).
-  if (p.window > 0 && !p.contiguous && !p.balanced && p.grid % 2 == 0) {
+  // Polled fan-in only: the kernel anchors the favoured parity to the XCDs with the fan-in epoch.
+  if (p.window > 0 && !p.contiguous && !p.balanced && p.grid % 2 == 0 && p.poll && p.grid > 1) {
     int permille = cfg.xcd_skew == (-2147483647 - 1) ? tuned_xcd_skew(t, p) : cfg.xcd_skew;
     if (const char* e = std::getenv("MIREDUCE_XCD_SKEW")) permille = std::atoi(e);
     const uint64_t tile = static_cast<uint64_t>(p.block) * static_cast<uint64_t>(p.unroll);
     const uint64_t rounds = tile ? p.nvec / tile / static_cast<uint64_t>(p.grid) : 0;
     const int64_t d = (static_cast<int64_t>(rounds) * permille + (permille >= 0 ? 500 : -500)) / 1000;
-    p.xskew = static_cast<int>(d);
+    // the common rounds must stay >= 1 (the kernel resolves the anchor at their end)
+    const uint64_t ad = static_cast<uint64_t>(d < 0 ? -d : d), ntiles = tile ? p.nvec / tile : 0;
+    const uint64_t g = static_cast<uint64_t>(p.grid);
+    p.xskew = ad * (g / 2) + g <= ntiles ? static_cast<int>(d) : 0;
   }
   return p;
 }
@@ -350,12 +354,9 @@ static kern::Args make_args(const void* in, const LaunchPlan& p, DType t, const 
       a.xskew = 0;
       a.x_ra = ntiles / grid;
       a.x_dd = 0;
-    } else if (ntiles >= d * half) {
+    } else {  // plan_reduce keeps d * half + grid <= ntiles: >= 1 common round
       a.x_ra = (ntiles - d * half) / grid;
       a.x_dd = d;
-    } else {
-      a.x_ra = 0;
-      a.x_dd = ntiles / half;
     }
   }
   return a;

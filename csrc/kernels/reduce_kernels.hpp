@@ -80,7 +80,8 @@ struct Args {
   int contig;            // 1: workgroup b streams one contiguous run of tiles; 0: tiles b, b+grid, ...
   const XrankDesc* xrank;  // non-null: fold the ranks' partials in-kernel before writing out (xrank.hpp)
   uint64_t* slots;         // non-null: polled fan-in (no tickets), [gridDim.x][2] epoch-tagged words
-  unsigned* fan;           // polled fan-in state (Workspace): [0] epoch = finished launches, [1] sticky error
+  unsigned* fan;           // polled fan-in state (Workspace): [0] epoch = finished launches, [1] sticky error,
+                           // [2..3] the XCD anchor of the weighted split (XcdAnchor)
   uint64_t fan_bound;      // polled fan-in: finisher's wait bound in wall-clock ticks
   unsigned fan_slots;      // polled fan-in: slots in the workspace (all zeroed when the epoch wraps)
   int balance;             // 1 (interleaved split): whole rounds of tiles, then the leftover < grid
@@ -89,7 +90,7 @@ struct Args {
   uint64_t delay_ticks;    // delay_ticks before publishing its partial; -1 = none
   uint64_t* wg_stamps;     // diagnostic (ReduceConfig::debug_wg_stamps): per-workgroup end stamps
   int xskew;               // XCD-weighted split (window bodies, interleaved): |xskew| extra rounds of
-                           // tiles for the odd (xskew > 0) or even (< 0) workgroups; 0 = equal rounds
+                           // tiles for the workgroups on odd (xskew > 0) or even (< 0) XCCs; 0 = equal
   uint64_t x_ra;           // weighted split, precomputed on the host: common rounds (ntiles / grid at 0)
   uint64_t x_dd;           // extra rounds actually given to the favoured parity
 };
@@ -324,61 +325,159 @@ __device__ __forceinline__ void stream_window(AccT (&acc)[UNROLL], const V* __re
 // than the odd ones' in every run (tools/xcd_balance.py, profiles/r4_suite/), and the kernel ends
 // with the slowest. The weighted split gives one parity a few more rounds so both end together.
 struct TileSeq {
-  uint64_t s0, st0, n0, s1, st1, n1, s2, n2;
-  __device__ __forceinline__ uint64_t count() const { return n0 + n1 + n2; }
-  __device__ __forceinline__ uint64_t at(uint64_t i) const {
-    if (i < n0) return s0 + i * st0;
-    i -= n0;
-    if (i < n1) return s1 + i * st1;
-    return s2 + (i - n1) * st0;
-  }
+  uint64_t s0, st0, s1, st1, s2;
+  uint32_t n0, n1, n2;  // tile counts fit 32 bits (2^32 tiles of 4 KB+ = 16 TB+)
+  __device__ __forceinline__ uint32_t count() const { return n0 + n1 + n2; }
 };
 
-// Workgroup b's tiles of the interleaved split of `ntiles` over `grid` workgroups. Without skew:
-// tiles b, b + grid, ... (run 0 over the ra = ntiles / grid whole rounds, run 2 = the leftover
-// tile of the first ntiles % grid workgroups). With skew (even grid): every workgroup takes the
-// `ra` common rounds interleaved, the favoured parity then `dd` more rounds interleaved among
-// themselves, and the leftover (< grid tiles) goes one tile each to the favoured workgroups first.
-// `ra` and `dd` come precomputed from the host (no 64-bit division on the device). A bijection
-// onto [0, ntiles) for any skew (GPU test: tests/test_kernels_gpu.py::test_xcd_weighted_split).
-__device__ __forceinline__ TileSeq weighted_tiles(uint64_t ntiles, uint64_t grid, int xskew, uint64_t ra,
-                                                  uint64_t dd, uint64_t b) {
-  TileSeq q{};
-  q.s0 = b;
-  q.st0 = grid;
-  q.n0 = ra;
-  const uint64_t base1 = ra * grid;
-  if (xskew == 0) {
-    q.s2 = base1 + b;
-    q.n2 = b < ntiles - base1 ? 1 : 0;
-    return q;
-  }
-  const uint64_t half = grid >> 1;
-  const bool favoured = (b & 1u) == (xskew > 0 ? 1u : 0u);
+// Runs 1 and 2 of the weighted split of workgroup b, the blockIdx parity `fpar` taking the extra
+// rounds: after the `ra` common rounds (run 0: b, b + grid, ...), the favoured workgroups take `dd`
+// more rounds interleaved among themselves, and the leftover (< grid tiles) goes one tile each to
+// the favoured workgroups first. A bijection onto [0, ntiles) for either parity.
+__device__ __forceinline__ void weighted_tail(TileSeq& q, uint64_t ntiles, uint64_t grid, unsigned fpar, uint64_t ra,
+                                              uint64_t dd, uint64_t b) {
+  const uint64_t half = grid >> 1, base1 = ra * grid;
+  const bool favoured = (b & 1u) == fpar;
   q.s1 = base1 + (b >> 1);
   q.st1 = half;
-  q.n1 = favoured ? dd : 0;
+  q.n1 = favoured ? static_cast<uint32_t>(dd) : 0u;
   const uint64_t base2 = base1 + dd * half, left = ntiles - base2;  // < grid
   const uint64_t rank2 = favoured ? (b >> 1) : half + (b >> 1);   // favoured workgroups first
   q.s2 = base2 + rank2;
   q.n2 = rank2 < left ? 1 : 0;
+}
+
+// Workgroup b's tiles of the interleaved split of `ntiles` over `grid` workgroups with the blockIdx
+// parity `fpar` favoured (skewed: even grid, `ra` / `dd` precomputed on the host — no 64-bit
+// division on the device). Unskewed: tiles b, b + grid, ... (run 0 over the ra = ntiles / grid
+// whole rounds, run 2 = the leftover tile of the first ntiles % grid workgroups).
+// GPU test: tests/test_kernels_gpu.py::test_xcd_weighted_split.
+__device__ __forceinline__ TileSeq weighted_tiles(uint64_t ntiles, uint64_t grid, bool skewed, unsigned fpar,
+                                                  uint64_t ra, uint64_t dd, uint64_t b) {
+  TileSeq q{};
+  q.s0 = b;
+  q.st0 = grid;
+  q.n0 = static_cast<uint32_t>(ra);
+  if (!skewed) {
+    q.s2 = ra * grid + b;
+    q.n2 = b < ntiles - ra * grid ? 1 : 0;
+    return q;
+  }
+  weighted_tail(q, ntiles, grid, fpar, ra, dd, b);
   return q;
 }
 
+// Which XCD runs workgroup b is (b + the XCD of workgroup 0) % 8, and that start is not fixed per
+// launch: it follows the hardware queue (a stream of the process's own was dealt from another XCD
+// than torch's, profiles/r4_ab/), so the favoured blockIdx parity cannot be chosen on the host.
+// The launch's workgroup 0 publishes its XCC's parity, tagged with the launch's fan-in epoch, into
+// Workspace fan[2..3] (uncached); every workgroup loads it some tiles before its common rounds end
+// and derives the same favoured parity from it — the split stays a bijection whatever the deal.
+struct XcdAnchor {
+  uint64_t* word;     // null: the split is complete up front (q); else q is run 0 (>= 1 tile) only
+  unsigned favour;    // XCC parity taking the extra rounds (xskew > 0: odd)
+  bool publish;       // workgroup 0
+  unsigned* err;      // sticky error word (Workspace fan[1]); bit 2: the anchor never arrived
+  uint64_t bound;     // wait bound in wall-clock ticks
+  uint64_t ntiles, grid, ra, dd, b;
+};
+
+constexpr uint32_t kAnchorLead = 8;
+
+// this launch's fan-in epoch (fan[0] + 1, never 0: the tag of a zeroed slot)
+__device__ __forceinline__ unsigned fan_epoch(unsigned fan_raw) {
+  const unsigned e = __builtin_amdgcn_readfirstlane(fan_raw) + 1u;
+  return e == 0 ? 1u : e;
+}  // tiles before the common rounds end that the anchor is loaded
+
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  return static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v))) |
+         static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32))) << 32;
+}
+
+// The anchored runs 1 and 2: `w` is the anchor as loaded; re-polled (bounded) while it is an earlier
+// launch's.
+__device__ __forceinline__ void resolve_anchor(TileSeq& q, const XcdAnchor& x, unsigned fan_raw, uint64_t w) {
+  const uint64_t tag = static_cast<uint64_t>(fan_epoch(fan_raw)) << 32;
+  w = rfl64(w);
+  if ((w & ~0xffffffffull) != tag) {
+    const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
+    for (;;) {
+      __builtin_amdgcn_s_sleep(1);
+      w = rfl64(__hip_atomic_load(x.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if ((w & ~0xffffffffull) == tag) break;
+      if (static_cast<uint64_t>(wall_clock64()) - t0 > x.bound) {  // reported, never silent
+        if (threadIdx.x == 0) __hip_atomic_fetch_or(x.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        w = tag;
+        break;
+      }
+    }
+  }
+  // favoured blockIdx parity: the one that lands on XCCs of parity `favour`
+  weighted_tail(q, x.ntiles, x.grid, x.favour ^ static_cast<unsigned>(w & 1u), x.ra, x.dd, x.b);
+  q.s1 = rfl64(q.s1), q.st1 = rfl64(q.st1), q.s2 = rfl64(q.s2);
+  q.n1 = __builtin_amdgcn_readfirstlane(q.n1), q.n2 = __builtin_amdgcn_readfirstlane(q.n2);
+  if (q.n1 == 0) q.s1 = q.s2, q.n1 = q.n2, q.n2 = 0;
+}
+
+// The window body over a TileSeq. The next tile is found incrementally with 32-bit uniform counters
+// (scalar compares and branches: gfx950's SALU has no 64-bit less-than, and a first version that
+// indexed the runs with 64-bit compares put them on the VALU in front of every tile's loads, 0.15-0.4 %
+// slower than the single-run loop, profiles/r4_ab/). With an anchor, runs 1 and 2 are resolved when
+// run 0 ends; the loop is split where the anchor's load issues (no load under a branch in the loop:
+// hipcc's wait counts would turn conservative for every tile).
 template <class OpT, class T, class AccT, class V, int N, int BLOCK, int UNROLL, int WIN>
-__device__ __forceinline__ void stream_window_seq(AccT (&acc)[UNROLL], const V* __restrict__ vin, const TileSeq& q) {
+__device__ __forceinline__ uint32_t stream_window_seq(AccT (&acc)[UNROLL], const V* __restrict__ vin, TileSeq q,
+                                                      const XcdAnchor& x, unsigned fan_raw) {
   static_assert(UNROLL % WIN == 0, "the window must divide the unroll");
   constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
   constexpr uint32_t kStride = BLOCK * 16;
-  const uint64_t n = q.count();
-  if (n == 0) return;
+  // every field is uniform over the workgroup; say so, or the divergence analysis may keep them in
+  // VGPRs and wrap each tile's loads in a readfirstlane waterfall loop
+  q.s0 = rfl64(q.s0), q.st0 = rfl64(q.st0), q.s1 = rfl64(q.s1), q.st1 = rfl64(q.st1), q.s2 = rfl64(q.s2);
+  q.n0 = __builtin_amdgcn_readfirstlane(q.n0), q.n1 = __builtin_amdgcn_readfirstlane(q.n1);
+  q.n2 = __builtin_amdgcn_readfirstlane(q.n2);
+  const bool anchored = x.word != nullptr;
+  // runs in order, empty ones dropped: (start, step, count) of the current run, then the rest
+  if (q.n0 == 0) {
+    q.s0 = q.s1, q.st0 = q.st1, q.n0 = q.n1;
+    q.s1 = q.s2, q.n1 = q.n2, q.n2 = 0;
+    if (q.n0 == 0) q.s0 = q.s1, q.n0 = q.n1, q.n1 = 0;
+  } else if (q.n1 == 0) {
+    q.s1 = q.s2, q.n1 = q.n2, q.n2 = 0;
+  }
+  const bool pending = anchored;  // runs 1 and 2 resolved when run 0 (>= 1 tile when anchored) ends
+  uint32_t n = q.count();  // tiles left, the current one included (run 0's only while pending)
+  if (n == 0) return 0;
+  uint32_t total = n;
+  uint64_t t = q.s0, st = q.st0;
+  uint32_t left = q.n0;  // tiles of the current run from t on
   const uint32_t voff = threadIdx.x * 16;
-  __amdgpu_buffer_rsrc_t rp = tile_rsrc(vin + q.at(0) * kTile);
+  __amdgpu_buffer_rsrc_t rp = tile_rsrc(vin + t * kTile);
   V buf[WIN];
 #pragma unroll
   for (int j = 0; j < WIN; ++j) buf[j] = ld_buf_nt<V>(rp, voff, j * kStride);
-  for (uint64_t i = 0; i + 1 < n; ++i) {  // the same loose window as stream_window
-    const __amdgpu_buffer_rsrc_t rq = tile_rsrc(vin + q.at(i + 1) * kTile);
+  // Workgroup 0 publishes its XCC's parity for this launch, after the first loads: the tag's wait
+  // (the fan-in epoch, loaded at the kernel's start) is then no later than the first consume's.
+  if (anchored && x.publish && threadIdx.x == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const uint64_t tag = static_cast<uint64_t>(fan_epoch(fan_raw)) << 32;
+    __hip_atomic_store(x.word, tag | (xcc & 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  auto step = [&]() {  // the next tile's loads under this one's consume: the loose window of stream_window
+    if (left > 1) {
+      t += st;
+      --left;
+    } else {  // the next run (runs 1 and 2 share run 1's step; run 2 holds at most one tile)
+      t = q.s1;
+      st = q.st1;
+      left = q.n1;
+      q.s1 = q.s2;
+      q.n1 = q.n2;
+      q.n2 = 0;
+    }
+    const __amdgpu_buffer_rsrc_t rq = tile_rsrc(vin + t * kTile);
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
 #pragma unroll
@@ -388,14 +487,38 @@ __device__ __forceinline__ void stream_window_seq(AccT (&acc)[UNROLL], const V* 
       __builtin_amdgcn_sched_barrier(0);
     }
     rp = rq;
+  };
+  // (no unrolling: a constant-trip copy is straight-line code, where hipcc hoists every tile's loads
+  // to the top — the window gone)
+  if (pending) {
+    if (n > kAnchorLead) {
+#pragma nounroll
+      for (; n > kAnchorLead; --n) step();
+      // the anchor's load, then one straight-line tile: every path to its use has >= WIN loads
+      // issued after it, so its wait is vmcnt(WIN), not a drain of the window
+      const uint64_t w = __hip_atomic_load(x.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      step();
+#pragma nounroll
+      for (--n; n > 1; --n) step();
+      resolve_anchor(q, x, fan_raw, w);
+    } else {
+#pragma nounroll
+      for (; n > 1; --n) step();
+      resolve_anchor(q, x, fan_raw, __hip_atomic_load(x.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    n += q.n1 + q.n2;
+    total += q.n1 + q.n2;
   }
+#pragma nounroll
+  for (; n > 1; --n) step();
 #pragma unroll
-  for (int u = 0; u < UNROLL; ++u) {
+  for (int u = 0; u < UNROLL; ++u) {  // the last tile: no loads of a next one
 #pragma unroll
     for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(buf[u % WIN], k)));
     const int j = u + WIN;
     if (j < UNROLL) buf[u % WIN] = ld_buf_nt<V>(rp, voff, j * kStride);
   }
+  return total;
 }
 
 // PIPE: software-pipelined body — tile t+grid's loads are issued before tile t is consumed, so
@@ -453,6 +576,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       }
     }
   }
+  uint32_t streamed = 0;  // full tiles of the window body (diagnostic stamps)
   if constexpr (PIPE) {
     if (t0 < t1) {
       V cur[UNROLL];
@@ -469,14 +593,28 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   } else if constexpr (WIN > 0) {
     // one window body for every split: contiguous runs, whole rounds (balanced), or interleaved
     TileSeq q{};
+    XcdAnchor x{};
     if (a.contig || balanced) {
       q.s0 = t0;
       q.st0 = step;
-      q.n0 = t1 > t0 ? (t1 - t0 + step - 1) / step : 0;
-    } else {
-      q = weighted_tiles(ntiles, grid, a.xskew, a.x_ra, a.x_dd, blockIdx.x);
+      q.n0 = t1 > t0 ? static_cast<uint32_t>((t1 - t0 + step - 1) / step) : 0u;
+    } else if (a.xskew != 0 && polled && (grid & 1u) == 0 && a.x_ra > 0) {  // weighted, anchored to the XCDs
+      q.s0 = blockIdx.x;
+      q.st0 = grid;
+      q.n0 = static_cast<uint32_t>(a.x_ra);
+      x.word = reinterpret_cast<uint64_t*>(a.fan + 2);
+      x.favour = a.xskew > 0 ? 1u : 0u;
+      x.publish = blockIdx.x == 0;
+      x.err = a.fan + 1;
+      x.bound = a.fan_bound;
+      x.ntiles = ntiles, x.grid = grid, x.ra = a.x_ra, x.dd = a.x_dd, x.b = blockIdx.x;
+    } else {  // unskewed, or skewed by blockIdx parity (no fan-in epoch to tag an anchor with)
+      q = weighted_tiles(ntiles, grid, a.xskew != 0 && (grid & 1u) == 0, a.xskew > 0 ? 1u : 0u, a.x_ra, a.x_dd,
+                         blockIdx.x);
     }
-    stream_window_seq<OpT, T, AccT, V, N, BLOCK, UNROLL, WIN>(acc, vin, q);
+    // fan_raw (the launch's fan-in epoch, the anchor's tag) passed as is: a copy into the struct
+    // would be a VGPR move that waits for its load before the first tile's loads issue
+    streamed = stream_window_seq<OpT, T, AccT, V, N, BLOCK, UNROLL, WIN>(acc, vin, q, x, fan_raw);
   } else if constexpr (WIN < 0) {  // strict window (experiments only: tools/window_ab.hip)
     stream_window<OpT, T, AccT, V, N, BLOCK, UNROLL, -WIN, true>(acc, vin, t0, t1, step);
   } else {
@@ -546,8 +684,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     uint64_t* st = a.wg_stamps + 3 * static_cast<uint64_t>(blockIdx.x);
     st[0] = t_end;
     st[1] = xcc & 0xfu;
-    st[2] = (WIN > 0 && !a.contig && !balanced) ? weighted_tiles(ntiles, grid, a.xskew, a.x_ra, a.x_dd, blockIdx.x).count()
-            : a.contig ? t1 - t0 : (t1 > t0 ? (t1 - t0 + step - 1) / step : 0);
+    st[2] = WIN > 0 ? streamed : a.contig ? t1 - t0 : (t1 > t0 ? (t1 - t0 + step - 1) / step : 0);
   }
 
   // Fused cross-rank finish: this launch's epoch (counter + 1; only the finishing workgroup bumps
@@ -593,8 +730,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   // instead of store, drain, ticket (x2) and a load round. Slots live in uncached memory, so
   // polls always see the other XCDs' stores.
   if (a.slots) {
-    unsigned fan_e = __builtin_amdgcn_readfirstlane(fan_raw) + 1u;
-    if (fan_e == 0) fan_e = 1;  // 0 is the tag of a zeroed slot
+    const unsigned fan_e = fan_epoch(fan_raw);
     const uint64_t tag = static_cast<uint64_t>(fan_e) << 32;
     if (threadIdx.x == 0) {
       if (static_cast<int>(blockIdx.x) == a.delay_wg) {  // test hook: a slow workgroup
@@ -678,6 +814,8 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       __syncthreads();
       for (unsigned i = threadIdx.x; i < 2u * a.fan_slots; i += BLOCK)
         __hip_atomic_store(a.slots + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x == 0)  // and the XCD anchor (XcdAnchor), tagged with the same epochs
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(a.fan + 2), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
     }
     if (threadIdx.x < 64) {

@@ -435,8 +435,46 @@ def test_xcd_weighted_split(monkeypatch, permille, n, op):
                     out.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert plan["window"] > 0 and plan["grid"] % 2 == 0, plan
-    rounds = n // 2 // (plan["block"] * plan["unroll"]) // plan["grid"]
+    ntiles = n // 2 // (plan["block"] * plan["unroll"])
+    rounds = ntiles // plan["grid"]
     q = rounds * permille + (500 if permille >= 0 else -500)  # the planner's rounding (half away from 0)
-    assert plan["xskew"] == (abs(q) // 1000) * (1 if q >= 0 else -1), plan
+    d = (abs(q) // 1000) * (1 if q >= 0 else -1)
+    # no skew when it would leave no common round (the kernel anchors the split at their end)
+    assert plan["xskew"] == (d if abs(d) * (plan["grid"] // 2) + plan["grid"] <= ntiles else 0), plan
     exp = x.sum().item() if op == "sum" else x.max().item()
     assert out.item() == exp and red.check() is None
+
+
+@pytest.mark.parametrize("permille", [100, -100])
+@pytest.mark.parametrize("stream", ["current", "side"])
+def test_xcd_weighted_split_follows_the_xccs(monkeypatch, permille, stream):
+    # The weighted split is anchored to the XCDs, not to blockIdx parity (XcdAnchor): which XCD
+    # runs workgroup 0 follows the hardware queue (profiles/r4_ab/), so workgroup 0 publishes its
+    # XCC's parity and every workgroup derives the favoured blockIdx parity from it. On torch's
+    # stream and on a side stream (another queue), the workgroups with the extra rounds are exactly
+    # those on odd (permille > 0) / even XCCs (the production kernel's own stamps: XCC, tiles), and
+    # the sum stays exact.
+    monkeypatch.setenv("MIREDUCE_XCD_SKEW", str(permille))
+    C = native()
+    n = 26_000_003
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randint(-(1 << 40), 1 << 40, (n,), generator=g, dtype=torch.int64).to(DEV)
+    red = Reducer(torch.device(DEV))
+    out = torch.zeros(1, dtype=torch.int64, device=DEV)
+    st = torch.zeros(3 * red.ws.max_grid, dtype=torch.int64, device=DEV)
+    s = torch.cuda.current_stream() if stream == "current" else torch.cuda.Stream()
+    from cuda_mpi_reductions_amd.ops import dtype_code, op_code
+    torch.cuda.synchronize()
+    for k in range(3):  # later launches too: the anchor word carries an earlier launch's tag
+        plan = C.reduce(red.ws, x.data_ptr(), n, dtype_code(x.dtype), op_code("sum"), dtype_code(torch.int64),
+                        out.data_ptr(), s.cuda_stream, wg_stamps=st.data_ptr())
+        s.synchronize()
+        assert out.item() == x.sum().item() and red.check() is None
+        assert plan["xskew"] != 0 and plan["xskew"] * permille > 0, plan
+        grid = plan["grid"]
+        v = st[: 3 * grid].view(grid, 3).cpu()
+        odd = v[:, 1] % 2 == 1
+        fav, other = (v[odd, 2], v[~odd, 2]) if permille > 0 else (v[~odd, 2], v[odd, 2])
+        assert len(fav) == len(other) == grid // 2, (len(fav), len(other))
+        assert int(fav.min()) > int(other.max()), (fav.tolist()[:8], other.tolist()[:8])
+        assert int(v[:, 2].sum()) == n // 2 // (plan["block"] * plan["unroll"])  # every full tile once

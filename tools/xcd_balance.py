@@ -39,12 +39,14 @@ def main(argv=None) -> int:
                          "round on the same array (default: the plan's own)")
     ap.add_argument("--offset-tiles", type=int, default=0,
                     help="start the array this many 32 KB tiles into its allocation (address-residue test)")
+    ap.add_argument("--stream", choices=("current", "new"), default="current",
+                    help="launch on torch's current stream or on a new one (another hardware queue)")
     a = ap.parse_args(argv)
     C = native()
     dev = torch.device("cuda", 0)
     red = Reducer(dev)
     out = torch.zeros(1, dtype=torch.float64, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.current_stream(dev) if a.stream == "current" else torch.cuda.Stream(dev)
     skews = [None] if a.skews is None else [int(v) for v in a.skews.split(",")]
     off = a.offset_tiles * 4096  # 32 KB tiles of float64
     for n in (int(float(x)) for x in a.sizes.split(",")):
@@ -64,10 +66,10 @@ def main(argv=None) -> int:
             plan = launch()
             grid = plan["grid"]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
+            e0.record(stream)
             for _ in range(a.launches):
                 launch()
-            e1.record()
+            e1.record(stream)
             launch(stamps.data_ptr())
             torch.cuda.synchronize()
             us_per = e0.elapsed_time(e1) * 1e3 / a.launches
@@ -75,8 +77,11 @@ def main(argv=None) -> int:
             end = (st[:, 0] - st[:, 0].min()).double() / TICKS_PER_US
             xcc = st[:, 1]
             srt = end.sort().values
+            # XCC of workgroup b minus b % 8: one constant when the dispatcher deals round-robin
+            rot = ((xcc - torch.arange(grid)) % 8).tolist()
             per = {int(k): round(float(end[xcc == k].mean()), 2) for k in sorted(set(xcc.tolist()))}
-            row = {"n": n, "round": r, "skew": sk, "xskew": plan.get("xskew"), "offset_tiles": a.offset_tiles,
+            row = {"n": n, "round": r, "skew": sk, "xskew": plan.get("xskew"), "offset_tiles": a.offset_tiles, "stream": a.stream,
+                   "xcc_rotation": {int(k): rot.count(k) for k in sorted(set(rot))},
                    "base_mod_2mb": int(x.data_ptr() % (2 << 20)), "grid": grid, "us_per_launch": round(us_per, 2),
                    "end_spread_us": {"p50": round(float(srt[grid // 2]), 2),
                                      "p99": round(float(srt[int(0.99 * (grid - 1))]), 2),

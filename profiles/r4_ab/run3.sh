@@ -1,11 +1,12 @@
 #!/bin/bash
 # Round 4: (1) the incremental 32-bit TileSeq walker vs the pre-TileSeq build (same box, skew 0),
-# (2) does the blockIdx -> XCC deal depend on the stream (hardware queue)? The reduction app (own
+# (2) does the blockIdx -> XCC deal depend on the stream (hardware queue)? (3) the XCD-anchored split
+# (XcdAnchor) at skew +-20 in the app. The reduction app (own
 # non-blocking stream) measured skew 20 slower, tools/xcd_balance.py (torch's current stream) faster.
 set -o pipefail
 O=${O:-gpurun_out/r4_ab3}
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
     tests/test_kernels_gpu.py tests/test_fanin_gpu.py > $O/pytest.txt 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/status.txt; [ $rc -eq 0 ] || exit $rc
 for st in current new; do

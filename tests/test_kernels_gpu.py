@@ -449,9 +449,10 @@ def test_xcd_weighted_split(monkeypatch, permille, n, op):
 @pytest.mark.parametrize("stream", ["current", "side"])
 def test_xcd_weighted_split_follows_the_xccs(monkeypatch, permille, stream):
     # The weighted split is anchored to the XCDs, not to blockIdx parity (XcdAnchor): which XCD
-    # runs workgroup 0 follows the hardware queue (profiles/r4_ab/), so workgroup 0 publishes its
-    # XCC's parity and every workgroup derives the favoured blockIdx parity from it. On torch's
-    # stream and on a side stream (another queue), the workgroups with the extra rounds are exactly
+    # runs workgroup 0 is not fixed (the reduction app's launches were dealt otherwise than
+    # tools/xcd_balance.py's, profiles/r4_ab/), so workgroup 0 publishes its XCC's parity and
+    # every workgroup derives the favoured blockIdx parity from it. On torch's stream and on a
+    # side stream, the workgroups with the extra rounds are exactly
     # those on odd (permille > 0) / even XCCs (the production kernel's own stamps: XCC, tiles), and
     # the sum stays exact.
     monkeypatch.setenv("MIREDUCE_XCD_SKEW", str(permille))

@@ -367,9 +367,10 @@ __device__ __forceinline__ TileSeq weighted_tiles(uint64_t ntiles, uint64_t grid
   return q;
 }
 
-// Which XCD runs workgroup b is (b + the XCD of workgroup 0) % 8, and that start is not fixed per
-// launch: it follows the hardware queue (a stream of the process's own was dealt from another XCD
-// than torch's, profiles/r4_ab/), so the favoured blockIdx parity cannot be chosen on the host.
+// Which XCD runs workgroup b is (b + the XCD of workgroup 0) % 8, and that start is not fixed:
+// tools/xcd_balance.py always saw workgroup 0 on XCC 0, but the reduction app's launches were
+// dealt otherwise (favouring odd blockIdx slowed it, odd XCCs speed it up; profiles/r4_ab/), so
+// the favoured blockIdx parity cannot be chosen on the host.
 // The launch's workgroup 0 publishes its XCC's parity, tagged with the launch's fan-in epoch, into
 // Workspace fan[2..3] (uncached); every workgroup loads it some tiles before its common rounds end
 // and derives the same favoured parity from it — the split stays a bijection whatever the deal.

@@ -169,21 +169,43 @@ bool split_contiguous() {
   return false;
 }
 
+// `fan` non-null: the second level of a two-pass reduce_stream launch, which ends its fan-in epoch
+// (kern::finalize).
+struct FanEnd {
+  unsigned* fan = nullptr;
+  uint64_t* slots = nullptr;
+  unsigned fan_slots = 0;
+};
+
 template <class OpT, class AccT>
-void launch_finalize(const void* partials, uint64_t count, void* out, hipStream_t s) {
+void launch_finalize(const void* partials, uint64_t count, void* out, hipStream_t s, const FanEnd& f) {
   hipLaunchKernelGGL((kern::finalize<OpT, AccT>), dim3(1), dim3(256), 0, s,
-                     static_cast<const AccT*>(partials), count, static_cast<AccT*>(out));
+                     static_cast<const AccT*>(partials), count, static_cast<AccT*>(out), f.fan, f.slots,
+                     f.fan_slots);
 }
 
 template <class OpT>
-void finalize_by_acc(DType acc, const void* partials, uint64_t count, void* out, hipStream_t s) {
+void finalize_by_acc(DType acc, const void* partials, uint64_t count, void* out, hipStream_t s,
+                     const FanEnd& f = FanEnd{}) {
   switch (acc) {
-    case DType::Int32: launch_finalize<OpT, int32_t>(partials, count, out, s); break;
-    case DType::Int64: launch_finalize<OpT, int64_t>(partials, count, out, s); break;
-    case DType::Float32: launch_finalize<OpT, float>(partials, count, out, s); break;
-    case DType::Float64: launch_finalize<OpT, double>(partials, count, out, s); break;
+    case DType::Int32: launch_finalize<OpT, int32_t>(partials, count, out, s, f); break;
+    case DType::Int64: launch_finalize<OpT, int64_t>(partials, count, out, s, f); break;
+    case DType::Float32: launch_finalize<OpT, float>(partials, count, out, s, f); break;
+    case DType::Float64: launch_finalize<OpT, double>(partials, count, out, s, f); break;
     default: MIREDUCE_REQUIRE(false, "finalize: accumulator must be int32, int64, float32 or float64");
   }
+}
+
+void fold_partials(const void* partials, uint64_t count, DType acc, Op op, void* out, hipStream_t stream,
+                   const FanEnd& f) {
+  switch (op) {  // partials are already transformed: SUMSQ folds like SUM, AMAX like MAX
+    case Op::Sum:
+    case Op::SumSq: finalize_by_acc<SumOp>(acc, partials, count, out, stream, f); break;
+    case Op::Min: finalize_by_acc<MinOp>(acc, partials, count, out, stream, f); break;
+    case Op::Max:
+    case Op::AbsMax: finalize_by_acc<MaxOp>(acc, partials, count, out, stream, f); break;
+  }
+  MIREDUCE_HIP_THROW(hipGetLastError());
 }
 
 template <class OpT, class T>
@@ -317,8 +339,10 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   p.balanced = !p.contiguous && balance_leftover();
   // XCD-weighted split (window bodies, interleaved, even grids): permille of the rounds per
   // workgroup -> extra rounds for one parity. MIREDUCE_XCD_SKEW=<permille> overrides (A/B runs).
-  // Polled fan-in only: the kernel anchors the favoured parity to the XCDs with the fan-in epoch.
-  if (p.window > 0 && !p.contiguous && !p.balanced && p.grid % 2 == 0 && p.poll && p.grid > 1) {
+  // Launches with a fan-in epoch only (the polled fan-in, or two-pass: its finalize ends the epoch):
+  // the kernel anchors the favoured parity to the XCDs with it.
+  if (p.window > 0 && !p.contiguous && !p.balanced && p.grid % 2 == 0 && (p.poll || !p.single_pass) &&
+      p.grid > 1) {
     int permille = cfg.xcd_skew == (-2147483647 - 1) ? tuned_xcd_skew(t, p) : cfg.xcd_skew;
     if (const char* e = std::getenv("MIREDUCE_XCD_SKEW")) permille = std::atoi(e);
     const uint64_t tile = static_cast<uint64_t>(p.block) * static_cast<uint64_t>(p.unroll);
@@ -362,6 +386,18 @@ static kern::Args make_args(const void* in, const LaunchPlan& p, DType t, const 
   return a;
 }
 
+// The two-pass launch's finalize ends the first level's fan-in epoch (grid > 1: a one-workgroup
+// first level reads no epoch).
+static FanEnd fan_end(const kern::Args& a, const Workspace& ws) {
+  FanEnd f;
+  if (a.two_pass_epoch) {
+    f.fan = a.fan;
+    f.slots = ws.slots();
+    f.fan_slots = a.fan_slots;
+  }
+  return f;
+}
+
 LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
                   hipStream_t stream, const ReduceConfig& cfg) {
   const int c = combo_index(op, t, acc);
@@ -378,11 +414,12 @@ LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out
   a.slots = p.poll ? ws.slots() : nullptr;
   a.fan = ws.fan();
   a.fan_slots = static_cast<unsigned>(ws.max_grid());
+  a.two_pass_epoch = p.single_pass ? 0 : 1;
   a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
   const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][body_index(p)];
   fn(a, p.grid, stream);
   MIREDUCE_HIP_THROW(hipGetLastError());
-  if (!p.single_pass) reduce_finalize(ws.partials(), p.grid, acc, op, out, stream);
+  if (!p.single_pass) fold_partials(ws.partials(), p.grid, acc, op, out, stream, fan_end(a, ws));
   return p;
 }
 
@@ -429,6 +466,7 @@ BoundReduce::BoundReduce(const void* in, size_t n, DType t, Op op, DType acc, vo
   a.slots = p.poll ? ws.slots() : nullptr;
   a.fan = ws.fan();
   a.fan_slots = static_cast<unsigned>(ws.max_grid());
+  a.two_pass_epoch = p.single_pass ? 0 : 1;
   a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
   impl_ = new Impl{a, table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][body_index(p)],
                    p, op, acc, &ws};
@@ -441,7 +479,8 @@ void BoundReduce::launch(hipStream_t stream, void* out) const {
   if (out) a.out = out;
   impl_->fn(a, impl_->plan.grid, stream);
   MIREDUCE_HIP_THROW(hipGetLastError());
-  if (!impl_->plan.single_pass) reduce_finalize(a.partials, impl_->plan.grid, impl_->acc, impl_->op, a.out, stream);
+  if (!impl_->plan.single_pass)
+    fold_partials(a.partials, impl_->plan.grid, impl_->acc, impl_->op, a.out, stream, fan_end(a, *impl_->ws));
 }
 
 const LaunchPlan& BoundReduce::plan() const { return impl_->plan; }
@@ -491,14 +530,7 @@ ReducePasses reduce_passes(const void* in, size_t n, DType t, Op op, DType acc, 
 
 void reduce_finalize(const void* partials, size_t count, DType acc, Op op, void* out,
                      hipStream_t stream) {
-  switch (op) {  // partials are already transformed: SUMSQ folds like SUM, AMAX like MAX
-    case Op::Sum:
-    case Op::SumSq: finalize_by_acc<SumOp>(acc, partials, count, out, stream); break;
-    case Op::Min: finalize_by_acc<MinOp>(acc, partials, count, out, stream); break;
-    case Op::Max:
-    case Op::AbsMax: finalize_by_acc<MaxOp>(acc, partials, count, out, stream); break;
-  }
-  MIREDUCE_HIP_THROW(hipGetLastError());
+  fold_partials(partials, count, acc, op, out, stream, FanEnd{});
 }
 
 void combine_elementwise(void* inout, const void* other, size_t n, DType t, Op op,

@@ -93,6 +93,7 @@ struct Args {
                            // tiles for the workgroups on odd (xskew > 0) or even (< 0) XCCs; 0 = equal
   uint64_t x_ra;           // weighted split, precomputed on the host: common rounds (ntiles / grid at 0)
   uint64_t x_dd;           // extra rounds actually given to the favoured parity
+  int two_pass_epoch;      // two-pass launch whose finalize ends the fan-in epoch (fan[0]; XcdAnchor)
 };
 
 // Polled fan-in: a published partial is two 8-byte words (epoch << 32 | 32 data bits), where the
@@ -541,7 +542,9 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   // pins that no wait sits between it and the body). Every workgroup reads it before the finisher
   // can advance it: the finisher advances fan[0] only after every slot holds this epoch.
   const bool polled = a.slots && gridDim.x > 1;
-  const unsigned fan_raw = polled ? __hip_atomic_load(a.fan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  // the launch's fan-in epoch: the polled fan-in's, or a two-pass launch's (its finalize ends it)
+  const bool epoch = (polled || a.two_pass_epoch) && gridDim.x > 1;
+  const unsigned fan_raw = epoch ? __hip_atomic_load(a.fan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
 
   const V* __restrict__ vin = static_cast<const V*>(a.body);
   constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
@@ -599,7 +602,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       q.s0 = t0;
       q.st0 = step;
       q.n0 = t1 > t0 ? static_cast<uint32_t>((t1 - t0 + step - 1) / step) : 0u;
-    } else if (a.xskew != 0 && polled && (grid & 1u) == 0 && a.x_ra > 0) {  // weighted, anchored to the XCDs
+    } else if (a.xskew != 0 && epoch && (grid & 1u) == 0 && a.x_ra > 0) {  // weighted, anchored to the XCDs
       q.s0 = blockIdx.x;
       q.st0 = grid;
       q.n0 = static_cast<uint32_t>(a.x_ra);
@@ -917,14 +920,30 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
 
 // Second level of the two-pass path (and the on-device fold for reduce_finalize): one
 // workgroup folds `count` values. Launched after a kernel boundary, so plain loads are fine.
+// `fan` (two-pass launches of reduce_stream; null otherwise): this launch then also ends the first
+// level's fan-in epoch, as the polled fan-in's finisher does (the first level's workgroups tag
+// the XCD anchor with it), zeroing the workspace's `fan_slots` polled slots and the anchor first
+// when the epoch wraps.
 template <class OpT, class AccT>
 __global__ __launch_bounds__(256) void finalize(const AccT* __restrict__ partials, uint64_t count,
-                                                AccT* __restrict__ out) {
+                                                AccT* __restrict__ out, unsigned* fan, uint64_t* slots,
+                                                unsigned fan_slots) {
   __shared__ AccT lds[4];
   AccT s = OpT::template identity<AccT>();
   for (uint64_t i = threadIdx.x; i < count; i += 256) s = OpT::apply(s, partials[i]);
   s = block_reduce<OpT, AccT, 256>(s, lds);
   if (threadIdx.x == 0) *out = s;
+  if (fan) {
+    const unsigned e = fan_epoch(__hip_atomic_load(fan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (e == 0xffffffffu) {  // the epoch wraps after this launch: invalidate every tag first
+      for (unsigned i = threadIdx.x; i < 2u * fan_slots; i += 256)
+        __hip_atomic_store(slots + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x == 0)
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(fan + 2), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(fan, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 template <class OpT, class T>

@@ -130,6 +130,30 @@ def test_fanin_epoch_wrap_invalidates_old_slots():
     assert outs.tolist() == exp and red.check() is None
 
 
+def test_xcd_anchor_across_the_epoch_wrap_single_and_two_pass(monkeypatch):
+    # The XCD-weighted split's anchor (XcdAnchor) is tagged with the launch's fan-in epoch, which
+    # the polled finisher or — two-pass — the finalize launch ends. Skewed launches of both kinds,
+    # interleaved on one workspace and across the epoch's wrap (both ends zero the slots and the
+    # anchor there): every result exact, no anchor wait ever timing out (error bit 2).
+    from cuda_mpi_reductions_amd._native import native
+    from cuda_mpi_reductions_amd.ops import Reducer
+    monkeypatch.setenv("MIREDUCE_XCD_SKEW", "100")
+    C = native()
+    dev = torch.device("cuda", 0)
+    n = 26_000_003
+    g = torch.Generator(device="cpu").manual_seed(17)
+    x = torch.randint(-(1 << 40), 1 << 40, (n,), generator=g, dtype=torch.int64).to(dev)
+    exp = x.sum().item()
+    red = Reducer(dev)
+    outs = torch.zeros(8, dtype=torch.int64, device=dev)
+    _set_epoch(C, red, 0xFFFFFFFB)
+    for i in range(8):  # epochs 0xfffffffc .. 0xffffffff (wrap), 1, 2, 3, 4
+        plan = _launch(C, red, x, outs[i:i + 1], single_pass=(i % 2 == 0))
+        assert plan["xskew"] > 0 and plan["single_pass"] == (i % 2 == 0), plan
+    torch.cuda.synchronize()
+    assert outs.tolist() == [exp] * 8 and red.check() is None
+
+
 def test_fanin_slow_workgroup_within_bound_is_exact():
     # a straggler that publishes before the bound is simply waited for
     from cuda_mpi_reductions_amd._native import native

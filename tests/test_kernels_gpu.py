@@ -447,14 +447,16 @@ def test_xcd_weighted_split(monkeypatch, permille, n, op):
 
 @pytest.mark.parametrize("permille", [100, -100])
 @pytest.mark.parametrize("stream", ["current", "side"])
-def test_xcd_weighted_split_follows_the_xccs(monkeypatch, permille, stream):
+@pytest.mark.parametrize("single_pass", [True, False])
+def test_xcd_weighted_split_follows_the_xccs(monkeypatch, permille, stream, single_pass):
     # The weighted split is anchored to the XCDs, not to blockIdx parity (XcdAnchor): which XCD
     # runs workgroup 0 is not fixed (the reduction app's launches were dealt otherwise than
     # tools/xcd_balance.py's, profiles/r4_ab/), so workgroup 0 publishes its XCC's parity and
     # every workgroup derives the favoured blockIdx parity from it. On torch's stream and on a
     # side stream, the workgroups with the extra rounds are exactly
     # those on odd (permille > 0) / even XCCs (the production kernel's own stamps: XCC, tiles), and
-    # the sum stays exact.
+    # the sum stays exact — single-pass (polled fan-in epoch) and two-pass (the finalize launch ends
+    # the epoch).
     monkeypatch.setenv("MIREDUCE_XCD_SKEW", str(permille))
     C = native()
     n = 26_000_003
@@ -468,8 +470,9 @@ def test_xcd_weighted_split_follows_the_xccs(monkeypatch, permille, stream):
     torch.cuda.synchronize()
     for k in range(3):  # later launches too: the anchor word carries an earlier launch's tag
         plan = C.reduce(red.ws, x.data_ptr(), n, dtype_code(x.dtype), op_code("sum"), dtype_code(torch.int64),
-                        out.data_ptr(), s.cuda_stream, wg_stamps=st.data_ptr())
+                        out.data_ptr(), s.cuda_stream, single_pass=single_pass, wg_stamps=st.data_ptr())
         s.synchronize()
+        assert plan["single_pass"] == single_pass
         assert out.item() == x.sum().item() and red.check() is None
         assert plan["xskew"] != 0 and plan["xskew"] * permille > 0, plan
         grid = plan["grid"]

@@ -148,12 +148,11 @@ bool balance_leftover() {
 }
 
 // XCD-weighted split default (permille of the rounds per workgroup given extra to the workgroups
-// on odd XCCs; see plan_reduce, weighted_tiles and XcdAnchor). Measured for the 8-byte window plan on two boxes
-// (profiles/r4_xcd/): 0 -> 16 -> 24 permille take the 1 GB shard from 138.0-138.6 to 137.2-137.8 us
-// and 8 GB from 1092.1-1092.7 to 1086.3-1089.7 us, the even XCDs' late end gone from the stamps.
-// The fp32 window-4 plan wants the same (8 GB: 1106.5 -> 1099.1 us at 20, 1114.2 at -20;
-// profiles/r4_shard/); the bf16 one does not (1084.4 -> 1088.8 us at 20, profiles/r4_xcd/), and the
-// window-2 plans (int32 SUM, 16-bit MIN/MAX) are unmeasured: 0 there. bench.py re-measures
+// on odd XCCs; see plan_reduce, weighted_tiles and XcdAnchor). Measured per plan with the anchored
+// split (profiles/r4_skew/, 8 GB, 0 / 10 / 20 / 30): 20 is the best for every window-4 plan of 8-
+// and 4-byte elements (f64 MAX 1096.5 -> 1090.1 us, int64 MIN 1108.1 -> 1101.4, fp32 SUM 1107.8 ->
+// 1101.1, int32 MAX 1095.9 -> 1090.4; f64 SUM 1092.6 -> 1087.5, profiles/r4_ab/), 0 for bf16 (1089.5
+// at 0, 1105+ with any) and the window-2 int32 SUM plan (1102.5 at 0, 1105.7+). bench.py re-measures
 // 0 / default / 2x on the node for the headline's shards.
 int tuned_xcd_skew(DType t, const LaunchPlan& p) {
   const size_t es = dtype_size(t);

@@ -85,7 +85,7 @@ class KernelConfig:
     single_pass: bool = True
     pipelined: Optional[bool] = None    # None: tuned choice
     window: Optional[int] = None        # loads in flight per thread: None tuned, 0 hipcc's schedule, 2 | 4
-    xcd_skew: Optional[int] = None      # XCD-weighted split, permille of rounds (+: odd XCDs more); None tuned
+    xcd_skew: Optional[int] = None      # XCD-weighted split, permille of rounds (+: odd XCCs more); None tuned
 
     @property
     def policy(self) -> int:

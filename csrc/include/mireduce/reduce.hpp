@@ -36,8 +36,9 @@ struct ReduceConfig {
   // profiles/r3_window/.
   int window = -1;
   // XCD-weighted split of the interleaved window body, in permille of the rounds per workgroup:
-  // > 0 gives the odd workgroups (odd XCDs) that many more rounds, < 0 the even ones; 0 equal
-  // rounds; INT_MIN = tuned default. (profiles/r4_xcd/)
+  // > 0 gives the workgroups on odd XCCs that many more rounds, < 0 those on even ones; 0 equal
+  // rounds; INT_MIN = tuned default. Launches with a fan-in epoch only (polled single-pass or
+  // two-pass): the kernel anchors the parity on the device. (profiles/r4_xcd/, r4_ab/, r4_skew/)
   int xcd_skew = -2147483647 - 1;
   bool single_pass = true;   // last-arriver finalisation vs a second finalize launch
   // Fused cross-rank finish: XrankChannel::device_desc() (xrank.hpp). The launch then writes the

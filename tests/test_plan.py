@@ -53,8 +53,9 @@ def test_tuned_defaults_by_size():
     assert all(C.plan(0, n, F64)["nontemporal"] for n in (1, 1 << 20, 3 << 23, 1 << 25, 3 << 24, 1 << 27))
     i64 = C.plan(0, 10**9, 1)              # 8 GB of int64: like fp64
     assert (i64["block"], i64["unroll"], i64["grid"], i64["window"]) == (256, 8, 256, 4)
-    # XCD-weighted split (profiles/r4_xcd/): 20 permille of the rounds extra for the odd workgroups
-    # of 8-byte window plans; explicit values override; no window -> no skew; 4-byte: 0 until measured
+    # XCD-weighted split (profiles/r4_xcd/, r4_skew/): 20 permille of the rounds extra for the
+    # workgroups on odd XCCs in the 8- and 4-byte window-4 plans; explicit values override; no
+    # window -> no skew
     assert big["xskew"] == 19 and mid["xskew"] == 2     # 953 and 119 rounds per workgroup
     assert C.plan(0, 10**9, F64, xcd_skew=0)["xskew"] == 0 and C.plan(0, 10**9, F64, xcd_skew=-40)["xskew"] == -38
     assert small["xskew"] == 0

@@ -494,6 +494,7 @@ LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, 
   c2.single_pass = false;
   c2.xrank = nullptr;
   LaunchPlan p = plan_reduce(in, n, t, c2, num_cus, max_grid, op);
+  p.xskew = 0;  // no workspace, so no fan-in epoch to anchor the XCD-weighted split with: equal rounds
   kern::Args a = make_args(in, p, t, c2);
   a.partials = partials;
   a.groups = 0;

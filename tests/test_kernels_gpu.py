@@ -445,6 +445,18 @@ def test_xcd_weighted_split(monkeypatch, permille, n, op):
     assert out.item() == exp and red.check() is None
 
 
+def test_reduce_partials_is_unskewed(monkeypatch):
+    # reduce_partials has no workspace, so no fan-in epoch to anchor the weighted split with: it
+    # streams equal rounds even under an explicit skew, and its partials fold to the exact sum
+    monkeypatch.setenv("MIREDUCE_XCD_SKEW", "100")
+    n = 26_000_003
+    g = torch.Generator(device="cpu").manual_seed(23)
+    x = torch.randint(-(1 << 40), 1 << 40, (n,), generator=g, dtype=torch.int64).to(DEV)
+    parts, plan = reduce_partials(x, "sum")
+    assert plan["window"] > 0 and plan["xskew"] == 0, plan
+    assert parts.sum().item() == x.sum().item()
+
+
 @pytest.mark.parametrize("permille", [100, -100])
 @pytest.mark.parametrize("stream", ["current", "side"])
 @pytest.mark.parametrize("single_pass", [True, False])

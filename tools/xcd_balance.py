@@ -23,14 +23,15 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from cuda_mpi_reductions_amd._native import native  # noqa: E402
-from cuda_mpi_reductions_amd.ops import Reducer, dtype_code, fill_, op_code  # noqa: E402
+from cuda_mpi_reductions_amd.ops import Reducer, default_acc_dtype, dtype_code, fill_, op_code  # noqa: E402
 
 TICKS_PER_US = 100.0  # gfx950 wall clock: 100 MHz
 
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
-    ap.add_argument("--sizes", default="125000000,1000000000", help="float64 element counts")
+    ap.add_argument("--sizes", default="125000000,1000000000", help="element counts")
+    ap.add_argument("--dtype", default="float64", choices=("float64", "float32", "bfloat16", "int64", "int32"))
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--json", default=None, help="append one JSON object per (size, round)")
@@ -45,18 +46,20 @@ def main(argv=None) -> int:
     C = native()
     dev = torch.device("cuda", 0)
     red = Reducer(dev)
-    out = torch.zeros(1, dtype=torch.float64, device=dev)
+    dt = getattr(torch, a.dtype)
+    acc = default_acc_dtype(dt, "sum")
+    out = torch.zeros(1, dtype=acc, device=dev)
     stream = torch.cuda.current_stream(dev) if a.stream == "current" else torch.cuda.Stream(dev)
     skews = [None] if a.skews is None else [int(v) for v in a.skews.split(",")]
-    off = a.offset_tiles * 4096  # 32 KB tiles of float64
+    off = a.offset_tiles * (32768 // torch.empty(0, dtype=dt).element_size())  # 32 KB tiles
     for n in (int(float(x)) for x in a.sizes.split(",")):
-        base = torch.empty(n + off, dtype=torch.float64, device=dev)
+        base = torch.empty(n + off, dtype=dt, device=dev)
         x = base[off:]
-        fill_(x, "uniform", seed=11)
+        fill_(x, "uniform" if dt.is_floating_point else "fullrange", seed=11)
         stamps = torch.zeros(3 * red.ws.max_grid, dtype=torch.int64, device=dev)
 
         def launch(st=0):
-            return C.reduce(red.ws, x.data_ptr(), n, dtype_code(x.dtype), op_code("sum"), dtype_code(torch.float64),
+            return C.reduce(red.ws, x.data_ptr(), n, dtype_code(x.dtype), op_code("sum"), dtype_code(acc),
                             out.data_ptr(), stream.cuda_stream, wg_stamps=st)
         for r, sk in ((r, sk) for r in range(a.rounds) for sk in skews):
             if sk is None:
@@ -80,7 +83,7 @@ def main(argv=None) -> int:
             # XCC of workgroup b minus b % 8: one constant when the dispatcher deals round-robin
             rot = ((xcc - torch.arange(grid)) % 8).tolist()
             per = {int(k): round(float(end[xcc == k].mean()), 2) for k in sorted(set(xcc.tolist()))}
-            row = {"n": n, "round": r, "skew": sk, "xskew": plan.get("xskew"), "offset_tiles": a.offset_tiles, "stream": a.stream,
+            row = {"n": n, "dtype": a.dtype, "round": r, "skew": sk, "xskew": plan.get("xskew"), "offset_tiles": a.offset_tiles, "stream": a.stream,
                    "xcc_rotation": {int(k): rot.count(k) for k in sorted(set(rot))},
                    "base_mod_2mb": int(x.data_ptr() % (2 << 20)), "grid": grid, "us_per_launch": round(us_per, 2),
                    "end_spread_us": {"p50": round(float(srt[grid // 2]), 2),

@@ -45,7 +45,7 @@ COMMLIB     := $(BUILD)/lib/libmireduce_comm.a
 APPS := $(BUILD)/bin/reduction $(BUILD)/bin/reduce_xgmi $(BUILD)/bin/bandwidth_test
 MPI_APP := $(BUILD)/bin/reduce_mpi
 
-.PHONY: all python apps mpi clean asan tsan unit diag examples window_ab
+.PHONY: all python apps mpi clean asan tsan unit diag examples window_ab dyntail_ab
 all: python apps mpi unit diag examples
 
 python: $(PYEXT)
@@ -116,6 +116,15 @@ $(BUILD)/obj/tools/window_ab.o: tools/window_ab.hip $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 $(BUILD)/bin/window_ab: $(BUILD)/obj/tools/window_ab.o $(LIB)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive $(LDLIBS) -o $@
+
+# Experiment: a workgroup-level dynamic tail vs the static XCD-weighted split (tools/dyntail_ab.hip).
+dyntail_ab: $(BUILD)/bin/dyntail_ab
+$(BUILD)/obj/tools/dyntail_ab.o: tools/dyntail_ab.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+$(BUILD)/bin/dyntail_ab: $(BUILD)/obj/tools/dyntail_ab.o $(LIB)
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive $(LDLIBS) -o $@
 

@@ -88,7 +88,8 @@ template <int B, int U, int W>
 void launch_global_window(const kern::Args& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL((global_window<B, U, W>), dim3(grid), dim3(B), 0, s, a);
   hipLaunchKernelGGL((kern::finalize<SumOp, double>), dim3(1), dim3(256), 0, s,
-                     static_cast<const double*>(a.partials), static_cast<uint64_t>(grid), static_cast<double*>(a.out));
+                     static_cast<const double*>(a.partials), static_cast<uint64_t>(grid), static_cast<double*>(a.out),
+                     nullptr, nullptr, 0u);
 }
 
 template <int B, int U, int W>

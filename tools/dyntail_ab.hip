@@ -8,7 +8,8 @@
 // launch, every result checked:
 //   prod s0 / prod s20   the production kern::reduce_stream (256 x 8, window 4, polled fan-in):
 //                        equal rounds / the anchored XCD-weighted split (19 extra rounds at 1e9)
-//   dyn K                this kernel, the last K rounds of tiles dynamic (partials folded on the
+//   dyn K                this kernel, the last K rounds of tiles dynamic (s20+dyn K: after the
+//                        weighted split's static rounds; partials folded on the
 //                        host after timing: no fan-in in the timed launch, which favours it by the
 //                        production fan-in's ~1 us)
 //   build: make dyntail_ab      run: build/bin/dyntail_ab [--n=1e9] [--rounds=5] [--iters=20]
@@ -55,7 +56,7 @@ __device__ __forceinline__ unsigned claim_read(unsigned c) {
 }
 template <int BLOCK, int UNROLL, int WIN>
 __global__ __launch_bounds__(BLOCK) void dyn_tail(const double* __restrict__ x, uint64_t nvec, uint32_t static_rounds,
-                                                  unsigned* ctr, double* partials) {
+                                                  uint32_t extra, unsigned* ctr, double* partials) {
   using V = kern::Vec16<double>::type;
   __shared__ double lds[BLOCK / 64];
   __shared__ unsigned claim[2];
@@ -69,7 +70,8 @@ __global__ __launch_bounds__(BLOCK) void dyn_tail(const double* __restrict__ x, 
   const uint32_t ntiles = static_cast<uint32_t>(nvec / kTile), grid = gridDim.x;
   const uint32_t sr0 = static_rounds * grid <= ntiles ? static_rounds : ntiles / grid;
   const uint32_t sr = sr0 > 0 ? sr0 : 1;  // >= 1 static tile per workgroup (the grid <= ntiles here)
-  const uint32_t p0 = sr * grid;          // first dynamic tile
+  const uint32_t half = grid / 2, ex = sr * grid + extra * half <= ntiles ? extra : 0u;
+  const uint32_t p0 = sr * grid + ex * half;  // first dynamic tile
   const bool wave0 = threadIdx.x < 64;
   auto claim_tile = [&](unsigned c) { return p0 + c < ntiles ? p0 + c : kDone; };
   // the first claim: made now, used when the static tiles run out (its wait is long over by then)
@@ -91,11 +93,22 @@ __global__ __launch_bounds__(BLOCK) void dyn_tail(const double* __restrict__ x, 
     }
     rp = rq;
   };
-  // static phase: tiles b, b + grid, ... (sr of them)
+  // static phase: tiles b, b + grid, ... (sr of them), then `ex` more rounds for the odd
+  // workgroups interleaved among themselves (the XCD-weighted split, by blockIdx parity: this
+  // tool launches on the null stream, where workgroup b runs on XCC b % 8)
 #pragma nounroll
   for (uint32_t k = 1; k < sr; ++k) {
     t += grid;
     step(t);
+  }
+  if ((blockIdx.x & 1u) && ex > 0) {
+    t = sr * grid + (blockIdx.x >> 1);
+    step(t);
+#pragma nounroll
+    for (uint32_t k = 1; k < ex; ++k) {
+      t += half;
+      step(t);
+    }
   }
   // the first dynamic tile (broadcast), then one claim ahead per step
   if (wave0) claim[0] = claim_tile(claim_read(c0));
@@ -169,11 +182,12 @@ int main(int argc, char** argv) {
 
   struct Var {
     std::string name;
-    int skew;   // production: extra rounds for the favoured XCC parity (-1: dyn)
+    int skew;   // production: extra rounds for the favoured XCC parity (-1: dyn, -2: skewed dyn)
     int dynk;   // dyn: rounds left dynamic
   };
   std::vector<Var> vars = {{"prod s0", 0, 0}, {"prod s20", 19, 0}};
-  for (int kk : {2, 4, 8, 16, 32}) vars.push_back({"dyn K=" + std::to_string(kk), -1, kk});
+  for (int kk : {2, 4, 8}) vars.push_back({"dyn K=" + std::to_string(kk), -1, kk});
+  for (int kk : {1, 2, 4, 8}) vars.push_back({"s20+dyn K=" + std::to_string(kk), -2, kk});
 
   auto prod_args = [&](int skew) {
     kern::Args a{};
@@ -213,8 +227,12 @@ int main(int argc, char** argv) {
         if (v.skew >= 0) {
           detail::launch_stream<SumOp, double, double, B, U, true, false, W>(prod_args(v.skew), grid, 0);
         } else {
+          // -1: equal static rounds; -2: the weighted split's common rounds (19 extra for the odd
+          // workgroups, as production at 1e9) minus the K dynamic ones
+          const uint32_t d = v.skew == -2 ? 19u : 0u;
+          const uint32_t ra = static_cast<uint32_t>((ntiles - static_cast<uint64_t>(d) * (grid / 2)) / grid);
           hipLaunchKernelGGL((dyn_tail<B, U, W>), dim3(grid), dim3(B), 0, 0, x, nvec,
-                             rounds_all > static_cast<uint32_t>(v.dynk) ? rounds_all - v.dynk : 0u, ctr, dpart);
+                             ra > static_cast<uint32_t>(v.dynk) ? ra - v.dynk : 0u, d, ctr, dpart);
         }
       };
       launch();  // warm-up

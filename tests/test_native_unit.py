@@ -47,6 +47,14 @@ def test_host_sanitizers():
         assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
 
 
+def test_experiment_tools_build():
+    # tools/window_ab.hip and tools/dyntail_ab.hip include the production kernel header directly
+    # (their A/Bs run the real kern::reduce_stream): they must keep compiling as it changes.
+    subprocess.run(["make", "-C", ROOT, "-j8", "window_ab", "dyntail_ab"], check=True, stdout=subprocess.DEVNULL)
+    for b in ("window_ab", "dyntail_ab"):
+        assert os.path.exists(os.path.join(BIN, b))
+
+
 def test_threaded_host_references_race_free():
     # SURVEY.md §5.2 race detection: the multi-threaded CPU oracles under ThreadSanitizer agree
     # with their single-threaded results, and TSan reports nothing (it exits 66 on a report).

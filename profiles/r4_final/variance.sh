@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4: run-to-run variance of the default bench on one box (3 back-to-back runs of the driver's
 # N=1 command), then the same through torch.distributed.run with one rank (the driver's launcher).
-O=gpurun_out/r4_var
+O=${O:-gpurun_out/r4_var}
 mkdir -p $O
 for i in 1 2 3; do
   timeout -k 10 300 python -u bench.py > $O/bench_$i.json 2> $O/bench_$i.err

@@ -45,7 +45,7 @@ COMMLIB     := $(BUILD)/lib/libmireduce_comm.a
 APPS := $(BUILD)/bin/reduction $(BUILD)/bin/reduce_xgmi $(BUILD)/bin/bandwidth_test
 MPI_APP := $(BUILD)/bin/reduce_mpi
 
-.PHONY: all python apps mpi clean asan tsan unit diag examples window_ab dyntail_ab
+.PHONY: all python apps mpi clean asan tsan unit diag examples window_ab dyntail_ab i32sum_ab
 all: python apps mpi unit diag examples
 
 python: $(PYEXT)
@@ -125,6 +125,15 @@ $(BUILD)/obj/tools/dyntail_ab.o: tools/dyntail_ab.hip $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 $(BUILD)/bin/dyntail_ab: $(BUILD)/obj/tools/dyntail_ab.o $(LIB)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive $(LDLIBS) -o $@
+
+# Experiment: int32 SUM with dot2 half-sums (tools/i32sum_ab.hip).
+i32sum_ab: $(BUILD)/bin/i32sum_ab
+$(BUILD)/obj/tools/i32sum_ab.o: tools/i32sum_ab.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+$(BUILD)/bin/i32sum_ab: $(BUILD)/obj/tools/i32sum_ab.o $(LIB)
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive $(LDLIBS) -o $@
 

@@ -48,10 +48,10 @@ def test_host_sanitizers():
 
 
 def test_experiment_tools_build():
-    # tools/window_ab.hip and tools/dyntail_ab.hip include the production kernel header directly
+    # tools/window_ab.hip, dyntail_ab.hip and i32sum_ab.hip include the production kernel header directly
     # (their A/Bs run the real kern::reduce_stream): they must keep compiling as it changes.
-    subprocess.run(["make", "-C", ROOT, "-j8", "window_ab", "dyntail_ab"], check=True, stdout=subprocess.DEVNULL)
-    for b in ("window_ab", "dyntail_ab"):
+    subprocess.run(["make", "-C", ROOT, "-j8", "window_ab", "dyntail_ab", "i32sum_ab"], check=True, stdout=subprocess.DEVNULL)
+    for b in ("window_ab", "dyntail_ab", "i32sum_ab"):
         assert os.path.exists(os.path.join(BIN, b))
 
 

@@ -114,11 +114,7 @@ Defaults tuned_defaults(size_t bytes, DType t, Op op) {
   // accumulation doubles the VALU work per load, collapses with it (6.06-6.22 TB/s) and streams
   // best as 256x8x2 with a window of 2 (7.15-7.27, first at every size); 16-bit MIN/MAX run the
   // window-4 plan at 7.13 and 256x8x2 window 2 at 7.25 (8 GB f16 MAX; the old 256x4x2: 7.16).
-  // Round 4: int32 SUM sums its elements' 16-bit halves with dot2 instructions (2 VALU ops per
-  // element, reduce_kernels.hpp add_halves), and with that streams best on the window-4 plan with
-  // the XCD skew: 1101.3 vs 1108.9 us per 8 GB for 256x8x2 window 2 (tools/i32sum_ab.hip,
-  // profiles/r4_i32/). SUMSQ keeps the int64 path and the window-2 plan.
-  const bool widening_int = t == DType::Int32 && op == Op::SumSq;
+  const bool widening_int = t == DType::Int32 && (op == Op::Sum || op == Op::SumSq);
   const bool half_cmp = dtype_is_half(t) && op != Op::Sum && op != Op::SumSq;
   if (dtype_size(t) == 8 && bytes > 192 * MB) return {256, 8, 1, 1, 0, 4};
   if ((widening_int || half_cmp) && bytes > 192 * MB) return {256, 8, 2, 1, 0, 2};

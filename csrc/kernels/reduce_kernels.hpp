@@ -422,21 +422,6 @@ __device__ __forceinline__ void resolve_anchor(TileSeq& q, const XcdAnchor& x, u
   if (q.n1 == 0) q.s1 = q.s2, q.n1 = q.n2, q.n2 = 0;
 }
 
-// int32 SUM into int64 (kHalves): each element x = hi * 2^16 + lo goes into two 32-bit per-slot
-// sums by two dot2 instructions — the unsigned low halves (v_dot2_u32_u16 against (1, 0)) and the
-// signed high halves (v_dot2_i32_i16 against (0, 1)) — 2 VALU ops per element instead of the
-// sign-extend + 64-bit add's 3, which is what starved the window-4 plan (tools/i32sum_ab.hip,
-// profiles/r4_i32/). Exact while a slot's halves stay below 2^31: folded into the int64
-// accumulator every kHalvesFlush tiles (4 elements per slot per tile: < 2^18 * 2^13).
-typedef unsigned short HalvesU __attribute__((ext_vector_type(2)));
-typedef short HalvesS __attribute__((ext_vector_type(2)));
-constexpr uint32_t kHalvesFlush = 8192;
-
-__device__ __forceinline__ void add_halves(uint32_t& lo, int32_t& hi, int32_t x) {
-  lo = __builtin_amdgcn_udot2(__builtin_bit_cast(HalvesU, x), HalvesU{1, 0}, lo, false);
-  hi = __builtin_amdgcn_sdot2(__builtin_bit_cast(HalvesS, x), HalvesS{0, 1}, hi, false);
-}
-
 // The window body over a TileSeq. The next tile is found incrementally with 32-bit uniform counters
 // (scalar compares and branches: gfx950's SALU has no 64-bit less-than, and a first version that
 // indexed the runs with 64-bit compares put them on the VALU in front of every tile's loads, 0.15-0.4 %
@@ -482,35 +467,7 @@ __device__ __forceinline__ uint32_t stream_window_seq(AccT (&acc)[UNROLL], const
     const uint64_t tag = static_cast<uint64_t>(fan_epoch(fan_raw)) << 32;
     __hip_atomic_store(x.word, tag | (xcc & 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  constexpr bool kHalves = std::is_same_v<OpT, SumOp> && std::is_same_v<T, int32_t> && std::is_same_v<AccT, int64_t>;
-  uint32_t lo[UNROLL];
-  int32_t hi[UNROLL];
-  uint32_t since = 0;  // tiles since the halves were last folded
-#pragma unroll
-  for (int u = 0; u < UNROLL; ++u) lo[u] = 0, hi[u] = 0;
-  auto fold = [&]() {
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      acc[u] += static_cast<int64_t>(hi[u]) * 65536 + static_cast<int64_t>(lo[u]);
-      lo[u] = 0, hi[u] = 0;
-    }
-  };
-  auto consume = [&](int u) {
-    if constexpr (kHalves) {
-#pragma unroll
-      for (int k = 0; k < N; ++k) add_halves(lo[u], hi[u], buf[u % WIN][k]);
-    } else {
-#pragma unroll
-      for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(buf[u % WIN], k)));
-    }
-  };
   auto step = [&]() {  // the next tile's loads under this one's consume: the loose window of stream_window
-    if constexpr (kHalves) {
-      if (++since == kHalvesFlush) {
-        fold();
-        since = 0;
-      }
-    }
     if (left > 1) {
       t += st;
       --left;
@@ -525,7 +482,8 @@ __device__ __forceinline__ uint32_t stream_window_seq(AccT (&acc)[UNROLL], const
     const __amdgpu_buffer_rsrc_t rq = tile_rsrc(vin + t * kTile);
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      consume(u);
+#pragma unroll
+      for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(buf[u % WIN], k)));
       const int j = u + WIN;
       buf[u % WIN] = j < UNROLL ? ld_buf_nt<V>(rp, voff, j * kStride) : ld_buf_nt<V>(rq, voff, (j - UNROLL) * kStride);
       __builtin_amdgcn_sched_barrier(0);
@@ -557,11 +515,11 @@ __device__ __forceinline__ uint32_t stream_window_seq(AccT (&acc)[UNROLL], const
   for (; n > 1; --n) step();
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {  // the last tile: no loads of a next one
-    consume(u);
+#pragma unroll
+    for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(buf[u % WIN], k)));
     const int j = u + WIN;
     if (j < UNROLL) buf[u % WIN] = ld_buf_nt<V>(rp, voff, j * kStride);
   }
-  if constexpr (kHalves) fold();
   return total;
 }
 

@@ -445,24 +445,6 @@ def test_xcd_weighted_split(monkeypatch, permille, n, op):
     assert out.item() == exp and red.check() is None
 
 
-@pytest.mark.parametrize("max_blocks", [0, 2, 4])
-def test_int32_sum_dot2_halves_exact(max_blocks):
-    # int32 SUM on the window plans sums the elements' 16-bit halves with dot2 instructions into
-    # 32-bit per-slot sums, folded into int64 every kHalvesFlush tiles (reduce_kernels.hpp
-    # add_halves). Full-range values (both halves and signs vary), exact against torch's int64 sum;
-    # max_blocks=2 / 4 give each workgroup > 8192 tiles, so the periodic fold runs mid-stream.
-    n = 300_000_017
-    g = torch.Generator(device="cpu").manual_seed(29)
-    x = torch.randint(-(1 << 31), (1 << 31) - 1, (n,), generator=g, dtype=torch.int32).to(DEV)
-    x[:1000] = -(1 << 31)  # the extreme low halves / high halves
-    x[1000:2000] = (1 << 31) - 1
-    r = Reducer(DEV, config=KernelConfig(max_blocks=max_blocks))
-    got = r(x, "sum").item()
-    assert r.last_plan["window"] == 4, r.last_plan
-    assert got == x.long().sum().item()
-    assert r.check() is None
-
-
 def test_reduce_partials_is_unskewed(monkeypatch):
     # reduce_partials has no workspace, so no fan-in epoch to anchor the weighted split with: it
     # streams equal rounds even under an explicit skew, and its partials fold to the exact sum

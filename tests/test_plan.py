@@ -63,10 +63,8 @@ def test_tuned_defaults_by_size():
     assert f32["window"] == 4 and f32["xskew"] == 19
     bf16 = C.plan(0, 4 * 10**9, 4)         # bf16 SUM 8 GB: window 4 but no skew (profiles/r4_xcd/)
     assert bf16["window"] == 4 and bf16["xskew"] == 0
-    i32 = C.plan(0, 2 * 10**9, 0)          # int32 SUM: dot2 half-sums on the window-4 plan, skewed
-    assert i32["window"] == 4 and i32["xskew"] == 19  # (profiles/r4_i32/)
-    i32sq = C.plan(0, 2 * 10**9, 0, op=3)  # int32 SUMSQ keeps the int64 path: window 2, no skew
-    assert i32sq["window"] == 2 and i32sq["xskew"] == 0
+    i32 = C.plan(0, 2 * 10**9, 0)          # int32 SUM: the window-2 plan, unmeasured: no skew
+    assert i32["window"] == 2 and i32["xskew"] == 0
 
 
 # op codes: SUM 0, MIN 1, MAX 2, SUMSQ 3, AMAX 4; dtypes: int32 0, int64 1, f32 2, f64 3, bf16 4, f16 5
@@ -75,9 +73,8 @@ def test_tuned_defaults_by_size():
     (2, 250_000_000, 0, (256, 8, 256, 4)),  # f32 SUM 1 GB
     (2, 2 * 10**9, 2, (256, 8, 256, 4)),   # f32 MAX 8 GB
     (0, 2 * 10**9, 2, (256, 8, 256, 4)),   # int32 MAX 8 GB
-    (0, 2 * 10**9, 0, (256, 8, 256, 4)),   # int32 SUM: dot2 half-sums, window 4 (profiles/r4_i32/)
-    (0, 250_000_000, 0, (256, 8, 256, 4)),  # int32 SUM 1 GB
-    (0, 2 * 10**9, 3, (256, 8, 512, 2)),   # int32 SUMSQ (int64 accumulation): 256x8x2, window 2
+    (0, 2 * 10**9, 0, (256, 8, 512, 2)),   # int32 SUM (int64 accumulation): 256x8x2, window 2
+    (0, 250_000_000, 0, (256, 8, 512, 2)),  # int32 SUM 1 GB
     (4, 4 * 10**9, 0, (256, 8, 256, 4)),   # bf16 SUM 8 GB
     (4, 5 * 10**8, 0, (256, 8, 256, 4)),   # bf16 SUM 1 GB
     (5, 4 * 10**9, 2, (256, 8, 512, 2)),   # f16 MAX 8 GB: 256x8x2, window 2

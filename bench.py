@@ -49,12 +49,85 @@ import sys
 import time
 
 LAUNCHER_ENV = "MIREDUCE_BENCH_LAUNCHER"  # set by _launch_ranks for its children: "self-spawned"
+T0_ENV = "MIREDUCE_BENCH_T0"  # the job's start (time.time()), handed to self-spawned ranks
+# The whole run's clock starts here, before torch is imported (a fresh box's first import takes
+# minutes): every phase deadline is derived from what is left of --budget.
+T0 = float(os.environ.get(T0_ENV) or time.time())
+DEFAULT_BUDGET_S = 420.0  # the driver allows 600 s per run; this leaves it a margin
+PARENT_GRACE_S = 30.0  # the self-spawning parent kills the ranks this long after the budget
 
 
 def _free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def _no_line(n: int, why: str) -> dict:
+    """The diagnostic result line of a run that produced no measurement."""
+    return {"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": n, "verified": None,
+            "higher_is_better": True, "scaling": "strong", "error": why}
+
+
+def _is_result_line(line: str) -> bool:
+    if not line.startswith("{"):
+        return False
+    try:
+        d = json.loads(line)
+    except ValueError:
+        return False
+    return isinstance(d, dict) and "metric" in d and "value" in d
+
+
+def _relay_child(child, budget_end: float, n: int) -> int:
+    """The self-spawning parent's side: relay the ranks' stdout line by line, bound the job at
+    ``budget_end`` + PARENT_GRACE_S (SIGTERM to the ranks' process group, SIGKILL 15 s later), and
+    if no result line came out, print a diagnostic one itself. Returns the job's exit status."""
+    import threading
+    seen = {"line": False}
+
+    def pump():
+        for raw in iter(child.stdout.readline, b""):
+            text = raw.decode("utf-8", "replace")
+            if _is_result_line(text.strip()):
+                seen["line"] = True
+            sys.stdout.write(text)
+            sys.stdout.flush()
+
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    killed = False
+    while True:
+        try:
+            rc = child.wait(timeout=max(0.1, budget_end + PARENT_GRACE_S - time.time()))
+            break
+        except subprocess.TimeoutExpired:
+            killed = True
+            print("[bench] the ranks exceeded the run budget: terminating them", file=sys.stderr, flush=True)
+            rc = None
+            for sig, wait_s in ((signal.SIGTERM, 15.0), (signal.SIGKILL, 15.0)):
+                try:
+                    os.killpg(child.pid, sig)
+                except (ProcessLookupError, PermissionError):
+                    pass
+                try:
+                    rc = child.wait(timeout=wait_s)
+                    break
+                except subprocess.TimeoutExpired:
+                    rc = None
+            if rc is None:
+                rc = child.wait()
+            break
+        except KeyboardInterrupt:  # forwarded by the handler; keep waiting for the child's status
+            continue
+    th.join(timeout=5.0)
+    rc = rc if rc >= 0 else 128 - rc  # killed by a signal: the shell's convention
+    if not seen["line"]:
+        why = ("the ranks exceeded the run budget and were killed" if killed else
+               f"the ranks ended (status {rc}) without printing a result line")
+        print(json.dumps(_no_line(n, why + "; no measurement")), flush=True)
+        return rc if rc != 0 else 2
+    return 2 if killed and rc == 0 else rc
 
 
 def _launch_ranks(argv: list) -> "int | None":
@@ -65,24 +138,26 @@ def _launch_ranks(argv: list) -> "int | None":
       rank 0 prints a diagnostic JSON line and every rank exits with 2 (a mis-launched job must not
       report a 1-rank number as an N-GPU one). Returns None (run the bench in this process).
     * ``WORLD_SIZE`` unset and ``--gpus N > 1``: start ``torch.distributed.run`` with N ranks of this
-      same command line as a CHILD process (never exec: a replaced process image is not allowed
-      on the GPU pool), relay nothing (the child inherits stdout / stderr), forward SIGTERM / SIGINT,
-      and return the child's exit status. Each rank records ``launcher: "self-spawned"``.
+      same command line as a CHILD process in its own process group (never exec: a replaced process
+      image is not allowed on the GPU pool), relay its stdout, forward SIGTERM / SIGINT, enforce the
+      run budget on it, print a diagnostic line if it printed none, and return its exit status.
+      Each rank records ``launcher: "self-spawned"`` and inherits the job's start time.
     * otherwise (one rank): None.
 
     Reference: reduce.c reports the rank count it ran with (NODES = commSize, mpi/reduce.c:81,95);
-    the job shape comes from the launcher (mpi/ccni_vn.sh:7)."""
+    the job shape comes from the launcher (mpi/ccni_vn.sh:7); every job ends by its wall time
+    (mpi/submit_all.sh:4)."""
     pre = argparse.ArgumentParser(add_help=False)
     pre.add_argument("--gpus", type=int, default=None)
+    pre.add_argument("--budget", type=float, default=DEFAULT_BUDGET_S)
     known, _ = pre.parse_known_args(argv)
     ws = os.environ.get("WORLD_SIZE")
     n = known.gpus if known.gpus is not None else int(ws or 1)  # no --gpus: the launcher's shape
     if ws is not None:
         if int(ws) != n:
             if os.environ.get("RANK", "0") == "0":
-                print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": n, "verified": None,
-                                  "error": f"--gpus {n} but the launcher started WORLD_SIZE={ws} ranks; "
-                                           "refusing to report a measurement for the wrong number of GPUs"}),
+                print(json.dumps(_no_line(n, f"--gpus {n} but the launcher started WORLD_SIZE={ws} ranks; "
+                                             "refusing to report a measurement for the wrong number of GPUs")),
                       flush=True)
             print(f"[bench] --gpus {n} != WORLD_SIZE {ws}: exiting with 2", file=sys.stderr, flush=True)
             return 2
@@ -91,6 +166,7 @@ def _launch_ranks(argv: list) -> "int | None":
         return None
     env = dict(os.environ)
     env[LAUNCHER_ENV] = "self-spawned"
+    env[T0_ENV] = repr(T0)
     # the native TCP bootstrap defaults to MASTER_PORT + 17: give it a port known to be free
     env.setdefault("MIREDUCE_BOOTSTRAP_PORT", str(_free_port()))
     master = _free_port()
@@ -106,7 +182,8 @@ def _launch_ranks(argv: list) -> "int | None":
         except Exception:  # noqa: BLE001
             pass
 
-    child = subprocess.Popen(cmd, env=env, preexec_fn=_die_with_parent)
+    child = subprocess.Popen(cmd, env=env, preexec_fn=_die_with_parent, stdout=subprocess.PIPE,
+                             start_new_session=True)
 
     def _forward(sig, _frame):
         try:
@@ -116,12 +193,7 @@ def _launch_ranks(argv: list) -> "int | None":
 
     for s in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
         signal.signal(s, _forward)
-    while True:
-        try:
-            rc = child.wait()
-            return rc if rc >= 0 else 128 - rc  # killed by a signal: the shell's convention
-        except KeyboardInterrupt:  # forwarded above; keep waiting for the child's status
-            continue
+    return _relay_child(child, T0 + known.budget, n)
 
 
 METRIC = "reduction bandwidth (GB/s, whole node), 1B-double sum at 1/2/4/8 MI355X"
@@ -221,7 +293,16 @@ def parse_args(argv=None):
                    help="failure-detection test: KIND[@RANK][:STEP][/SITE], KIND = exit|hang|corrupt|delay=<ms>|"
                         "mailbox, SITE = step (headline; steps count warm-up first; forces eager issue) | extras "
                         "(the after-headline candidates)")
-    p.add_argument("--pg-timeout", type=float, default=600.0, help="process-group collective timeout (s)")
+    p.add_argument("--pg-timeout", type=float, default=120.0, help="process-group collective timeout (s)")
+    p.add_argument("--budget", type=float, default=DEFAULT_BUDGET_S,
+                   help="seconds the whole run may take, from process start (self-spawned ranks: from the "
+                        "parent's start); the headline / extras / teardown deadlines are cut to what is left, "
+                        "extras that no longer fit are skipped, and a self-spawning parent kills the ranks "
+                        f"{PARENT_GRACE_S:.0f} s past it")
+    p.add_argument("--extras-file", default=None,
+                   help="where rank 0 writes the full after-headline record (reduce.c table, per-rank plans, "
+                        "decomposition, candidates, peer read); default gpurun_out/bench_extras_n<N>.json "
+                        "next to bench.py. The printed line carries only the headline and a summary")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--compare-torch", action="store_true",
                    help="after the measurement, time torch's own reduction of the same shard (reported as "
@@ -564,10 +645,12 @@ def _plan_candidates(bytes_per_gpu: float, esize: int) -> list:
     (256x8x1 with an explicit load window of 4 and the XCD-weighted split for 8-byte types above
     192 MB, profiles/r3_window/, profiles/r4_xcd/). The ranking of the top plans moves by 1-2 %
     between boxes, so for the headline's 8-byte shards the bench measures the default against the
-    same plan with equal rounds per XCD (skew 0) and with twice the skew, and against the runner-up
-    of the round-3 window sweep, instead of trusting one box's table."""
+    same plan with equal rounds per XCD (skew 0), with twice the skew, with the skew favouring the
+    EVEN XCCs (-20: a GPU whose even XCDs are the faster half) and against the runner-up of the
+    round-3 window sweep, instead of trusting one box's table. Each rank keeps its own best
+    (_tune_plan)."""
     if esize == 8 and bytes_per_gpu >= 768 * (1 << 20):
-        return [(0, 0, 0, -1, None), (0, 0, 0, -1, 0), (0, 0, 0, -1, 40), (256, 4, 2, 2, None)]
+        return [(0, 0, 0, -1, None), (0, 0, 0, -1, 0), (0, 0, 0, -1, 40), (0, 0, 0, -1, -20), (256, 4, 2, 2, None)]
     return [(0, 0, 0, -1, None)]
 
 
@@ -672,7 +755,8 @@ def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph
     written = warmup + (sg.chunk if sg is not None else K)
     if sg is not None:
         sg.reset()  # captured RCCL work must not outlive the communicator
-    return {"elapsed": elapsed, "elapsed_min": fastest, "launch": launch, "written": written}
+    return {"elapsed": elapsed, "elapsed_min": fastest, "elapsed_local": t1 - t0, "launch": launch,
+            "written": written}
 
 
 def _replay_probe(wl, ctx, args, fault, serial: bool, step, capture: bool) -> "str | None":
@@ -840,29 +924,111 @@ class _PhaseWatchdog:
             return True
 
 
-class _ExtrasWatchdog(_PhaseWatchdog):
-    """The after-headline extras' deadline: on expiry the finished headline ``line`` is printed
-    with whatever extras completed so far (``partial``, filled in place by the extras) and the
-    rest marked as timed out, and every rank exits with the headline's status."""
+def _collect_verified(obj, out: list) -> list:
+    """Every ``verified`` flag (not None) anywhere in an extras record."""
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            if k == "verified" and v is not None:
+                out.append(bool(v))
+            else:
+                _collect_verified(v, out)
+    elif isinstance(obj, list):
+        for v in obj:
+            _collect_verified(v, out)
+    return out
 
-    def __init__(self, line: "dict | None", deadline_s: float, rc: int, partial: "dict | None" = None):
-        def make():
-            if line is None:
-                return None
-            out = dict(line)
-            msg = f"extras did not finish within {deadline_s:.0f} s (headline measured and verified before them)"
-            out["extras_error"] = msg
-            for _ in range(3):  # the extras may be mid-update in the main thread: snapshot via JSON
-                try:
-                    out.update(json.loads(json.dumps(partial or {})))
-                    break
-                except (RuntimeError, ValueError):
-                    time.sleep(0.01)
-            rc_vec = dict(out.get("reduce_c_vector") or {})
-            rc_vec["error"] = msg
-            out["reduce_c_vector"] = rc_vec
-            return out
-        super().__init__("after-headline extras", deadline_s, rc, make)
+
+def _summarise(ex: dict) -> dict:
+    """The few extras numbers the printed line carries (the full record is the sidecar)."""
+    s = {}
+    pt = ex.get("plan_tuning")
+    if isinstance(pt, dict) and pt.get("plan_by_rank"):
+        s["plans"] = _plans_summary(pt["plan_by_rank"])
+    c = ex.get("candidates")
+    if isinstance(c, dict):
+        pipe = [v["gbps"] for k, v in c.items() if k.endswith("pipelined") and isinstance(v, dict) and v.get("gbps")]
+        s["pipelined_gbps"] = max(pipe) if pipe else None
+        s["rccl_serial_gbps"] = (c.get("rccl_serial") or {}).get("gbps")
+    dec = ex.get("decomposition")
+    if isinstance(dec, dict) and "error" not in dec:
+        s["local_gbps"] = dec.get("local_gbps")
+        s["efficiency_vs_local"] = dec.get("scaling_efficiency_vs_local")
+        s["exchange_us"] = dec.get("exchange_us_per_step")
+    v = ex.get("reduce_c_vector")
+    if isinstance(v, dict):
+        s["reduce_c_gibps"] = {impl: (v.get(f"reduce_{impl}") or {}).get("gibps") for impl in ("direct", "rccl")}
+        if isinstance(v.get("peer_read"), dict):
+            s["peer_node_gbps"] = v["peer_read"].get("node_gbps")
+    if "torch_gbps" in ex:
+        s["torch_gbps"] = ex["torch_gbps"]
+    if "skipped" in ex:
+        s["extras_skipped"] = ex["skipped"]
+    flags = _collect_verified(ex, [])
+    s["extras_verified"] = all(flags) if flags else None
+    return s
+
+
+def _default_extras_path(n: int) -> str:
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "gpurun_out", f"bench_extras_n{n}.json")
+
+
+class _Record:
+    """Rank 0's result. The printed line is compact and self-proving: the driver contract's keys,
+    ``verified`` / ``ranks_seen`` / ``rccl_ranks_seen`` among the first, the launcher and the
+    native source hash, and a small ``summary`` of the extras. Everything else — the long config
+    descriptions, the kernel plan, the topology, the per-rank plan tuning, the decomposition, the
+    candidates, reduce.c's whole table, the peer read — goes to a JSON sidecar (``path``), written
+    again at every update so a killed run still leaves what it measured. The sidecar holds the line
+    merged with all of it (tools/scaling.py reads either). Reference: reduce.c prints one short
+    row per measurement (mpi/reduce.c:81,95)."""
+
+    def __init__(self, line: dict, detail: dict, path: str):
+        self.line, self.detail, self.path = line, detail, path
+        self.extras: dict = {}
+        self.run = f"{int(time.time() * 1e3):x}-{os.getpid():x}"
+
+    def _snapshot(self) -> dict:
+        for _ in range(5):  # the extras may be mid-update in the main thread: snapshot via JSON
+            try:
+                return json.loads(json.dumps(self.extras))
+            except (RuntimeError, ValueError):
+                time.sleep(0.01)
+        return {}
+
+    def final(self, error: "str | None" = None) -> dict:
+        """The line to print (and the sidecar, written as a side effect). ``error``: why the
+        extras stopped early (they are then marked so in the sidecar)."""
+        ex = self._snapshot()
+        if error and isinstance(ex.get("reduce_c_vector"), dict):
+            ex["reduce_c_vector"]["error"] = error
+        summary = _summarise(ex)
+        summary["run"] = self.run
+        if error:
+            summary["extras_error"] = error
+        summary["extras_file"] = self.path
+        out = dict(self.line)
+        out["summary"] = summary
+        try:
+            os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
+            tmp = f"{self.path}.{os.getpid()}.tmp"
+            with open(tmp, "w") as f:
+                json.dump({**out, **self.detail, **ex}, f, indent=1)
+            os.replace(tmp, self.path)
+        except OSError as e:
+            summary["extras_file"] = None
+            summary["extras_file_error"] = f"{type(e).__name__}: {e}"[:160]
+        return out
+
+
+class _ExtrasWatchdog(_PhaseWatchdog):
+    """The after-headline extras' deadline: on expiry the finished headline is printed with the
+    summary of whatever extras completed so far (the record's sidecar keeps them all, the rest
+    marked as timed out), and every rank exits with the headline's status."""
+
+    def __init__(self, record: "_Record | None", deadline_s: float, rc: int):
+        msg = f"extras did not finish within {deadline_s:.0f} s (headline measured and verified before them)"
+        super().__init__("after-headline extras", deadline_s, rc,
+                         lambda: record.final(error=msg) if record is not None else None)
 
 
 def _gbps(wl, K: int, elapsed: float) -> float:
@@ -996,12 +1162,18 @@ def _exchange_wait(wl, ctx, args, fault, cap: int = 4096, allow_graph: bool = Tr
 
 
 def _tune_plan(wl, ctx, args, fault, kernel, cands) -> "tuple[KernelConfig, dict]":
-    """Streaming-kernel plan for this shard: the tuned default against the runners-up
-    (profiles/r2_plan/), each measured with the headline protocol (one lane, fused finish, serial,
-    graph replay, MAX over ranks) in two rounds, best of each (a first candidate measured while the
-    driver works on memory released just before it runs slow: profiles/r3_selfcheck/). A candidate whose fused exchange or fan-in flagged an error is
-    out for good (-1, sticky)."""
+    """Streaming-kernel plan for this rank's shard, chosen PER RANK: every candidate is measured on
+    every rank at once (between barriers), kernel-only — the step's own local launch without the
+    combine (``wl.local_step``: one lane, serial, graph replay) — in two rounds, best of each (a
+    first candidate measured while the driver works on memory released just before it runs slow:
+    profiles/r3_selfcheck/), and each rank keeps the plan that is fastest on ITS GPU. The step time
+    of the N-GPU job is the max over ranks of (local + combine), so per-rank choice
+    strictly dominates one plan for all: max_r min_p t(r, p) <= min_p max_r t(r, p). A candidate
+    whose fan-in flagged an error on any rank is out for every rank (-1, sticky; the error words
+    are agreed over ranks). Returns this rank's kernel config and the record (``chosen`` = rank 0's
+    plan, ``plan_by_rank`` = every rank's, ``gbps_by_rank`` = every rank's table)."""
     T = max(4, args.tune_steps) if args.tune_steps else _auto_tune_steps(wl.bytes_total / ctx.world_size)
+    local_bytes = wl.count * wl.x.element_size()
     res = {}
     for _round in range(2):
         for c in cands:
@@ -1011,14 +1183,27 @@ def _tune_plan(wl, ctx, args, fault, kernel, cands) -> "tuple[KernelConfig, dict
             b, u, w, win, skew = c
             wl.use_kernel(replace(kernel, block=b, unroll=u, wg_per_cu=w, window=None if win < 0 else win,
                                   xcd_skew=skew), streams=1)
-            mt = _measure(wl, wl.new_slots(2 + T), ctx, args, fault, serial=True, warmup=2, steps=T)
-            g = round(_gbps(wl, T, mt["elapsed"]), 3)
+            mt = _measure(wl, wl.new_slots(2 + T), ctx, args, fault, serial=True, warmup=2, steps=T,
+                          site="tune", step_fn=wl.local_step)
+            g = round(local_bytes * T / mt["elapsed_local"] / 1e9, 3)
             res[key] = -1.0 if wl.check() is not None else max(res.get(key, 0.0), g)
     best = max(res, key=res.get)
     b, u, w, win, skew = next(c for c in cands if _plan_key(c) == best)
     kernel = replace(kernel, block=b, unroll=u, wg_per_cu=w, window=None if win < 0 else win, xcd_skew=skew)
-    wl.use_kernel(kernel, streams=1)
-    return kernel, {"steps": T, "gbps": res, "chosen": best}
+    wl.use_kernel(kernel, streams=1)  # (collective: every rank re-binds, each with its own plan)
+    rows = [{"chosen": best, "gbps": res}]
+    if ctx.world_size > 1:
+        rows = [None] * ctx.world_size
+        torch.distributed.all_gather_object(rows, {"chosen": best, "gbps": res})
+    return kernel, {"steps": T, "measure": "kernel-only local launch per rank (GB/s of the rank's shard)",
+                    "chosen": rows[0]["chosen"], "plan_by_rank": [r["chosen"] for r in rows],
+                    "gbps_by_rank": [r["gbps"] for r in rows]}
+
+
+def _plans_summary(plan_by_rank: list) -> str:
+    """'tuned default x6; tuned default, XCD skew -20 x2' — the per-rank plans, compactly."""
+    from collections import Counter
+    return "; ".join(f"{k} x{c}" if len(plan_by_rank) > 1 else k for k, c in Counter(plan_by_rank).items())
 
 
 def _topology(ctx) -> dict:
@@ -1037,6 +1222,22 @@ def _topology(ctx) -> dict:
                            (pm.error or "every pair of GPUs")}
 
 
+HEADLINE_RESERVE_S = 40.0  # run budget kept after the headline phase (extras window, teardown)
+EXTRAS_RESERVE_S = 25.0  # run budget kept after the extras (teardown, the parent's grace)
+EXTRAS_MIN_S = 15.0  # an extras window shorter than this is skipped (agreed over ranks)
+NONROOT_GRACE_S = 10.0  # non-root ranks' headline deadline is this much later than rank 0's
+
+
+def _budget_left(args) -> float:
+    return T0 + args.budget - time.time()
+
+
+def _deadline(args, requested: float, reserve: float, floor: float = 5.0) -> float:
+    """A phase deadline: the requested one, cut so that ``reserve`` seconds of the run budget stay
+    for what follows the phase (never below ``floor``)."""
+    return max(floor, min(requested, _budget_left(args) - reserve))
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     C = native()  # fail loudly if the HIP extension is missing
@@ -1046,43 +1247,58 @@ def main(argv=None) -> int:
     else:  # CPU-rank configs (reduce.c plumbing) run on CPU ranks even on a GPU box
         device_type = "cpu" if CONFIGS[args.config].device == "cpu" else None
     fault = FaultInjector.from_flag_or_env(args.inject_fault)
+    cfg = CONFIGS[args.config]
+    if args.elements is not None:
+        cfg = replace(cfg, n_total=args.elements)
+    K, W = args.steps, args.warmup
+    metric = METRIC if cfg.name == NORTH_STAR else f"reduction bandwidth (GB/s), {cfg.name}"
+    # Before the process group exists the launcher's environment says who this rank is.
+    rank_env, world_env = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+
+    # ------------------------------------------------------------------ headline phase (deadline)
+    # Armed from before the process-group rendezvous: a rank that never joins must not leave the
+    # job without a line (rank 0 prints the diagnostic when the deadline passes).
+    stage = {"now": "init"}
+    headline_deadline = _deadline(args, args.headline_deadline, HEADLINE_RESERVE_S)
+
+    def diag(why: "str | None" = None):
+        if rank_env != 0:
+            return None
+        d = _no_line(world_env, (why or f"headline phase did not finish within {headline_deadline:.0f} s") +
+                     f" (stage: {stage['now']}); no measurement")
+        d.update(metric=metric, steps=K, warmup=W, native_source_hash=C.source_hash())
+        return d
+
+    def at_stage(name: str) -> None:
+        stage["now"] = name
+        _arm(diag("the process was terminated (signal) during the headline phase"))
+
+    # Rank 0 owns the line, so the other ranks' deadline is a little later: on a common hang rank 0
+    # reports it (stage named) rather than being torn down by a peer that gave up first.
+    watch = _PhaseWatchdog("headline phase", headline_deadline + (0.0 if rank_env == 0 else NONROOT_GRACE_S), 2,
+                           diag)
+    # fault site "init": before this rank arms anything or joins the group (a rank that exits here
+    # leaves no line of its own; one that hangs here keeps the others in the rendezvous)
+    fault.at(rank_env, fault.spec.step, "init", "process-group init")
+    at_stage("init")
     ctx = pdist.init(backend=None if args.backend == "auto" else args.backend, device_type=device_type,
                      timeout_s=args.pg_timeout)
     if args.gpus is None:
         args.gpus = ctx.world_size
     if args.gpus != ctx.world_size:  # (main() called directly; the __main__ launcher checks this first)
+        watch.finish()
         if ctx.is_root:
-            _emit({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": args.gpus, "verified": None,
-                   "error": f"--gpus {args.gpus} but WORLD_SIZE={ctx.world_size}"})
+            _emit(_no_line(args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={ctx.world_size}"))
         pdist.shutdown(ctx)
         return 2
-    cfg = CONFIGS[args.config]
-    if args.elements is not None:
-        cfg = replace(cfg, n_total=args.elements)
     if cfg.mode == "vector":
+        at_stage("vector collectives")
         rc = run_vector(args, ctx, cfg, fault)
+        watch.finish()
         pdist.shutdown(ctx)
         return rc
-    K, W = args.steps, args.warmup
     dev = ctx.device
-    metric = METRIC if cfg.name == NORTH_STAR else f"reduction bandwidth (GB/s), {cfg.name}"
-
-    # ------------------------------------------------------------------ headline phase (deadline)
-    stage = {"now": "setup"}
-
-    def diag(why: "str | None" = None):
-        if not ctx.is_root:
-            return None
-        return {"metric": metric, "value": None, "unit": "GB/s", "n_gpus": ctx.world_size, "steps": K,
-                "warmup": W, "higher_is_better": True, "scaling": "strong", "verified": None,
-                "error": (why or f"headline phase did not finish within {args.headline_deadline:.0f} s") +
-                         f" (stage: {stage['now']}); no measurement", "native_source_hash": C.source_hash()}
-
-    def at_stage(name: str) -> None:
-        stage["now"] = name
-        _arm(diag("the process was terminated (signal) during the headline phase"))
     at_stage("setup")
-    watch = _PhaseWatchdog("headline phase", args.headline_deadline, 2, diag)
 
     kernel = KernelConfig(block=args.block, unroll=args.unroll, wg_per_cu=args.wg_per_cu,
                           groups=args.groups,
@@ -1144,7 +1360,7 @@ def main(argv=None) -> int:
     gbps = _gbps(wl, K, m["elapsed"])
     ms = m["elapsed"] / K * 1e3
     topo = _topology(ctx) if dev.type == "cuda" else None  # collective at N > 1 (cached after fused)
-    line = None
+    record = None
     if ctx.is_root:
         world1 = ctx.world_size == 1
         if m_issues:
@@ -1156,11 +1372,15 @@ def main(argv=None) -> int:
                        "fused in-kernel cross-rank finish (IPC mailboxes over xGMI, csrc/include/mireduce/xrank.hpp)")
         else:
             combine = "none (--local-only)"
-        line = {
+        launcher = os.environ.get(LAUNCHER_ENV) or ("external" if "WORLD_SIZE" in os.environ else "single process")
+        line = {  # the proof fields first: the driver keeps a bounded set of keys and a stdout tail
             "metric": metric,
             "value": round(gbps, 3),
             "unit": "GB/s",
             "n_gpus": ctx.world_size,
+            "verified": verified,
+            "ranks_seen": seen,
+            "rccl_ranks_seen": seen if ctx.backend == "nccl" else None,
             "steps": K,
             "warmup": W,
             "ms_per_step": round(ms, 5),
@@ -1168,7 +1388,6 @@ def main(argv=None) -> int:
             "scaling": "strong",
             "vs_baseline": round(gbps / cfg.baseline, 3) if cfg.baseline else None,
             "dtype": "fp64" if cfg.dtype == torch.float64 else str(cfg.dtype).replace("torch.", ""),
-            "device": dev.type,
             "data": "synthetic (on-device counter-based U[0,1) fill, untimed; random-filled array)",
             "config": {
                 "model": f"{cfg.name}: {cfg.description}",
@@ -1180,6 +1399,15 @@ def main(argv=None) -> int:
                 "bytes_per_step": wl.bytes_total,
                 "op": cfg.op.upper(),
                 "collective": collective,
+                "launch": m["launch"],
+            },
+            "launcher": launcher,
+            "native_source_hash": C.source_hash(),
+        }
+        if err is not None:
+            line["device_error"] = err[:300]
+        detail = {
+            "config_detail": {
                 "collective_choice": ("auto: fused finish passed its self-check on every rank"
                                       if args.collective == "auto" and collective == "fused" else
                                       f"auto; fused unavailable: {collective_note}" if collective_note else
@@ -1190,50 +1418,46 @@ def main(argv=None) -> int:
                            ("pipelined (step i+1 local reduce || step i all-reduce)" if m_issues
                             else f"pipelined over {m_lanes} stream lanes"),
                 "streams": m_lanes,
-                "launch": m["launch"],
                 "kernel_plan": wl.reducer.last_plan if getattr(wl, "reducer", None) else getattr(wl, "plan", None),
+                "topology": topo,
             },
+            "device": dev.type,
             "per_gpu_gbps": round(gbps / ctx.world_size, 3),
             "baseline_value": cfg.baseline,
             "baseline_source": cfg.baseline_source,
-            "verified": verified,
             "native_ext": os.path.basename(native_path()),
-            "native_source_hash": C.source_hash(),
-            **_launch_record(ctx, seen),
+            "ranks_seen_backend": ctx.backend,
+            "budget_s": args.budget,
+            "headline_done_s": round(time.time() - T0, 2),
         }
-        if err is not None:
-            line["device_error"] = err
-        if not args.pipelined:
-            line["serial_gbps"] = line["value"]
-            line["serial_ms_per_step"] = line["ms_per_step"]
-            line["serial_launch"] = m["launch"]
-            line["serial_collective"] = collective
+        record = _Record(line, detail, args.extras_file or _default_extras_path(ctx.world_size))
         if plan_tuning is not None:
-            line["plan_tuning"] = plan_tuning
-        if topo is not None:
-            line["config"]["topology"] = topo
+            record.extras["plan_tuning"] = plan_tuning
     rc = 0 if verified in (None, True) else 1
     if not watch.finish():
         return 2  # (unreachable: the watchdog ended the process)
 
     # ------------------------------------------------------------------ extras (watchdog; never the headline)
-    # Order: the fused 2-lane candidate (kernels only), reduce.c's table (direct collective first: no
-    # RCCL), then the RCCL step candidates, so a hang costs the fewest extras; the watchdog prints
-    # what has completed.
-    extras = {}
-    guard = _ExtrasWatchdog(line, args.extras_deadline, rc, partial=extras)
+    # Order: the decomposition and the fused 2-lane candidate (kernels only), reduce.c's table
+    # (direct collective first: no RCCL), then the RCCL step candidates, so a hang costs the fewest
+    # extras; the watchdog prints the line with the summary of what has completed. Extras that no
+    # longer fit in the run budget are skipped (agreed over ranks).
+    extras_deadline = _deadline(args, args.extras_deadline, EXTRAS_RESERVE_S, floor=0.0)
+    do_extras = -pdist.max_over_ranks(-float(extras_deadline >= EXTRAS_MIN_S), ctx) > 0.5  # AND over ranks
+    extras = record.extras if record is not None else {}
+    guard = _ExtrasWatchdog(record, max(extras_deadline, 1.0), rc)
 
     def rearm() -> None:  # the finished headline + the extras so far, should the process be killed now
-        if line is not None:
-            out = dict(line)
-            out.update(json.loads(json.dumps(extras)))
-            out["extras_error"] = "the process was terminated (signal) during the extras; headline measured and " \
-                                  "verified before them"
-            _arm(out)
+        if record is not None:
+            _arm(record.final(error="the process was terminated (signal) during the extras; headline measured "
+                                    "and verified before them"))
     rearm()
-    run_cands = args.candidates and dev.type == "cuda" and hasattr(wl, "use_collective") and not args.pipelined
+    if not do_extras:
+        extras["skipped"] = f"run budget: {max(0.0, _budget_left(args)):.0f} s left after the headline"
+    run_cands = do_extras and args.candidates and dev.type == "cuda" and hasattr(wl, "use_collective") \
+        and not args.pipelined
     cap_failed = m["launch"].startswith("eager (graph capture failed")
-    if args.decompose and not args.pipelined and hasattr(wl, "local_step"):  # kernels only: cheap, first
+    if do_extras and args.decompose and not args.pipelined and hasattr(wl, "local_step"):  # kernels only: first
         try:
             # (after a failed capture of the headline's collective steps another capture in this process
             # can abort it: profiles/r2_full/; the decomposition then issues its steps eagerly)
@@ -1245,33 +1469,22 @@ def main(argv=None) -> int:
     if run_cands:  # the fused (kernel-only) candidate first: before the torch-heavy extras below
         extras["candidates"] = _candidates(wl, ctx, args, fault, collective == "fused", cap_failed, which="fused")
         rearm()
-    if args.vector_extras and dev.type == "cuda" and cfg.name == NORTH_STAR:
+    if do_extras and args.vector_extras and dev.type == "cuda" and cfg.name == NORTH_STAR:
         extras["reduce_c_vector"] = {}
         _vector_extras(ctx, out=extras["reduce_c_vector"], progress=rearm, canary=args.canary,
                        canary_timeout=args.canary_timeout)
         rearm()
-    if args.compare_torch and dev.type == "cuda":
+    if do_extras and args.compare_torch and dev.type == "cuda":
         extras["torch_gbps"] = round(_time_torch_reduction(wl, K, W, ctx), 3)
         rearm()
     if run_cands:  # the RCCL candidates last: a hang there costs the fewest extras
-        extras["candidates"].update(_candidates(wl, ctx, args, fault, collective == "fused", cap_failed,
-                                                which="rccl"))
-    if guard.finish() and line is not None:
-        cands = extras.get("candidates")
-        if cands is not None:
-            line["candidates"] = cands
-            pipe = [v["gbps"] for k, v in cands.items() if k.endswith("pipelined") and v.get("gbps")]
-            line["pipelined_gbps"] = max(pipe) if pipe else None
-            line["rccl_serial_gbps"] = cands.get("rccl_serial", {}).get("gbps")
-        for k in ("torch_gbps", "reduce_c_vector", "decomposition"):
-            if k in extras:
-                line[k] = extras[k]
-        _emit(line)
-    elif line is not None:  # the watchdog printed it
-        pass
+        extras.setdefault("candidates", {}).update(
+            _candidates(wl, ctx, args, fault, collective == "fused", cap_failed, which="rccl"))
+    if guard.finish() and record is not None:
+        _emit(record.final())
     # The line is out: a teardown stuck in a collective (communicator destruction) must not hold
     # the job either, so it gets a deadline of its own and exits with the headline's status.
-    teardown = _PhaseWatchdog("teardown", args.teardown_deadline, rc, lambda: None)
+    teardown = _PhaseWatchdog("teardown", _deadline(args, args.teardown_deadline, 0.0), rc, lambda: None)
     fault.at(ctx.rank, fault.spec.step, site="teardown")
     _sync(dev)
     pdist.shutdown(ctx)

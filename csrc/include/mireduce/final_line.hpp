@@ -6,8 +6,13 @@
 // lost with it. `arm_final_line` keeps the line to print in that case (updated as the run
 // progresses, e.g. with the extras finished so far); signal handlers for SIGTERM, SIGINT, SIGHUP,
 // SIGABRT, SIGSEGV, SIGBUS and SIGFPE write the armed line to fd 1 with write(2) (async-signal-
-// safe) and then re-raise with the default action. `emit_final_line` is the normal path; a
-// process-wide once-guard makes sure that whichever comes first is the only line printed.
+// safe) and then hand the signal to whatever handled it before (Python's SIGINT handler, a
+// faulthandler, ...) or, if that was the default action, re-raise it. Every arm re-installs the
+// handlers if a library replaced them since (the replacement becomes the one chained to).
+// `emit_final_line` is the normal path; a process-wide once-guard makes sure that whichever comes
+// first is the only line printed, and a handler that finds another thread mid-way through printing
+// waits (bounded, ~2 s) for it to finish before the process can die. The line goes to stdout as it
+// was at the first arm (a duplicate of fd 1 taken then), even if fd 1 is routed elsewhere later.
 #pragma once
 
 #include <string>

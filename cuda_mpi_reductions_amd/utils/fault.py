@@ -16,6 +16,9 @@ RANK defaults to 1, STEP to 0, SITE to ``step`` (also read from ``MIREDUCE_INJEC
   ``capture``: inside bench.py's replay probe of captured collective steps (STEP ignored) — a
   probe that misses its deadline on one rank must send every rank to eager issue, and the
   headline must still be measured and verified.
+  ``init``: before the rank arms its result line or joins the process group (STEP ignored) — a
+  rank that hangs there must still end the job within the headline deadline with exactly one
+  diagnostic line (rank 0's, or the self-spawning parent's when rank 0 itself dies there).
 * KIND ``mailbox``: rank RANK fails to create its fused-finish mailbox
   (:func:`parallel.xrank.open_channel`); every rank must then agree on the RCCL fallback.
 """
@@ -30,7 +33,7 @@ from typing import Optional
 __all__ = ["FaultSpec", "FaultInjector", "parse_fault_spec"]
 
 KINDS = ("none", "exit", "hang", "corrupt", "delay", "mailbox")
-SITES = ("step", "extras", "teardown", "capture")
+SITES = ("step", "extras", "teardown", "capture", "init")
 
 
 @dataclass(frozen=True)

@@ -1,4 +1,5 @@
 """Shared helpers for the CPU test suite."""
+import json
 import os
 import socket
 import subprocess
@@ -45,3 +46,23 @@ def torchrun(nproc, script_args, timeout=600, cwd=None, env=None):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(master)] + script_args
     return run(cmd, timeout=timeout, cwd=cwd, env=e)
+
+
+def bench_record(stdout: str) -> dict:
+    """bench.py's result as tests read it: the (first) JSON line on stdout, merged with the extras
+    sidecar the line names (``summary.extras_file``, same ``summary.run``): the line's keys win, and
+    the sidecar's ``config_detail`` (long descriptions, kernel plan, topology) is folded into
+    ``config`` so both can be asserted on in one place."""
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    d = json.loads(lines[0])
+    path = (d.get("summary") or {}).get("extras_file")
+    if not path or not os.path.exists(path):
+        return d
+    with open(path) as f:
+        side = json.load(f)
+    if (side.get("summary") or {}).get("run") != d["summary"].get("run"):
+        return d
+    merged = dict(side)
+    merged.update(d)
+    merged["config"] = {**(side.get("config_detail") or {}), **d.get("config", {})}
+    return merged

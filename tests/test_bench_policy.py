@@ -27,40 +27,42 @@ def test_auto_tune_steps_covers_about_30ms():
     assert b._auto_tune_steps(1e6) == 400 and b._auto_tune_steps(1e12) == 20  # clamps
 
 
-def _watchdog_child(deadline, work_s, rc):
+def _watchdog_child(deadline, work_s, rc, side):
     import subprocess
     import sys
     code = (
         "import importlib.util, os, sys, time\n"
         f"spec = importlib.util.spec_from_file_location('b', os.path.join({ROOT!r}, 'bench.py'))\n"
         "b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)\n"
-        f"g = b._ExtrasWatchdog({{'metric': 'm', 'value': 1.0}}, {deadline}, {rc})\n"
+        f"rec = b._Record({{'metric': 'm', 'value': 1.0}}, {{}}, {side!r})\n"
+        f"g = b._ExtrasWatchdog(rec, {deadline}, {rc})\n"
         f"time.sleep({work_s})\n"
         "print('finished' if g.finish() else 'late', flush=True)\n"
         "sys.exit(7)\n")
     return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
 
 
-def test_extras_watchdog_prints_headline_and_exits_on_deadline():
+def test_extras_watchdog_prints_headline_and_exits_on_deadline(tmp_path):
     import json
-    r = _watchdog_child(0.3, 30, 0)
+    r = _watchdog_child(0.3, 30, 0, str(tmp_path / "x.json"))
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert r.returncode == 0 and len(lines) == 1 and "finished" not in r.stdout, (r.stdout, r.stderr)
     d = json.loads(lines[0])
-    assert d["value"] == 1.0 and "did not finish" in d["reduce_c_vector"]["error"]
+    assert d["value"] == 1.0 and "did not finish" in d["summary"]["extras_error"]
     assert "exceeded" in r.stderr
 
 
-def test_extras_watchdog_stays_quiet_when_extras_finish():
-    r = _watchdog_child(30, 0.1, 0)
+def test_extras_watchdog_stays_quiet_when_extras_finish(tmp_path):
+    r = _watchdog_child(30, 0.1, 0, str(tmp_path / "x.json"))
     assert r.returncode == 7 and r.stdout.strip() == "finished", (r.stdout, r.stderr)
 
 
 def test_plan_candidates_only_for_the_headline_shards():
     b = _bench()
     GB = 1 << 30
-    # the tuned default (its XCD skew), equal rounds per XCD, twice the skew, the window runner-up
-    cands = [(0, 0, 0, -1, None), (0, 0, 0, -1, 0), (0, 0, 0, -1, 40), (256, 4, 2, 2, None)]
+    # the tuned default (its XCD skew), equal rounds per XCD, twice the skew, the skew favouring the
+    # even XCCs, the window runner-up
+    cands = [(0, 0, 0, -1, None), (0, 0, 0, -1, 0), (0, 0, 0, -1, 40), (0, 0, 0, -1, -20), (256, 4, 2, 2, None)]
     assert b._plan_candidates(8e9, 8) == cands  # N=1 / N=2 shards
     assert b._plan_candidates(1e9, 8) == cands  # N=8 shard
     assert b._plan_candidates(0.5 * GB, 8) == [(0, 0, 0, -1, None)]
@@ -70,27 +72,33 @@ def test_plan_candidates_only_for_the_headline_shards():
     assert b._plan_key((0, 0, 0, -1, None)) == "tuned default" and b._plan_key((0, 0, 0, -1, 0)) == "tuned default, XCD skew 0"
 
 
-def test_extras_watchdog_reports_the_extras_completed_so_far():
+def test_extras_watchdog_reports_the_extras_completed_so_far(tmp_path):
     # a hang mid-way through the extras (e.g. an RCCL collective at N>1) must still publish the rows
-    # measured before it, next to the headline
+    # measured before it: their summary in the line, all of them in the sidecar it names
     import json
+    side = tmp_path / "extras.json"
     import subprocess
     import sys
     code = (
         "import importlib.util, os, sys, time\n"
         f"spec = importlib.util.spec_from_file_location('b', os.path.join({ROOT!r}, 'bench.py'))\n"
         "b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)\n"
-        "extras = {}\n"
-        "g = b._ExtrasWatchdog({'metric': 'm', 'value': 1.0}, 0.5, 0, partial=extras)\n"
-        "extras['reduce_c_vector'] = {'rows': {'direct': ['# DATATYPE OP NODES GB/sec', 'INT MAX 8   1.000']}}\n"
+        f"rec = b._Record({{'metric': 'm', 'value': 1.0}}, {{}}, {str(side)!r})\n"
+        "g = b._ExtrasWatchdog(rec, 0.5, 0)\n"
+        "rec.extras['reduce_c_vector'] = {'rows': {'direct': ['# DATATYPE OP NODES GB/sec', 'INT MAX 8   1.000']},\n"
+        "                                 'reduce_direct': {'gibps': 3.5, 'verified': True}}\n"
         "time.sleep(30)\n")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert r.returncode == 0 and len(lines) == 1, (r.stdout, r.stderr)
     d = json.loads(lines[0])
-    v = d["reduce_c_vector"]
+    assert "did not finish" in d["summary"]["extras_error"] and d["value"] == 1.0
+    assert d["summary"]["reduce_c_gibps"]["direct"] == 3.5 and d["summary"]["extras_verified"] is True
+    assert d["summary"]["extras_file"] == str(side)
+    full = json.loads(side.read_text())
+    v = full["reduce_c_vector"]
     assert v["rows"]["direct"][1] == "INT MAX 8   1.000" and "did not finish" in v["error"]
-    assert "did not finish" in d["extras_error"] and d["value"] == 1.0
+    assert full["value"] == 1.0 and full["summary"]["run"] == d["summary"]["run"]
 
 
 class _StubWorkload:

@@ -8,7 +8,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from helpers import ROOT, free_port, run, torchrun
+from helpers import ROOT, bench_record, free_port, run, torchrun
 
 
 def _worker(rank, world, port, fn_name, q):
@@ -146,7 +146,7 @@ def test_bench_self_launches_n_ranks_without_torchrun(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
-    d = json.loads(lines[0])
+    d = bench_record(r.stdout)
     assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["ranks_seen_backend"] == "gloo"
     assert d["launcher"] == "self-spawned" and d["verified"] is True
     assert d["rccl_ranks_seen"] is None  # gloo here; on GPUs the same all-reduce runs over RCCL
@@ -165,11 +165,42 @@ def test_bench_four_cpu_ranks_probe_and_decomposition(tmp_path):
     r = torchrun(4, [os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "5", "--warmup", "1",
                      "--device", "cpu", "--elements", "400007"], cwd=tmp_path)
     assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    d = bench_record(r.stdout)
     assert d["verified"] is True and d["n_gpus"] == 4 and d["ranks_seen"] == 4 and d["launcher"] == "external"
     assert d["config"]["launch"] == "eager; replay probe ok", d["config"]["launch"]
     dec = d["decomposition"]
     assert dec["consistent"] is True and dec["local_ms_min"] <= dec["local_ms_max"]
+
+
+CONTRACT_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                 "scaling", "vs_baseline", "dtype", "data", "config")
+
+
+def test_bench_line_is_compact_and_self_proving_at_eight_ranks(tmp_path):
+    # the driver keeps a bounded set of keys and a stdout tail, so the line holds
+    # only the contract keys, the proof fields (verified, ranks_seen, rccl_ranks_seen among the first,
+    # launcher, native source hash) and a small summary; the full extras go to the sidecar it names.
+    side = tmp_path / "extras8.json"
+    r = torchrun(8, [os.path.join(ROOT, "bench.py"), "--gpus", "8", "--device", "cpu", "--steps", "3",
+                     "--warmup", "1", "--elements", "800009", "--extras-file", str(side)], cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    assert len(lines[0].encode()) < 2048, len(lines[0])
+    d = json.loads(lines[0])
+    keys = list(d)
+    extra = [k for k in keys if k not in CONTRACT_KEYS]
+    assert set(CONTRACT_KEYS) <= set(keys)
+    assert set(extra) == {"verified", "ranks_seen", "rccl_ranks_seen", "launcher", "native_source_hash", "summary"}
+    assert len(keys) <= 20 and keys.index("verified") < 6 and keys.index("rccl_ranks_seen") < 8
+    assert d["verified"] is True and d["ranks_seen"] == 8 and d["n_gpus"] == 8 and d["launcher"] == "external"
+    s = d["summary"]
+    assert s["extras_file"] == str(side) and len(json.dumps(s)) < 600
+    full = json.loads(side.read_text())  # the sidecar: the line + everything else
+    assert full["summary"]["run"] == s["run"] and full["value"] == d["value"]
+    dec = full["decomposition"]
+    assert dec["consistent"] is True and s["local_gbps"] == dec["local_gbps"]
+    assert full["config_detail"]["overlap"].startswith("serial") and full["ranks_seen_backend"] == "gloo"
 
 
 def test_bench_refuses_world_size_mismatch(tmp_path):
@@ -185,7 +216,7 @@ def test_bench_external_launcher_recorded(tmp_path):
     r = torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
                      "--device", "cpu", "--elements", "100003", "--no-decompose"], cwd=tmp_path)
     assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    d = bench_record(r.stdout)
     assert d["launcher"] == "external" and d["ranks_seen"] == 2 and "decomposition" not in d
 
 

@@ -80,7 +80,7 @@ def test_rank_killed_during_extras_keeps_the_verified_headline(tmp_path):
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["value"] > 0 and d["verified"] is True and d["n_gpus"] == 2
-    assert "terminated (signal) during the extras" in d["extras_error"]
+    assert "terminated (signal) during the extras" in d["summary"]["extras_error"]
 
 
 def test_hung_rank_hits_deadline(tmp_path):
@@ -106,6 +106,74 @@ def test_hang_in_teardown_keeps_the_line_and_status(tmp_path):
     assert d is not None and d["verified"] is True
     assert "[fault] rank 1 hang at teardown" in r.stderr and "teardown exceeded 5 s" in r.stderr
     assert time.time() - t0 < 120
+
+
+def test_rank_hung_before_init_ends_within_the_headline_deadline(tmp_path):
+    # rank 1 never joins the process group (fault site "init"). Rank 0 armed its
+    # diagnostic line and started the headline deadline BEFORE the rendezvous, so the job ends with
+    # exactly one line (no number, stage "init") long before the process-group timeout.
+    t0 = time.time()
+    r = torchrun(2, [BENCH, *SCALAR, "--inject-fault", "hang@1/init", "--headline-deadline", "15",
+                     "--pg-timeout", "120"], cwd=tmp_path, timeout=300)
+    assert r.returncode != 0
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (r.stdout, r.stderr[-2000:])
+    d = json.loads(lines[0])
+    assert d["value"] is None and "stage: init" in d["error"] and d["n_gpus"] == 2, d
+    assert "[fault] rank 1 hang at process-group init" in r.stderr
+    assert time.time() - t0 < 100
+
+
+def test_self_spawned_rank0_dead_before_arming_parent_prints_the_line(tmp_path):
+    # without a launcher, bench.py starts the ranks as a child and relays their
+    # stdout; rank 0 dies before it armed anything, so no rank prints a line: the parent does (one
+    # diagnostic line, rc != 0), within the run budget.
+    from helpers import run as run_cmd
+    import sys
+    t0 = time.time()
+    r = run_cmd([sys.executable, BENCH, *SCALAR, "--inject-fault", "exit@0/init", "--pg-timeout", "20"],
+                cwd=tmp_path, timeout=300)
+    assert r.returncode != 0
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (r.stdout, r.stderr[-2000:])
+    d = json.loads(lines[0])
+    assert d["value"] is None and "without printing a result line" in d["error"] and d["n_gpus"] == 2, d
+    assert time.time() - t0 < 120
+
+
+def test_parent_enforces_the_run_budget(capsys):
+    # the self-spawning parent's backstop: a child that outlives budget + grace is terminated (its
+    # whole process group) and, having printed nothing, gets one diagnostic line from the parent
+    import importlib.util
+    import subprocess
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    b.PARENT_GRACE_S = 0.5
+    child = subprocess.Popen(["sleep", "100"], stdout=subprocess.PIPE, start_new_session=True)
+    t0 = time.time()
+    rc = b._relay_child(child, time.time() + 1.0, 4)
+    out = capsys.readouterr().out
+    assert time.time() - t0 < 20 and rc != 0
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["value"] is None and "exceeded the run budget" in d["error"] and d["n_gpus"] == 4
+
+
+def test_child_line_is_relayed_once(capsys):
+    # a child that prints its own result line: the parent relays it and adds nothing
+    import importlib.util
+    import subprocess
+    import sys
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    code = "import json; print('noise'); print(json.dumps({'metric': 'm', 'value': 2.0, 'n_gpus': 2}))"
+    child = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, start_new_session=True)
+    rc = b._relay_child(child, time.time() + 60, 2)
+    out = capsys.readouterr().out
+    assert rc == 0 and out.count("{") == 1 and "noise" in out and '"value": 2.0' in out
 
 
 # ---------------------------------------------------------------- native apps on CPU ranks (MPICH)

@@ -10,7 +10,7 @@ import time
 import pytest
 import torch
 
-from helpers import ROOT, run, torchrun
+from helpers import ROOT, bench_record, run, torchrun
 
 pytestmark = pytest.mark.gpu
 
@@ -18,7 +18,7 @@ BENCH = os.path.join(ROOT, "bench.py")
 
 
 def _json(r):
-    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    return bench_record(r.stdout)
 
 
 # ---------------------------------------------------------------- kernel numerics at world 1
@@ -71,9 +71,8 @@ def test_bench_torchrun_one_rank_graphs_both_modes(tmp_path, collective):
     d = _json(r)
     assert d["verified"] is True and d["n_gpus"] == 1 and d["config"]["collective"] == collective
     assert d["config"]["launch"].startswith("graph"), d["config"]["launch"]
-    assert d["serial_launch"].startswith("graph"), d["serial_launch"]
     # the headline IS the per-reduction (serial, one lane) measurement
-    assert d["serial_gbps"] == d["value"] > 0 and d["serial_ms_per_step"] == d["ms_per_step"] > 0
+    assert d["value"] > 0 and d["ms_per_step"] > 0
     assert d["config"]["streams"] == 1 and d["config"]["overlap"].startswith("serial")
     combine = d["config"]["cross_rank_combine"]
     assert combine.startswith("none at world 1")  # the JSON says the combine is a no-op at world 1
@@ -217,12 +216,11 @@ def test_bench_auto_headline_is_serial_fused_extras_after(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
     assert d["verified"] is True and d["config"]["collective"] == "fused"
-    assert d["value"] == d["serial_gbps"] and d["serial_collective"] == "fused"
     assert d["config"]["streams"] == 1 and d["config"]["launch"].startswith("graph")
     c = d["candidates"]
     assert c["fused_2lane_pipelined"]["verified"] is True and c["fused_2lane_pipelined"]["gbps"] > 0
-    assert d["pipelined_gbps"] == c["fused_2lane_pipelined"]["gbps"]
-    assert d["rccl_serial_gbps"] is None and "world 1" in c["rccl_serial"]["note"]
+    assert d["summary"]["pipelined_gbps"] == c["fused_2lane_pipelined"]["gbps"]
+    assert d["summary"]["rccl_serial_gbps"] is None and "world 1" in c["rccl_serial"]["note"]
 
 
 # ---------------------------------------------------------------- direct collective from Python
@@ -336,7 +334,8 @@ def test_bench_eight_ranks_auto_on_one_gpu(tmp_path, monkeypatch):
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
     assert d["verified"] is True and d["n_gpus"] == 8
-    assert d["config"]["collective"] == "fused" and d["value"] == d["serial_gbps"] and "reduce_c_vector" in d
+    assert d["config"]["collective"] == "fused" and "reduce_c_vector" in d
+    assert d["rccl_ranks_seen"] is None and d["ranks_seen"] == 8  # gloo here
     # peer_map: eight ranks, one physical GPU, nothing to map across devices
     assert d["config"]["topology"] == {"hosts": 1, "gpus": 1, "ranks_per_gpu": 8, "peer_access": "n/a (one GPU)"}
     ex = d["reduce_c_vector"]
@@ -367,8 +366,9 @@ def test_bench_extras_deadline_keeps_the_headline(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
-    d = json.loads(lines[0])
+    d = _json(r)
     assert d["verified"] is True and "did not finish" in d["reduce_c_vector"]["error"]
+    assert "did not finish" in d["summary"]["extras_error"]
 
 
 def test_bench_extras_hang_in_rccl_candidate_keeps_the_headline(tmp_path, monkeypatch):
@@ -382,7 +382,7 @@ def test_bench_extras_hang_in_rccl_candidate_keeps_the_headline(tmp_path, monkey
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
-    assert d["verified"] is True and d["value"] > 0 and "did not finish" in d["extras_error"]
+    assert d["verified"] is True and d["value"] > 0 and "did not finish" in d["summary"]["extras_error"]
     assert "hang at bench extras 0" in r.stderr
 
 
@@ -392,16 +392,19 @@ def test_bench_plan_tuning_at_the_eight_gpu_shard(tmp_path):
     r = run([sys.executable, BENCH, "--steps", "8", "--warmup", "2", "--elements", "125000000",
              "--no-vector-extras", "--tune-steps", "8"], cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    d = _json(r)
     assert d["verified"] is True
     pt = d["plan_tuning"]
-    assert set(pt["gbps"]) == {"tuned default", "tuned default, XCD skew 0", "tuned default, XCD skew 40",
-                               "256x4x2 window 2"}
-    assert pt["chosen"] == max(pt["gbps"], key=pt["gbps"].get)
+    table = pt["gbps_by_rank"][0]  # per rank: one rank here
+    assert set(table) == {"tuned default", "tuned default, XCD skew 0", "tuned default, XCD skew 40",
+                          "tuned default, XCD skew -20", "256x4x2 window 2"}
+    assert pt["chosen"] == max(table, key=table.get) == pt["plan_by_rank"][0]
+    assert d["summary"]["plans"] == pt["chosen"]
     plan = d["config"]["kernel_plan"]
     # (block, unroll, window, xskew): 119 rounds per workgroup at the 1 GB shard
     want = {"tuned default": (256, 8, 4, 2), "tuned default, XCD skew 0": (256, 8, 4, 0),
-            "tuned default, XCD skew 40": (256, 8, 4, 5), "256x4x2 window 2": (256, 4, 2, 0)}
+            "tuned default, XCD skew 40": (256, 8, 4, 5), "tuned default, XCD skew -20": (256, 8, 4, -2),
+            "256x4x2 window 2": (256, 4, 2, 0)}
     assert (plan["block"], plan["unroll"], plan["window"], plan["xskew"]) == want[pt["chosen"]]
 
 
@@ -410,7 +413,7 @@ def test_bench_maxloc_config_skips_plan_tuning(tmp_path):
     r = run([sys.executable, BENCH, "--config", "xgmi_1b_double_maxloc", "--steps", "4", "--warmup", "1",
              "--elements", "125000000", "--no-vector-extras"], cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    d = _json(r)
     assert d["verified"] is True and "plan_tuning" not in d
 
 

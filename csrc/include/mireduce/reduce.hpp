@@ -51,6 +51,10 @@ struct ReduceConfig {
   // wall-clock ticks before publishing its partial (-1: none).
   int debug_delay_wg = -1;
   uint64_t debug_delay_ticks = 0;
+  // Test hook: workgroup 0 of an XCD-weighted launch sleeps this many wall-clock ticks before it
+  // publishes the XCD anchor (0: none); past fanin_bound_ticks every other workgroup gives up on
+  // it, the launch is poisoned and Workspace::error() has bit 2 set.
+  uint64_t debug_delay_anchor_ticks = 0;
   // Diagnostic hook (tools/xcd_balance.py): workgroup b writes [3b] the wall clock after its last
   // streamed tile was consumed, [3b+1] its XCC id, [3b+2] its tile count (device pointer; null: off).
   uint64_t* debug_wg_stamps = nullptr;
@@ -95,10 +99,13 @@ class Workspace {
   unsigned* tickets() const { return tickets_; }
   uint64_t* slots() const { return slots_; }
   unsigned* fan() const { return fan_; }
-  // Sticky error of the polled fan-in (synchronous read: call after the launches completed).
-  // Non-zero: some launch's finisher reached its wait bound; that launch and every later one
-  // wrote a poisoned result (NaN, or the operator's identity for integers — for which this word,
-  // not the value, is the signal) until reset().
+  // Sticky error word of the launches on this workspace (synchronous read: call after they
+  // completed). Bit 0: some launch's polled fan-in finisher reached its wait bound. Bit 1: the
+  // XCD anchor of a weighted split (XcdAnchor) was late: some workgroup waited past the bound
+  // for workgroup 0's publish, so its tiles were not the split's (it then withholds its partial,
+  // and in two-pass mode the finalize poisons the result). Non-zero: that launch and every later
+  // one wrote a poisoned result (NaN, or the operator's identity for integers — for which this
+  // word, not the value, is the signal) until reset(). (Bit 1 is the word's value 2.)
   unsigned error() const;
   // Re-zero the tickets, fan-in slots and the sticky error (after an error or an aborted launch;
   // stream-ordered: no launch on this workspace may be running on another stream).
@@ -137,7 +144,8 @@ LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out
 
 // Synchronous form: reduce(), wait for `stream`, and return the error state of this and every
 // earlier launch on `ws` since its last reset(): 0 = out[0] is valid; bit 0 = the polled fan-in
-// reached its wait bound; bits 8.. = the fused finish's channel error (<< 8: 1 a peer's partial
+// reached its wait bound; bit 1 = an XCD anchor was late (Workspace::error()); bits 8.. = the
+// fused finish's channel error (<< 8: 1 a peer's partial
 // timed out, 2 a peer pushed a poisoned partial). Non-zero: out[0] is poisoned; reset() the
 // workspace (and XrankChannel::clear_error()) before relying on later launches.
 unsigned reduce_checked(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,

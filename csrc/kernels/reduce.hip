@@ -154,8 +154,13 @@ bool balance_leftover() {
 // 1101.1, int32 MAX 1095.9 -> 1090.4; f64 SUM 1092.6 -> 1087.5, profiles/r4_ab/), 0 for bf16 (1089.5
 // at 0, 1105+ with any) and the window-2 int32 SUM plan (1102.5 at 0, 1105.7+). bench.py re-measures
 // 0 / default / 2x on the node for the headline's shards.
-int tuned_xcd_skew(DType t, const LaunchPlan& p) {
+// The measured asymmetry is between the XCDs of a whole MI355X in SPX mode (8 XCDs, 256 CUs, workgroups
+// dealt round-robin): a partition with one XCD (CPX, 32 CUs) has no parity to balance, and one of 2-4
+// XCDs (DPX / QPX) was never measured, so the default skew is 0 there (an explicit skew still applies).
+constexpr int kSpxCus = 256;
+int tuned_xcd_skew(DType t, const LaunchPlan& p, int num_cus) {
   const size_t es = dtype_size(t);
+  if (num_cus < kSpxCus) return 0;
   return (es == 8 || es == 4) && p.window == 4 ? 20 : 0;
 }
 
@@ -337,13 +342,17 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   p.contiguous = split_contiguous();
   p.balanced = !p.contiguous && balance_leftover();
   // XCD-weighted split (window bodies, interleaved, even grids): permille of the rounds per
-  // workgroup -> extra rounds for one parity. MIREDUCE_XCD_SKEW=<permille> overrides (A/B runs).
+  // workgroup -> extra rounds for one parity. MIREDUCE_XCD_SKEW=<permille> overrides the tuned
+  // default (A/B runs).
   // Launches with a fan-in epoch only (the polled fan-in, or two-pass: its finalize ends the epoch):
   // the kernel anchors the favoured parity to the XCDs with it.
   if (p.window > 0 && !p.contiguous && !p.balanced && p.grid % 2 == 0 && (p.poll || !p.single_pass) &&
       p.grid > 1) {
-    int permille = cfg.xcd_skew == (-2147483647 - 1) ? tuned_xcd_skew(t, p) : cfg.xcd_skew;
-    if (const char* e = std::getenv("MIREDUCE_XCD_SKEW")) permille = std::atoi(e);
+    // (the env override replaces the tuned default only: a caller's explicit skew — e.g. bench.py's
+    // plan-tuning candidates — is what it says)
+    int permille = cfg.xcd_skew == (-2147483647 - 1) ? tuned_xcd_skew(t, p, num_cus) : cfg.xcd_skew;
+    if (const char* e = std::getenv("MIREDUCE_XCD_SKEW"); e && cfg.xcd_skew == (-2147483647 - 1))
+      permille = std::atoi(e);
     const uint64_t tile = static_cast<uint64_t>(p.block) * static_cast<uint64_t>(p.unroll);
     const uint64_t rounds = tile ? p.nvec / tile / static_cast<uint64_t>(p.grid) : 0;
     const int64_t d = (static_cast<int64_t>(rounds) * permille + (permille >= 0 ? 500 : -500)) / 1000;
@@ -360,6 +369,7 @@ static kern::Args make_args(const void* in, const LaunchPlan& p, DType t, const 
   a.fan_bound = cfg.fanin_bound_ticks ? cfg.fanin_bound_ticks : kern::kFanBoundTicks;
   a.delay_wg = cfg.debug_delay_wg;
   a.delay_ticks = cfg.debug_delay_ticks;
+  a.anchor_delay = cfg.debug_delay_anchor_ticks;
   a.wg_stamps = cfg.debug_wg_stamps;
   a.head_ptr = in;
   a.body = static_cast<const char*>(in) + p.head * dtype_size(t);

@@ -88,6 +88,8 @@ struct Args {
                            // tiles split evenly over ALL workgroups (no one-tile tail on a few)
   int delay_wg;            // test hook (ReduceConfig::debug_delay_wg): this workgroup sleeps
   uint64_t delay_ticks;    // delay_ticks before publishing its partial; -1 = none
+  uint64_t anchor_delay;   // test hook (ReduceConfig::debug_delay_anchor_ticks): workgroup 0 sleeps this
+                           // long before publishing the XCD anchor; 0 = none
   uint64_t* wg_stamps;     // diagnostic (ReduceConfig::debug_wg_stamps): per-workgroup end stamps
   int xskew;               // XCD-weighted split (window bodies, interleaved): |xskew| extra rounds of
                            // tiles for the workgroups on odd (xskew > 0) or even (< 0) XCCs; 0 = equal
@@ -381,6 +383,7 @@ struct XcdAnchor {
   bool publish;       // workgroup 0
   unsigned* err;      // sticky error word (Workspace fan[1]); bit 2: the anchor never arrived
   uint64_t bound;     // wait bound in wall-clock ticks
+  uint64_t delay;     // test hook: workgroup 0 sleeps this long before publishing (0: none)
   uint64_t ntiles, grid, ra, dd, b;
 };
 
@@ -398,9 +401,12 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
 }
 
 // The anchored runs 1 and 2: `w` is the anchor as loaded; re-polled (bounded) while it is an earlier
-// launch's.
-__device__ __forceinline__ void resolve_anchor(TileSeq& q, const XcdAnchor& x, unsigned fan_raw, uint64_t w) {
+// launch's. Returns true (uniform) if the anchor never arrived within the bound: this workgroup then
+// streams the parity-0 tail, which need not match the other workgroups' — the split is no longer a
+// bijection, so the caller must poison the launch's result (sticky bit 2 of fan[1] is set here).
+__device__ __forceinline__ bool resolve_anchor(TileSeq& q, const XcdAnchor& x, unsigned fan_raw, uint64_t w) {
   const uint64_t tag = static_cast<uint64_t>(fan_epoch(fan_raw)) << 32;
+  bool late = false;
   w = rfl64(w);
   if ((w & ~0xffffffffull) != tag) {
     const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
@@ -411,6 +417,7 @@ __device__ __forceinline__ void resolve_anchor(TileSeq& q, const XcdAnchor& x, u
       if (static_cast<uint64_t>(wall_clock64()) - t0 > x.bound) {  // reported, never silent
         if (threadIdx.x == 0) __hip_atomic_fetch_or(x.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         w = tag;
+        late = true;
         break;
       }
     }
@@ -420,6 +427,7 @@ __device__ __forceinline__ void resolve_anchor(TileSeq& q, const XcdAnchor& x, u
   q.s1 = rfl64(q.s1), q.st1 = rfl64(q.st1), q.s2 = rfl64(q.s2);
   q.n1 = __builtin_amdgcn_readfirstlane(q.n1), q.n2 = __builtin_amdgcn_readfirstlane(q.n2);
   if (q.n1 == 0) q.s1 = q.s2, q.n1 = q.n2, q.n2 = 0;
+  return late;
 }
 
 // The window body over a TileSeq. The next tile is found incrementally with 32-bit uniform counters
@@ -428,9 +436,10 @@ __device__ __forceinline__ void resolve_anchor(TileSeq& q, const XcdAnchor& x, u
 // slower than the single-run loop, profiles/r4_ab/). With an anchor, runs 1 and 2 are resolved when
 // run 0 ends; the loop is split where the anchor's load issues (no load under a branch in the loop:
 // hipcc's wait counts would turn conservative for every tile).
+// `anchor_late` is set (uniform) when the anchor wait reached its bound (resolve_anchor).
 template <class OpT, class T, class AccT, class V, int N, int BLOCK, int UNROLL, int WIN>
 __device__ __forceinline__ uint32_t stream_window_seq(AccT (&acc)[UNROLL], const V* __restrict__ vin, TileSeq q,
-                                                      const XcdAnchor& x, unsigned fan_raw) {
+                                                      const XcdAnchor& x, unsigned fan_raw, bool& anchor_late) {
   static_assert(UNROLL % WIN == 0, "the window must divide the unroll");
   constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
   constexpr uint32_t kStride = BLOCK * 16;
@@ -462,6 +471,10 @@ __device__ __forceinline__ uint32_t stream_window_seq(AccT (&acc)[UNROLL], const
   // Workgroup 0 publishes its XCC's parity for this launch, after the first loads: the tag's wait
   // (the fan-in epoch, loaded at the kernel's start) is then no later than the first consume's.
   if (anchored && x.publish && threadIdx.x == 0) {
+    if (x.delay) {  // test hook: a late anchor
+      const uint64_t d0 = static_cast<uint64_t>(wall_clock64());
+      while (static_cast<uint64_t>(wall_clock64()) - d0 < x.delay) __builtin_amdgcn_s_sleep(127);
+    }
     unsigned xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     const uint64_t tag = static_cast<uint64_t>(fan_epoch(fan_raw)) << 32;
@@ -502,11 +515,11 @@ __device__ __forceinline__ uint32_t stream_window_seq(AccT (&acc)[UNROLL], const
       step();
 #pragma nounroll
       for (--n; n > 1; --n) step();
-      resolve_anchor(q, x, fan_raw, w);
+      anchor_late = resolve_anchor(q, x, fan_raw, w);
     } else {
 #pragma nounroll
       for (; n > 1; --n) step();
-      resolve_anchor(q, x, fan_raw, __hip_atomic_load(x.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      anchor_late = resolve_anchor(q, x, fan_raw, __hip_atomic_load(x.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     }
     n += q.n1 + q.n2;
     total += q.n1 + q.n2;
@@ -581,6 +594,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     }
   }
   uint32_t streamed = 0;  // full tiles of the window body (diagnostic stamps)
+  bool anchor_late = false;  // the XCD anchor missed its bound: this workgroup's tiles may overlap others
   if constexpr (PIPE) {
     if (t0 < t1) {
       V cur[UNROLL];
@@ -611,6 +625,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       x.publish = blockIdx.x == 0;
       x.err = a.fan + 1;
       x.bound = a.fan_bound;
+      x.delay = a.anchor_delay;
       x.ntiles = ntiles, x.grid = grid, x.ra = a.x_ra, x.dd = a.x_dd, x.b = blockIdx.x;
     } else {  // unskewed, or skewed by blockIdx parity (no fan-in epoch to tag an anchor with)
       q = weighted_tiles(ntiles, grid, a.xskew != 0 && (grid & 1u) == 0, a.xskew > 0 ? 1u : 0u, a.x_ra, a.x_dd,
@@ -618,7 +633,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     }
     // fan_raw (the launch's fan-in epoch, the anchor's tag) passed as is: a copy into the struct
     // would be a VGPR move that waits for its load before the first tile's loads issue
-    streamed = stream_window_seq<OpT, T, AccT, V, N, BLOCK, UNROLL, WIN>(acc, vin, q, x, fan_raw);
+    streamed = stream_window_seq<OpT, T, AccT, V, N, BLOCK, UNROLL, WIN>(acc, vin, q, x, fan_raw, anchor_late);
   } else if constexpr (WIN < 0) {  // strict window (experiments only: tools/window_ab.hip)
     stream_window<OpT, T, AccT, V, N, BLOCK, UNROLL, -WIN, true>(acc, vin, t0, t1, step);
   } else {
@@ -710,7 +725,8 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   AccT v = block_reduce<OpT, AccT, BLOCK>(acc[0], lds);
   AccT* partials = static_cast<AccT*>(a.partials);
   if (a.groups == 0) {  // two-pass mode: the finalize kernel (kernel boundary) reads these
-    if (threadIdx.x == 0) partials[blockIdx.x] = v;
+    // (a late anchor: the finalize sees fan[1] bit 2 after the kernel boundary and poisons the result)
+    if (threadIdx.x == 0) partials[blockIdx.x] = anchor_late ? poisoned<OpT, AccT>() : v;
     return;
   }
 
@@ -736,6 +752,11 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   if (a.slots) {
     const unsigned fan_e = fan_epoch(fan_raw);
     const uint64_t tag = static_cast<uint64_t>(fan_e) << 32;
+    // A workgroup whose XCD anchor was late (its tiles may double-count or skip others') does not
+    // publish: the finisher then reaches its bound and poisons the launch — never a plausible sum of
+    // the wrong tiles. (Publishing a flag instead would cost the finisher a load round trip after
+    // its poll on every launch, to order it after the slot stores.)
+    if (anchor_late && blockIdx.x != gridDim.x - 1) return;
     if (threadIdx.x == 0) {
       if (static_cast<int>(blockIdx.x) == a.delay_wg) {  // test hook: a slow workgroup
         const uint64_t d0 = static_cast<uint64_t>(wall_clock64());
@@ -812,7 +833,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       }
     }
     // Any lane past the bound (or an earlier launch's sticky error) poisons this launch's result.
-    const bool bad = __syncthreads_or(late) || fan_err != 0;
+    const bool bad = __syncthreads_or(late) || fan_err != 0 || anchor_late;
     t = block_reduce<OpT, AccT, BLOCK>(t, lds);
     if (fan_e == 0xffffffffu) {  // the epoch wraps after this launch: invalidate every slot first
       __syncthreads();
@@ -932,7 +953,9 @@ __global__ __launch_bounds__(256) void finalize(const AccT* __restrict__ partial
   AccT s = OpT::template identity<AccT>();
   for (uint64_t i = threadIdx.x; i < count; i += 256) s = OpT::apply(s, partials[i]);
   s = block_reduce<OpT, AccT, 256>(s, lds);
-  if (threadIdx.x == 0) *out = s;
+  // a first-level workgroup's XCD anchor was late (sticky bit 2): its tiles were not the split's
+  const bool anchor_err = fan && (__hip_atomic_load(fan + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2u);
+  if (threadIdx.x == 0) *out = anchor_err ? poisoned<OpT, AccT>() : s;
   if (fan) {
     const unsigned e = fan_epoch(__hip_atomic_load(fan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if (e == 0xffffffffu) {  // the epoch wraps after this launch: invalidate every tag first

@@ -281,7 +281,8 @@ PYBIND11_MODULE(_C, m) {
       [](Workspace& ws, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out,
          uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks, int groups,
          int policy, bool single_pass, int pipeline, uint64_t fanin_bound_ticks, int debug_delay_wg,
-         uint64_t debug_delay_ticks, int window, uintptr_t xrank, uintptr_t wg_stamps, int xcd_skew) {
+         uint64_t debug_delay_ticks, int window, uintptr_t xrank, uintptr_t wg_stamps, int xcd_skew,
+         uint64_t debug_delay_anchor_ticks) {
         ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline, window,
                                     xcd_skew);
         cfg.xrank = as_ptr<const void>(xrank);
@@ -289,6 +290,7 @@ PYBIND11_MODULE(_C, m) {
         cfg.fanin_bound_ticks = fanin_bound_ticks;
         cfg.debug_delay_wg = debug_delay_wg;
         cfg.debug_delay_ticks = debug_delay_ticks;
+        cfg.debug_delay_anchor_ticks = debug_delay_anchor_ticks;
         const LaunchPlan p = reduce(as_ptr<const void>(in), n, static_cast<DType>(dtype),
                                     static_cast<Op>(op), static_cast<DType>(acc),
                                     as_ptr<void>(out), ws, as_stream(stream), cfg);
@@ -300,7 +302,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("groups") = 0, py::arg("policy") = -1, py::arg("single_pass") = true,
       py::arg("pipeline") = -1, py::arg("fanin_bound_ticks") = 0, py::arg("debug_delay_wg") = -1,
       py::arg("debug_delay_ticks") = 0, py::arg("window") = -1, py::arg("xrank") = 0, py::arg("wg_stamps") = 0,
-      py::arg("xcd_skew") = kSkewAuto);
+      py::arg("xcd_skew") = kSkewAuto, py::arg("debug_delay_anchor_ticks") = 0);
 
   m.def(
       "plan",

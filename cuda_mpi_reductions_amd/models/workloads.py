@@ -341,15 +341,17 @@ class ScalarReduction:
             return None
         dev = self.ctx.device
         torch.cuda.synchronize(dev)
-        fan = sum(int(red.ws.error() != 0) for _, red, _, _ in self.lanes)
+        fan_words = [int(red.ws.error()) for _, red, _, _ in self.lanes]
+        fan = sum(int(w != 0) for w in fan_words)
+        anchor = sum(int(w & 2 != 0) for w in fan_words)
         words = [int(ch.error()) for ch in self.channels]
         late = sum(int(w & 1 != 0) for w in words)  # a peer's partial missed the timeout
         pois = sum(int(w & 2 != 0) for w in words)  # a peer pushed a poisoned partial
         if self.ctx.world_size > 1:
-            t = torch.tensor([fan, late, pois], dtype=torch.int64,
+            t = torch.tensor([fan, late, pois, anchor], dtype=torch.int64,
                              device=dev if self.ctx.backend == "nccl" else "cpu")
             torch.distributed.all_reduce(t)
-            fan, late, pois = (int(v) for v in t.tolist())
+            fan, late, pois, anchor = (int(v) for v in t.tolist())
         if fan:
             for _, red, _, _ in self.lanes:
                 red.ws.reset(_current_stream_handle(dev))
@@ -357,6 +359,9 @@ class ScalarReduction:
         msgs = []
         if fan:
             msgs.append(f"polled fan-in: {fan} workspace(s) reached the wait bound (results poisoned; reset)")
+        if anchor:
+            msgs.append(f"XCD-weighted split: {anchor} workspace(s) saw a late XCD anchor (tiles not the split's; "
+                        "results poisoned)")
         if late:
             msgs.append(f"fused cross-rank finish: {late} channel(s) timed out waiting for a peer")
         if pois:

@@ -49,6 +49,19 @@ XCD_SKEW_AUTO = -(2 ** 31)  # ReduceConfig::xcd_skew's "tuned default"
 FUSED_OPS = ("sumsq", "amax")
 
 
+def fan_error_message(word: int) -> str:
+    """What a non-zero Workspace::error() word means (csrc/include/mireduce/reduce.hpp)."""
+    msgs = []
+    if word & 1:
+        msgs.append("polled fan-in: a launch reached its wait bound")
+    if word & 2:
+        msgs.append("XCD-weighted split: a workgroup waited past the bound for the XCD anchor (its tiles were "
+                    "not the split's)")
+    if word & ~3:
+        msgs.append(f"fan-in error word {word:#x}")
+    return "; ".join(msgs) + " (results poisoned since; workspace reset)"
+
+
 def dtype_code(dt: torch.dtype) -> int:
     try:
         return DTYPE_CODES[dt]
@@ -142,11 +155,12 @@ class Reducer:
         which only this error word tells the result is bad. Synchronises the device; after an error
         the workspace is reset, so the next launch is good."""
         torch.cuda.synchronize(self.device)
-        if self.ws.error() == 0:
+        word = self.ws.error()
+        if word == 0:
             return None
         self.ws.reset(_stream_handle(self.device, stream))
         torch.cuda.synchronize(self.device)
-        return "polled fan-in: a launch reached its wait bound (results poisoned since; workspace reset)"
+        return fan_error_message(word)
 
     def __call__(
         self,

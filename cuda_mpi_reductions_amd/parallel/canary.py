@@ -5,8 +5,8 @@ reduction kernel. Every rank agrees on peer access before mapping (:mod:`.topolo
 are bounded and results are self-checked — but a fault of the mapping itself (a GPU memory-access
 fault) would abort the process, and with it the measurement it was meant to serve. So before a
 benchmark process touches a peer's memory, :func:`fused_canary` has one helper process per rank
-run the same exchange end to end: a private gloo group over the job's rendezvous store (a fresh
-key prefix), a channel, three fused launches of a 1-element-per-rank-distinguishable array, and a
+run the same exchange end to end: a private gloo group over a TCPStore that rank 0 serves for the
+canary on a free port, a channel, three fused launches of a 1-element-per-rank-distinguishable array, and a
 check of every result, the error words and a final barrier (nobody unmaps while a peer still
 polls). Each rank waits for its helper (bounded), and the verdicts are agreed over the real
 process group: any failure — a crash, a timeout, a wrong value — makes every rank decline the
@@ -141,20 +141,32 @@ def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int 
         idx = ctx.device.index if ctx.device.index is not None else 0
         if peer_map(idx).ranks_per_gpu > 1:
             return None
-    token = [secrets.token_hex(8) if ctx.rank == 0 else None]
-    dist.broadcast_object_list(token, src=0)
+    # The helpers' rendezvous: a fresh TCPStore that rank 0 serves on a free port for the duration
+    # of this call (not the job's own store, which need not be a TCPStore on MASTER_PORT — file or
+    # custom-port rendezvous — and would then cost every helper its full timeout).
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    server, where = None, [None]
+    if ctx.rank == 0:
+        try:
+            server = dist.TCPStore(host, 0, is_master=True, wait_for_workers=False,
+                                   timeout=datetime.timedelta(seconds=max(10.0, timeout_s)))
+            where = [(host, int(server.port), secrets.token_hex(8))]
+        except Exception as e:  # noqa: BLE001 - every rank then declines together
+            where = [("", f"rank 0 could not serve the canary's store: {type(e).__name__}: {e}"[:200], "")]
+    dist.broadcast_object_list(where, src=0)
+    addr, port, token = where[0]
     env = dict(os.environ)
     env.update({_ENV + "RANK": str(ctx.rank), _ENV + "WORLD": str(ctx.world_size),
-                _ENV + "ADDR": os.environ.get("MASTER_ADDR", "127.0.0.1"),
-                _ENV + "PORT": os.environ.get("MASTER_PORT", ""), _ENV + "PREFIX": f"mireduce_canary/{token[0]}/",
+                _ENV + "ADDR": addr, _ENV + "PORT": str(port) if addr else "",
+                _ENV + "PREFIX": f"mireduce_canary/{token}/",
                 _ENV + "DEVICE": str(ctx.device.index if ctx.device.index is not None else 0),
                 _ENV + "TIMEOUT": str(max(10.0, timeout_s - 10.0)), _ENV + "ELEMENTS": str(elements),
                 _ENV + "KIND": kind})
     if dry:
         env[_ENV + "DRY"] = "1"
     mine = None
-    if not env[_ENV + "PORT"]:
-        mine = "no rendezvous store address (MASTER_PORT unset)"
+    if not addr:
+        mine = str(port)
     else:
         try:
             p = subprocess.Popen([sys.executable, "-m", "cuda_mpi_reductions_amd.parallel.canary"], env=env,
@@ -175,7 +187,8 @@ def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int 
         except OSError as e:
             mine = f"could not start the helper: {e}"[:300]
     verdicts = [None] * ctx.world_size
-    dist.all_gather_object(verdicts, mine)
+    dist.all_gather_object(verdicts, mine)  # (every helper has ended: rank 0's store may go)
+    del server
     # the root causes first: helpers that crashed or hung, then the ones that only lost a peer
     first = [f"rank {r}: {m}" for r, m in enumerate(verdicts) if m and ("crashed" in m or "did not finish" in m)]
     rest = [f"rank {r}: {m}" for r, m in enumerate(verdicts) if m and not ("crashed" in m or "did not finish" in m)]

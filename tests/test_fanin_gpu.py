@@ -188,3 +188,40 @@ def test_fanin_epochs_do_not_leak_between_grids():
     exp = torch.tensor([float(big.numel()) if i % 2 == 0 else float(small.numel()) for i in range(40)],
                        dtype=torch.float64, device=dev)
     assert torch.equal(outs, exp) and red.check() is None
+
+
+@pytest.mark.parametrize("single_pass", [True, False], ids=["polled", "two_pass"])
+@pytest.mark.parametrize("dt", [torch.float64, torch.int64])
+def test_late_xcd_anchor_poisons_and_reports(dt, single_pass):
+    # a workgroup that gives up waiting for the XCD anchor streams the parity-0
+    # tail, which need not match its peers' — the split is no longer a bijection. The launch must
+    # then be poisoned (NaN / the identity) and flagged (error bit 2, its own message), in both the
+    # polled single-pass path and the two-pass path, and the launch after the reset is exact again.
+    from cuda_mpi_reductions_amd._native import native
+    from cuda_mpi_reductions_amd.ops import Reducer, default_acc_dtype
+    C = native()
+    dev = torch.device("cuda", 0)
+    n = 26_000_003  # 208 MB of 8-byte elements: the window-4 plan with the anchored XCD skew
+    g = torch.Generator(device="cpu").manual_seed(23)
+    if dt.is_floating_point:
+        x = torch.rand(n, generator=g, dtype=dt).to(dev)
+    else:
+        x = torch.randint(1, 1 << 30, (n,), generator=g, dtype=dt).to(dev)
+    exp = x.sum().item()
+    red = Reducer(dev)
+    out = torch.zeros(1, dtype=default_acc_dtype(dt, "sum"), device=dev)
+    plan = _launch(C, red, x, out, single_pass=single_pass, fanin_bound_ticks=1 * TICKS_PER_MS,
+                   debug_delay_anchor_ticks=20 * TICKS_PER_MS)
+    assert plan["xskew"] != 0 and plan["window"] == 4, plan
+    torch.cuda.synchronize()
+    word = red.ws.error()
+    assert word & 2, word
+    got = out.item()
+    assert (math.isnan(got) if dt.is_floating_point else got == 0), got  # never a plausible wrong sum
+    msg = red.check()
+    assert msg is not None and "XCD anchor" in msg, msg
+    _launch(C, red, x, out, single_pass=single_pass)
+    torch.cuda.synchronize()
+    assert red.check() is None
+    got = out.item()
+    assert (abs(got - exp) <= 1e-9 * abs(exp) if dt.is_floating_point else got == exp), (got, exp)

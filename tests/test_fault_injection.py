@@ -216,3 +216,52 @@ def test_replay_probe_miss_on_one_rank_goes_eager_and_still_measures(tmp_path):
     launch = d["config"]["launch"]
     assert launch.startswith("eager (replay probe failed: ") and "rank 1: 3 steps took" in launch, launch
     assert "[fault] rank 1 delay at replay probe" in r.stderr
+
+
+def _final_line_child(code: str):
+    import subprocess
+    import sys
+    pre = (f"import os, sys, signal, time\nsys.path.insert(0, {ROOT!r})\n"
+           "from cuda_mpi_reductions_amd._native import native\nC = native()\n")
+    return subprocess.run([sys.executable, "-c", pre + code], capture_output=True, text=True, timeout=60)
+
+
+def test_final_line_chains_to_python_sigint_handler():
+    # the once-guard prints the armed line and then hands SIGINT to the handler that was
+    # there before (Python's: KeyboardInterrupt), instead of killing the process with SIG_DFL
+    r = _final_line_child(
+        "C.arm_final_line('{\"value\": 1}')\n"
+        "try:\n"
+        "    os.kill(os.getpid(), signal.SIGINT)\n"
+        "    time.sleep(5)\n"
+        "except KeyboardInterrupt:\n"
+        "    print('KI', flush=True)\n"
+        "print('emitted-again' if C.emit_final_line('{\"value\": 2}') else 'once', flush=True)\n")
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.splitlines() == ['{"value": 1}', "KI", "once"], r.stdout
+
+
+def test_final_line_reaches_stdout_while_fd1_is_redirected():
+    # fd 1 routed to stderr for a while (dist.stdout_to_stderr during the rendezvous): the line armed
+    # before goes to the real stdout when the process is terminated then
+    r = _final_line_child(
+        "C.arm_final_line('{\"value\": 3}')\n"
+        "os.dup2(2, 1)\n"
+        "os.kill(os.getpid(), signal.SIGTERM)\n"
+        "time.sleep(5)\n")
+    assert r.returncode == -15
+    assert r.stdout.strip() == '{"value": 3}' and '{"value": 3}' not in r.stderr, (r.stdout, r.stderr)
+
+
+def test_final_line_reinstalls_over_a_later_handler():
+    # a library that installs its own SIGTERM handler after the first arm: the next arm puts the guard
+    # back on top and chains to that handler
+    r = _final_line_child(
+        "C.arm_final_line('{\"value\": 4}')\n"
+        "signal.signal(signal.SIGTERM, lambda s, f: print('lib-handler', flush=True))\n"
+        "C.arm_final_line('{\"value\": 5}')\n"
+        "os.kill(os.getpid(), signal.SIGTERM)\n"
+        "time.sleep(0.5)\n"
+        "print('alive', flush=True)\n")
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.splitlines() == ['{"value": 5}', "lib-handler", "alive"], r.stdout

@@ -164,3 +164,25 @@ def test_single_hip_runtime_in_process():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT, timeout=300)
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith("1 "), r.stdout
+
+
+def test_default_xcd_skew_needs_a_whole_spx_device():
+    # the default skew balances the 8 round-robin XCDs of a whole MI355X (SPX, 256 CUs);
+    # a one-XCD partition (CPX, 32 CUs) or an unmeasured 2-4 XCD one gets none by default, while an
+    # explicit skew still applies there
+    C = native()
+    assert C.plan(0, 10**9, F64, num_cus=256)["xskew"] == 19
+    for cus in (32, 64, 128):
+        p = C.plan(0, 10**9, F64, num_cus=cus)
+        assert p["window"] == 4 and p["xskew"] == 0, (cus, p)
+        assert C.plan(0, 10**9, F64, num_cus=cus, xcd_skew=20)["xskew"] > 0
+
+
+def test_env_skew_overrides_only_the_default(monkeypatch):
+    # MIREDUCE_XCD_SKEW replaces the tuned default, never a caller's explicit skew (bench.py's
+    # plan-tuning candidates must run what their labels say)
+    C = native()
+    monkeypatch.setenv("MIREDUCE_XCD_SKEW", "40")
+    assert C.plan(0, 10**9, F64)["xskew"] == 38
+    assert C.plan(0, 10**9, F64, xcd_skew=0)["xskew"] == 0
+    assert C.plan(0, 10**9, F64, xcd_skew=-20)["xskew"] == -19

@@ -145,3 +145,35 @@ def test_bench_reduce_c_rows_through_getavgs_match_the_reference_shape(tmp_path)
             if os.path.exists(ref_path):  # the reference's own file has the same shape
                 ref = open(ref_path).read().split("\n")
                 assert ref[0] == "" and all(line_rx.match(ln) for ln in ref[1:] if ln)
+
+
+def test_compact_lines_merge_their_sidecars(tmp_path):
+    # round 5: the printed line carries a summary and names its sidecar (the full extras record);
+    # the tool merges it (found by name next to the input when the recorded path is elsewhere), and
+    # a line passed together with its own sidecar counts once
+    side_dir = tmp_path / "out"
+    side_dir.mkdir()
+    lines = []
+    for n, run in ((1, "r1"), (8, "r8")):
+        ln = _line(n, 7300.0 * n * (0.95 if n > 1 else 1), 8.0 / (7.3 * n))
+        ln["summary"] = {"run": run, "extras_file": f"/elsewhere/bench_extras_n{n}.json"}
+        full = dict(ln)
+        full["decomposition"] = {"local_ms_per_step": 0.14 if n == 8 else 1.09, "exchange_us_per_step": 4.0,
+                                 "skew_us_per_step": 1.0, "scaling_efficiency_vs_local": 0.97}
+        (side_dir / f"bench_extras_n{n}.json").write_text(json.dumps(full))
+        lines.append(json.dumps(ln))
+    src = side_dir / "lines.jsonl"
+    src.write_text("\n".join(lines) + "\n")
+    rs = [scaling.with_sidecar(r, str(side_dir)) for r in scaling.parse_text(src.read_text())]
+    assert all("decomposition" in r for r in rs)
+    stale = dict(json.loads(lines[0]))
+    stale["summary"] = {"run": "other", "extras_file": str(side_dir / "bench_extras_n1.json")}
+    assert "decomposition" not in scaling.with_sidecar(stale)  # a different run's sidecar is not merged
+    out = tmp_path / "res"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling.py"), str(src),
+                        str(side_dir / "bench_extras_n8.json"), "--out", str(out)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    row8 = [ln for ln in (out / "scaling.md").read_text().splitlines() if "| 8 |" in ln]
+    cells = [c.strip() for c in row8[0].strip("|").split("|")] if len(row8) == 1 else []
+    assert cells[8] == "1" and cells[9] == "0.1400", row8  # one run (line + sidecar), local ms merged

@@ -31,6 +31,10 @@ poll, the most waiting ~ skew + xGMI latency). So a loss of efficiency at N=8
 splits into the per-GPU rate at the smaller shard (local ms vs N=1), the exchange and the skew.
 
     python tools/scaling.py SCALE_r01.json bench_*.json --out results/scaling
+
+Round 5+ lines are compact: each names its extras sidecar (``summary.extras_file``, bench.py's
+``--extras-file``), which is merged in when found (as named or next to the input file); a
+sidecar may also be passed directly (it holds the line too). A line and its sidecar count once.
 """
 from __future__ import annotations
 
@@ -71,6 +75,44 @@ def parse_text(text: str):
                 out.extend(_walk(json.loads(line)))
             except ValueError:
                 continue
+    return out
+
+
+def with_sidecar(r: dict, base_dir: "str | None" = None) -> dict:
+    """A bench.py line (round 5+) carries only the headline and a summary; the full extras record
+    (decomposition, reduce.c table, per-rank plans, ...) is the sidecar named in
+    ``summary.extras_file``. Merge it in when it exists (as named, or by file name next to
+    ``base_dir``) and belongs to the same run (``summary.run``); the line's keys win."""
+    s = r.get("summary")
+    if not isinstance(s, dict) or not s.get("extras_file"):
+        return r
+    for path in (s["extras_file"], os.path.join(base_dir or ".", os.path.basename(s["extras_file"]))):
+        try:
+            with open(path) as f:
+                side = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if isinstance(side, dict) and (side.get("summary") or {}).get("run") == s.get("run"):
+            merged = dict(side)
+            merged.update(r)
+            return merged
+    return r
+
+
+def dedupe(results):
+    """One result per bench run: a line and its sidecar (or the same line in two files) share
+    ``summary.run``; the record with more keys (the merged one) is kept. Results without a run id
+    (older rounds) are all kept."""
+    out, seen = [], {}
+    for r in results:
+        run = (r.get("summary") or {}).get("run") if isinstance(r.get("summary"), dict) else None
+        if run is None:
+            out.append(r)
+        elif run not in seen:
+            seen[run] = len(out)
+            out.append(r)
+        elif len(r) > len(out[seen[run]]):
+            out[seen[run]] = r
     return out
 
 
@@ -220,9 +262,10 @@ def main(argv=None):
     if a.inputs:
         for p in a.inputs:
             with open(p) as f:
-                results.extend(parse_text(f.read()))
+                results.extend(with_sidecar(r, os.path.dirname(os.path.abspath(p))) for r in parse_text(f.read()))
     else:
-        results.extend(parse_text(sys.stdin.read()))
+        results.extend(with_sidecar(r) for r in parse_text(sys.stdin.read()))
+    results = dedupe(results)
     if not results:
         print("[scaling] no bench.py results found", file=sys.stderr)
         return 1

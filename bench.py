@@ -344,6 +344,16 @@ def _arm(line: "dict | None") -> None:
         native().arm_final_line(json.dumps(line))
 
 
+RCCL_KNOBS = ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS", "NCCL_BUFFSIZE",
+              "NCCL_NTHREADS", "RCCL_MSCCL_ENABLE", "RCCL_MSCCLPP_ENABLE")
+
+
+def _rccl_env() -> str:
+    """The RCCL tuning knobs this run had set ("NCCL_ALGO=Ring NCCL_PROTO=Simple ..."; "" = RCCL's
+    defaults): tools/sweep.py --rccl-knobs sweeps them, and the record must say which ran."""
+    return " ".join(f"{k}={os.environ[k]}" for k in RCCL_KNOBS if k in os.environ)
+
+
 def _launch_record(ctx, seen: int) -> dict:
     """JSON fields that prove the job's shape: who started the ranks and how many the collective saw."""
     launcher = os.environ.get(LAUNCHER_ENV) or ("external" if "WORLD_SIZE" in os.environ else "single process")
@@ -445,7 +455,8 @@ def run_vector(args, ctx, cfg, fault) -> int:
             "data": "reduce.c MT19937 per-rank data" if dev.type == "cpu" else "synthetic rank-seeded device fill",
             "config": {"model": f"{cfg.name}: {cfg.description}", "global_batch": wl.count * ctx.world_size,
                        "seq_len": 1, "parallelism": f"dp{ctx.world_size}", "backend": ctx.backend,
-                       "impl": wl.impl, "op": cfg.op.upper(), "count_per_rank": wl.count},
+                       "impl": wl.impl, "op": cfg.op.upper(), "count_per_rank": wl.count,
+                       "rccl_env": _rccl_env()},
             "baseline_value": cfg.baseline, "baseline_unit": cfg.baseline_unit if cfg.baseline else None,
             "baseline_source": cfg.baseline_source or None,
             "verified": verified,
@@ -1427,6 +1438,7 @@ def main(argv=None) -> int:
             "baseline_source": cfg.baseline_source,
             "native_ext": os.path.basename(native_path()),
             "ranks_seen_backend": ctx.backend,
+            "rccl_env": _rccl_env(),
             "budget_s": args.budget,
             "headline_done_s": round(time.time() - T0, 2),
         }

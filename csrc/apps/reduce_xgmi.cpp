@@ -163,6 +163,20 @@ double time_iters(Ctx& c, F&& body) {
   return c.boot->max_double(dt);
 }
 
+// The RCCL tuning knobs this process ran with (tools/sweep.py --rccl-knobs sets them per point):
+// "NCCL_ALGO=Ring NCCL_PROTO=Simple ..." for every NCCL_* / RCCL_* variable set, "" for none.
+std::string rccl_env() {
+  std::string out;
+  for (const char* k : {"NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS", "NCCL_BUFFSIZE",
+                        "NCCL_NTHREADS", "RCCL_MSCCL_ENABLE", "RCCL_MSCCLPP_ENABLE"}) {
+    if (const char* v = std::getenv(k)) {
+      if (!out.empty()) out += ' ';
+      out += std::string(k) + '=' + v;
+    }
+  }
+  return out;
+}
+
 void emit(Ctx& c, DType t, Op o, double bytes_total, double dt, Json extra) {
   const double gib = bytes_total / dt / kGiB;
   const double gb = bytes_total / dt / kGB;
@@ -174,7 +188,7 @@ void emit(Ctx& c, DType t, Op o, double bytes_total, double dt, Json extra) {
           .set("dtype", dtype_gnuplot_name(t)).set("op", op_name(o)).set("ranks", c.env.world)
           .set("bytes_total", bytes_total).set("seconds", dt).set("gib_per_s", gib).set("gb_per_s", gb)
           .set("iters", c.iters).set("graph", c.graph).set("rccl_version", RcclComm::version())
-          .set("launcher", c.env.launcher);
+          .set("launcher", c.env.launcher).set("rccl_env", rccl_env());
       extra.write_file(c.json);
     }
   }

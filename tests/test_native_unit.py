@@ -1,5 +1,6 @@
 """Native C++ unit tests (host code), the TCP bootstrap under torchrun and mpirun, host
 sanitizers (ASan/UBSan on host code), and the resumable sweep orchestration."""
+import json
 import os
 import re
 import sys
@@ -77,6 +78,62 @@ def test_sweep_resume_and_collect(tmp_path):
     assert res[0] == "" and [ln.split()[2] for ln in res[1:]] == ["1", "2"]
     r2 = run(cmd, timeout=300)
     assert "P=1: done, skipping" in r2.stdout and "P=2: done, skipping" in r2.stdout
+
+
+def test_sweep_knob_grid_settings():
+    # the RCCL knob grid (default 2 x 2 x 3 settings), named per setting, with
+    # "default" meaning the variable is left unset and every other knob removed from the environment
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("sweep_knobs", os.path.join(ROOT, "tools", "sweep.py"))
+    sw = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sw)
+    st = sw.knob_settings()
+    assert len(st) == 12 and len({n for n, _ in st}) == 12
+    names = dict(st)
+    assert names["rccl-ring-simple-chdefault"] == {"NCCL_ALGO": "Ring", "NCCL_PROTO": "Simple",
+                                                   "NCCL_MIN_NCHANNELS": None}
+    assert names["rccl-tree-ll128-ch32"]["NCCL_MIN_NCHANNELS"] == "32"
+    os.environ["NCCL_PROTO"] = "LL"
+    try:
+        env = sw.knob_env({"NCCL_ALGO": "Tree", "NCCL_MIN_NCHANNELS": None})
+    finally:
+        os.environ.pop("NCCL_PROTO")
+    assert env["NCCL_ALGO"] == "Tree" and "NCCL_PROTO" not in env and "NCCL_MIN_NCHANNELS" not in env
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="MPICH not available")
+def test_sweep_rccl_knobs_writes_getavgs_results_per_setting(tmp_path):
+    # the knob sweep's orchestration on CPU ranks (reduce_mpi: the same reduce.c rows; MPICH ignores
+    # the NCCL_* variables): one getAvgs results directory per setting and the comparison table
+    out = tmp_path / "knobs"
+    r = run(["python", os.path.join(ROOT, "tools", "sweep.py"), "--rccl-knobs", "--app", "reduce_mpi", "--ranks", "2",
+             "--knob-grid", "NCCL_ALGO=Ring,Tree;NCCL_PROTO=Simple", "--out", str(out), "--",
+             "--ints=16k", "--doubles=16k", "--retries=2"], timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for name, algo in (("rccl-ring-simple", "Ring"), ("rccl-tree-simple", "Tree")):
+        sub = out / name
+        assert json.loads((sub / "knobs.json").read_text()) == {"NCCL_ALGO": algo, "NCCL_PROTO": "Simple"}
+        res = (sub / "results" / "DOUBLE_SUM.txt").read_text().splitlines()
+        assert res[0] == "" and res[1].split()[:3] == ["DOUBLE", "SUM", "2"]
+    md = (out / "rccl_knobs.md").read_text()
+    rows = [ln for ln in md.splitlines() if ln.startswith("| DOUBLE | SUM | 2 |")]
+    assert len(rows) == 2 and sum("**" in ln for ln in rows) >= 1, md
+
+
+def test_sweep_rccl_knobs_env_reaches_the_json(tmp_path):
+    # env passthrough: bench.py's reduce.c config on two gloo CPU ranks records the knobs it ran with
+    out = tmp_path / "knobs_bench"
+    r = run(["python", os.path.join(ROOT, "tools", "sweep.py"), "--rccl-knobs", "--app", "bench", "--ranks", "2",
+             "--knob-grid", "NCCL_ALGO=Tree;NCCL_MIN_NCHANNELS=default,16", "--out", str(out), "--",
+             "--config", "mpi_1m_int32_sum_cpu2", "--steps", "2", "--warmup", "1"], timeout=600,
+            env={"NCCL_PROTO": "LL"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = {}
+    for name in ("rccl-tree-chdefault", "rccl-tree-ch16"):
+        d = json.loads((out / name / "bench.jsonl").read_text().splitlines()[0])
+        assert d["verified"] is True
+        got[name] = d["config"]["rccl_env"]
+    assert got == {"rccl-tree-chdefault": "NCCL_ALGO=Tree", "rccl-tree-ch16": "NCCL_ALGO=Tree NCCL_MIN_NCHANNELS=16"}
 
 
 def test_sweep_node_preset_matrix():

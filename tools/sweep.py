@@ -13,6 +13,16 @@ reduce.c-format line into ``<out>/collected.txt``, averages them (tools/getAvgs.
     python tools/sweep.py --app reduce_mpi --ranks 2,4 --out runs/mpi -- --ints=1M --doubles=1M
     python tools/sweep.py --preset node --out runs/node      # the whole 1/2/4/8-GPU matrix below
 
+``--rccl-knobs`` sweeps RCCL's tuning knobs over reduce.c's element-wise table (the
+algorithm / protocol / channel count decide how much of the 7 xGMI links a collective uses):
+``NCCL_ALGO`` x ``NCCL_PROTO`` x ``NCCL_MIN_NCHANNELS`` (``--knob-grid``, default Ring|Tree x
+Simple|LL128 x default|16|32), one sub-directory per setting (``rccl-<algo>-<proto>-ch<n>/``, with
+``knobs.json`` and getAvgs-format ``collected.txt`` / ``results/``), every other NCCL_* knob unset,
+and ``<out>/rccl_knobs.md``: GiB/s per setting x N for each DATATYPE x OP, best setting per N marked.
+
+    python tools/sweep.py --rccl-knobs --ranks 2,4,8 --out runs/knobs            # reduce_xgmi, reduce
+    python tools/sweep.py --rccl-knobs --ranks 2,4,8 --out runs/knobs --rccl-collective allreduce
+
 ``--preset node`` runs, resumable point by point: the xGMI roofline (``bandwidth_test --peer``, once);
 reduce.c's vector benchmark over every collective — RCCL ``reduce`` / ``allreduce`` and the one-kernel
 direct ``direct-reduce`` / ``direct`` (csrc/kernels/direct.hip), each graph-replayed — at every rank
@@ -79,7 +89,87 @@ def node_preset(extra: list[str]) -> list[tuple]:
     return entries
 
 
-def run_points(app: str, name: str, ranks: list, extra: list[str], out: str, timeout: float, force: bool) -> int:
+KNOB_GRID = "NCCL_ALGO=Ring,Tree;NCCL_PROTO=Simple,LL128;NCCL_MIN_NCHANNELS=default,16,32"
+KNOB_VARS = ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS", "NCCL_BUFFSIZE",
+             "NCCL_NTHREADS", "RCCL_MSCCL_ENABLE", "RCCL_MSCCLPP_ENABLE")
+
+
+def knob_settings(grid: str = KNOB_GRID) -> list:
+    """Every combination of ``VAR=v1,v2;VAR=...`` (``default`` = leave the variable unset), as
+    (name, {VAR: value or None})."""
+    import itertools
+    axes = []
+    for part in (p for p in grid.split(";") if p.strip()):
+        var, vals = part.split("=", 1)
+        axes.append([(var.strip(), None if v.strip() == "default" else v.strip()) for v in vals.split(",")])
+    out = []
+    for combo in itertools.product(*axes):
+        short = {"NCCL_ALGO": "", "NCCL_PROTO": "", "NCCL_MIN_NCHANNELS": "ch"}
+        name = "rccl-" + "-".join(f"{short.get(k, k.lower() + '_')}{v if v is not None else 'default'}".lower()
+                                  for k, v in combo)
+        out.append((name, dict(combo)))
+    return out
+
+
+def knob_env(setting: dict) -> dict:
+    """The process environment of one knob setting: every known knob unset, then the setting's."""
+    env = {k: v for k, v in os.environ.items() if k not in KNOB_VARS}
+    env.update({k: v for k, v in setting.items() if v is not None})
+    return env
+
+
+def run_knobs(a) -> int:
+    """``--rccl-knobs``: reduce.c's table over RCCL for every knob setting (resumable per point)."""
+    ranks = [int(x) for x in a.ranks.split(",") if x]
+    app = a.app or "reduce_xgmi"
+    failures, table = 0, []
+    for name, setting in knob_settings(a.knob_grid):
+        sub = os.path.join(a.out, name)
+        os.makedirs(sub, exist_ok=True)
+        with open(os.path.join(sub, "knobs.json"), "w") as f:
+            json.dump({k: v for k, v in setting.items()}, f)
+        args = list(a.extra)
+        if app == "reduce_xgmi":
+            args = ["--mode=vector", f"--collective={a.rccl_collective}", "--graph", "--dtypes=INT,DOUBLE",
+                    "--json=points.jsonl"] + args
+        failures += run_points(app, name, ranks, args, os.path.abspath(sub), a.timeout, a.force,
+                               env=knob_env(setting))
+        collect(sub, name)
+        table.append((name, setting, _results_means(os.path.join(sub, "results"))))
+    with open(os.path.join(a.out, "rccl_knobs.md"), "w") as f:
+        f.write(knob_table(table))
+    print(knob_table(table), end="")
+    return 1 if failures else 0
+
+
+def _results_means(results_dir: str) -> dict:
+    """{(DT, OP, N): GiB/s} from a getAvgs results directory (missing -> {})."""
+    out = {}
+    if not os.path.isdir(results_dir):
+        return out
+    for fn in sorted(os.listdir(results_dir)):
+        for line in open(os.path.join(results_dir, fn)):
+            f = line.split()
+            if len(f) == 4:
+                out[(f[0], f[1], int(f[2]))] = float(f[3])
+    return out
+
+
+def knob_table(table: list) -> str:
+    """Markdown: one row per (DATATYPE, OP, N) x setting, the best setting per (DATATYPE, OP, N) in bold."""
+    keys = sorted({k for _, _, m in table for k in m})
+    lines = ["| DATATYPE | OP | N | setting | GiB/s |", "|---|---|---|---|---|"]
+    for k in keys:
+        vals = [(name, m[k]) for name, _, m in table if k in m]
+        best = max(v for _, v in vals)
+        for name, v in vals:
+            cell = f"**{v:.3f}**" if v == best else f"{v:.3f}"
+            lines.append(f"| {k[0]} | {k[1]} | {k[2]} | {name} | {cell} |")
+    return "\n".join(lines) + "\n"
+
+
+def run_points(app: str, name: str, ranks: list, extra: list[str], out: str, timeout: float, force: bool,
+               env: "dict | None" = None) -> int:
     failures = 0
     for p in ranks:
         base = os.path.join(out, f"stdout-{name}-P{p}")
@@ -95,7 +185,7 @@ def run_points(app: str, name: str, ranks: list, extra: list[str], out: str, tim
         for attempt in range(2):
             print(f"[sweep] {name} P={p}: {' '.join(cmd)}", flush=True)
             try:
-                r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=out)
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=out, env=env)
                 rc, stdout, err = r.returncode, r.stdout, r.stderr
             except subprocess.TimeoutExpired as e:
                 rc, stdout, err = 124, e.stdout or "", (e.stderr or "") + "\n[sweep] timeout"
@@ -157,6 +247,12 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--app", choices=["bench", "reduce_xgmi", "reduce_mpi", "reduction"])
     ap.add_argument("--preset", choices=["node"], help="run a predefined matrix instead of one --app")
+    ap.add_argument("--rccl-knobs", action="store_true",
+                    help="sweep RCCL's NCCL_ALGO / NCCL_PROTO / NCCL_MIN_NCHANNELS over reduce.c's table "
+                         "(--app: reduce_xgmi by default)")
+    ap.add_argument("--knob-grid", default=KNOB_GRID, help="VAR=v1,v2;VAR=... (default: %(default)s)")
+    ap.add_argument("--rccl-collective", default="reduce", choices=["reduce", "allreduce"],
+                    help="--rccl-knobs with reduce_xgmi: MPI_Reduce-like (reduce.c) or all-reduce")
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--out", required=True)
     ap.add_argument("--name", default="")
@@ -165,6 +261,8 @@ def main(argv=None) -> int:
     ap.add_argument("extra", nargs="*")
     a = ap.parse_args(argv)
     os.makedirs(a.out, exist_ok=True)
+    if a.rccl_knobs:
+        return run_knobs(a)
     if a.preset:
         return run_preset(a)
     if not a.app:

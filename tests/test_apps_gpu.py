@@ -191,7 +191,7 @@ def test_cpp_consumer_example():
 
 # ---------------------------------------------------------------------------------------------
 # Multi-rank paths rehearsed on the 1-GPU box (every rank on GPU 0).
-from helpers import ROOT, torchrun  # noqa: E402
+from helpers import ROOT, bench_record, torchrun  # noqa: E402
 
 
 @pytest.mark.parametrize("collective", ["direct", "direct-reduce"])
@@ -260,7 +260,7 @@ def test_bench_rehearsal_two_ranks_one_gpu(tmp_path):
         else:
             os.environ["MIREDUCE_FORCE_DEVICE"] = env_before
     assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    d = bench_record(r.stdout)
     assert d["verified"] is True and d["n_gpus"] == 2 and d["config"]["backend"] == "gloo"
 
 
@@ -272,7 +272,7 @@ def test_bench_graph_capture_failure_falls_back_on_all_ranks(tmp_path, monkeypat
                      "--warmup", "2", "--elements", "20000003", "--launch", "graph", "--collective", "rccl"],
                  cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    d = bench_record(r.stdout)
     assert d["verified"] is True
     assert d["config"]["launch"].startswith("eager (graph capture failed"), d["config"]["launch"]
 
@@ -283,7 +283,7 @@ def test_bench_launch_modes(tmp_path, launch):
     r = run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-vector-extras", "--steps", "37", "--warmup", "3", "--elements",
              "50000017", "--launch", launch, "--graph-chunk", "16"], cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    d = bench_record(r.stdout)
     assert d["verified"] is True and d["steps"] == 37
     assert d["config"]["launch"].startswith(launch)
     if launch == "graph":
@@ -369,7 +369,7 @@ def test_bench_maxloc_config(tmp_path, launch):
     r = run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "xgmi_1b_double_maxloc", "--steps", "20",
              "--warmup", "3", "--elements", "50000017", "--launch", launch], cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
-    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    d = bench_record(r.stdout)
     assert d["verified"] is True and d["config"]["op"] == "MAXLOC"
     assert d["config"]["launch"].startswith(launch)
     assert d["config"]["kernel_plan"]["splits"] > 1

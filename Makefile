@@ -45,7 +45,7 @@ COMMLIB     := $(BUILD)/lib/libmireduce_comm.a
 APPS := $(BUILD)/bin/reduction $(BUILD)/bin/reduce_xgmi $(BUILD)/bin/bandwidth_test
 MPI_APP := $(BUILD)/bin/reduce_mpi
 
-.PHONY: all python apps mpi clean asan tsan unit diag examples window_ab dyntail_ab i32sum_ab
+.PHONY: all python apps mpi clean asan tsan unit diag examples window_ab dyntail_ab i32sum_ab launch_floor
 all: python apps mpi unit diag examples
 
 python: $(PYEXT)
@@ -125,6 +125,16 @@ $(BUILD)/obj/tools/dyntail_ab.o: tools/dyntail_ab.hip $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 $(BUILD)/bin/dyntail_ab: $(BUILD)/obj/tools/dyntail_ab.o $(LIB)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive $(LDLIBS) -o $@
+
+# Where the per-launch fixed cost goes: empty / args / fan-in-only kernels vs the production
+# reduction, graph-replayed (tools/launch_floor.hip).
+launch_floor: $(BUILD)/bin/launch_floor
+$(BUILD)/obj/tools/launch_floor.o: tools/launch_floor.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+$(BUILD)/bin/launch_floor: $(BUILD)/obj/tools/launch_floor.o $(LIB)
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive $(LDLIBS) -o $@
 

@@ -41,6 +41,13 @@ struct ReduceConfig {
   // two-pass): the kernel anchors the parity on the device. (profiles/r4_xcd/, r4_ab/, r4_skew/)
   int xcd_skew = -2147483647 - 1;
   bool single_pass = true;   // last-arriver finalisation vs a second finalize launch
+  // Segmented launches (polled single-pass only): an array of more than 2 x kSegmentBytes bytes is
+  // reduced as a sequence of launches over consecutive segments of about this many bytes on the
+  // same stream, each segment's result carried into the last launch, which folds them with its own
+  // (and does the fused cross-rank finish). One launch over ~292 GB streamed 2.4 % slower than the
+  // same bytes as 8 GB launches (profiles/r5_hbmfill/): 0 = auto (kSegmentBytes above
+  // 2 x kSegmentBytes), < 0 = one launch, > 0 = this segment size (bytes, rounded to 1 MiB).
+  int64_t segment_bytes = 0;
   // Fused cross-rank finish: XrankChannel::device_desc() (xrank.hpp). The launch then writes the
   // fold over every rank's partial into out (single-pass only).
   const void* xrank = nullptr;
@@ -78,7 +85,18 @@ struct LaunchPlan {
   uint64_t head = 0;   // scalar elements before the first 16-B aligned vector
   uint64_t nvec = 0;   // 16-byte vectors in the streaming body
   uint64_t tail = 0;   // scalar elements after the body
+  // Segmented launches (ReduceConfig::segment_bytes): the fields above describe the first segment.
+  int segments = 1;
+  uint64_t segment_elems = 0;  // elements per segment (the last one holds the rest); 0 = not segmented
 };
+
+// Auto segment size of ReduceConfig::segment_bytes (8 GiB).
+constexpr int64_t kSegmentBytes = int64_t{8} << 30;
+
+// Fill `whole.segments` / `segment_elems` for a reduction of n elements planned as `whole`
+// (plan_reduce over the whole array): the segmentation reduce() / BoundReduce would use with a
+// workspace allowing `max_carry` carried results (min(256, max_grid)).
+void plan_segmentation(size_t n, DType t, const ReduceConfig& cfg, LaunchPlan& whole, int max_carry = 256);
 
 // Device scratch for one reduction stream: per-workgroup partials, per-group partials, the
 // arrival tickets (zeroed once; the last arriver of each launch resets them), the polled fan-in's

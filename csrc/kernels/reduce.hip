@@ -407,12 +407,47 @@ static FanEnd fan_end(const kern::Args& a, const Workspace& ws) {
   return f;
 }
 
-LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
-                  hipStream_t stream, const ReduceConfig& cfg) {
-  const int c = combo_index(op, t, acc);
-  MIREDUCE_REQUIRE(c >= 0, "unsupported (dtype, op, accumulator) combination");
-  MIREDUCE_REQUIRE(out != nullptr, "output pointer is null");
-  LaunchPlan p = plan_reduce(in, n, t, cfg, ws.num_cus(), ws.max_grid(), op);
+// Segmented launches (ReduceConfig::segment_bytes): how many consecutive segments of how many
+// elements; {1, 0} = one launch. Polled single-pass launches only (the last segment's finisher folds
+// the earlier segments' results, one per lane of its first wave: at most `max_carry` of them).
+struct Segments {
+  int count = 1;
+  uint64_t elems = 0;
+};
+static Segments plan_segments(size_t n, size_t es, const ReduceConfig& cfg, const LaunchPlan& whole, int max_carry) {
+  Segments sg;
+  if (!whole.poll || !whole.single_pass || cfg.segment_bytes < 0 || n == 0) return sg;
+  const uint64_t bytes = static_cast<uint64_t>(n) * es;
+  if (cfg.segment_bytes == 0 && bytes <= 2 * static_cast<uint64_t>(kSegmentBytes)) return sg;
+  constexpr uint64_t kMiB = 1ull << 20;
+  const uint64_t want = cfg.segment_bytes > 0 ? static_cast<uint64_t>(cfg.segment_bytes) : kSegmentBytes;
+  const uint64_t quantum = kMiB / es;  // segments start on 1 MiB boundaries of the array
+  uint64_t elems = std::max<uint64_t>(1, want / kMiB) * quantum;
+  uint64_t count = (n + elems - 1) / elems;
+  if (count > static_cast<uint64_t>(max_carry) + 1) {  // fewer, larger segments
+    elems = ((n + max_carry) / (static_cast<uint64_t>(max_carry) + 1) + quantum - 1) / quantum * quantum;
+    count = (n + elems - 1) / elems;
+  }
+  if (count <= 1) return sg;
+  sg.count = static_cast<int>(count);
+  sg.elems = elems;
+  return sg;
+}
+
+namespace {
+
+// One launch of the streaming kernel over [in, in + n): its plan, arguments and table entry.
+struct Launch {
+  LaunchPlan plan;
+  kern::Args args;
+  LaunchFn fn = nullptr;
+};
+
+Launch make_launch(const void* in, size_t n, DType t, Op op, int c, void* out, Workspace& ws, const ReduceConfig& cfg,
+                   const void* xrank, const void* carry, unsigned ncarry) {
+  Launch L;
+  L.plan = plan_reduce(in, n, t, cfg, ws.num_cus(), ws.max_grid(), op);
+  const LaunchPlan& p = L.plan;
   kern::Args a = make_args(in, p, t, cfg);
   a.partials = ws.partials();
   a.group_partials = ws.group_partials();
@@ -424,12 +459,68 @@ LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out
   a.fan = ws.fan();
   a.fan_slots = static_cast<unsigned>(ws.max_grid());
   a.two_pass_epoch = p.single_pass ? 0 : 1;
-  a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
-  const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][body_index(p)];
-  fn(a, p.grid, stream);
-  MIREDUCE_HIP_THROW(hipGetLastError());
-  if (!p.single_pass) fold_partials(ws.partials(), p.grid, acc, op, out, stream, fan_end(a, ws));
-  return p;
+  a.xrank = static_cast<const XrankDesc*>(xrank);
+  a.carry = carry;
+  a.ncarry = ncarry;
+  L.args = a;
+  L.fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][body_index(p)];
+  return L;
+}
+
+// Every launch of a reduction: one, or (segmented) one per segment — the earlier segments write
+// their results into the workspace's partials (unused by the polled fan-in), the last one carries
+// them in, writes `out` and does the fused cross-rank finish. The returned plans' first entry
+// describes the first launch, with `segments` / `segment_elems` set.
+std::vector<Launch> make_launches(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
+                                  const ReduceConfig& cfg) {
+  const int c = combo_index(op, t, acc);
+  MIREDUCE_REQUIRE(c >= 0, "unsupported (dtype, op, accumulator) combination");
+  MIREDUCE_REQUIRE(out != nullptr, "output pointer is null");
+  std::vector<Launch> v;
+  v.push_back(make_launch(in, n, t, op, c, out, ws, cfg, cfg.xrank, nullptr, 0));
+  const size_t es = dtype_size(t);
+  const Segments sg = plan_segments(n, es, cfg, v[0].plan, std::min(256, ws.max_grid()));
+  if (sg.count == 1) return v;
+  v.clear();
+  const size_t as = dtype_size(acc);
+  char* carry = static_cast<char*>(ws.partials());
+  for (int k = 0; k < sg.count; ++k) {
+    const uint64_t off = static_cast<uint64_t>(k) * sg.elems;
+    const uint64_t nk = std::min<uint64_t>(sg.elems, n - off);
+    const void* ink = static_cast<const char*>(in) + off * es;
+    const bool last = k == sg.count - 1;
+    v.push_back(make_launch(ink, nk, t, op, c, last ? out : carry + k * as, ws, cfg, last ? cfg.xrank : nullptr,
+                            last ? carry : nullptr, last ? static_cast<unsigned>(sg.count - 1) : 0u));
+  }
+  v[0].plan.segments = sg.count;
+  v[0].plan.segment_elems = sg.elems;
+  return v;
+}
+
+void run_launches(const std::vector<Launch>& v, void* out, Op op, DType acc, const Workspace& ws,
+                  hipStream_t stream) {
+  for (size_t k = 0; k < v.size(); ++k) {
+    kern::Args a = v[k].args;
+    if (out && k + 1 == v.size()) a.out = out;
+    v[k].fn(a, v[k].plan.grid, stream);
+    MIREDUCE_HIP_THROW(hipGetLastError());
+    if (!v[k].plan.single_pass) fold_partials(a.partials, v[k].plan.grid, acc, op, a.out, stream, fan_end(a, ws));
+  }
+}
+
+}  // namespace
+
+void plan_segmentation(size_t n, DType t, const ReduceConfig& cfg, LaunchPlan& whole, int max_carry) {
+  const Segments sg = plan_segments(n, dtype_size(t), cfg, whole, max_carry);
+  whole.segments = sg.count;
+  whole.segment_elems = sg.elems;
+}
+
+LaunchPlan reduce(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
+                  hipStream_t stream, const ReduceConfig& cfg) {
+  const std::vector<Launch> v = make_launches(in, n, t, op, acc, out, ws, cfg);
+  run_launches(v, nullptr, op, acc, ws, stream);
+  return v[0].plan;
 }
 
 unsigned reduce_checked(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
@@ -450,9 +541,7 @@ unsigned reduce_checked(const void* in, size_t n, DType t, Op op, DType acc, voi
 }
 
 struct BoundReduce::Impl {
-  kern::Args args;
-  LaunchFn fn;
-  LaunchPlan plan;
+  std::vector<Launch> launches;  // one, or one per segment (make_launches)
   Op op;
   DType acc;
   const Workspace* ws;
@@ -460,39 +549,15 @@ struct BoundReduce::Impl {
 
 BoundReduce::BoundReduce(const void* in, size_t n, DType t, Op op, DType acc, void* out, Workspace& ws,
                          const ReduceConfig& cfg)
-    : impl_(nullptr) {
-  const int c = combo_index(op, t, acc);
-  MIREDUCE_REQUIRE(c >= 0, "unsupported (dtype, op, accumulator) combination");
-  MIREDUCE_REQUIRE(out != nullptr, "output pointer is null");
-  const LaunchPlan p = plan_reduce(in, n, t, cfg, ws.num_cus(), ws.max_grid(), op);
-  kern::Args a = make_args(in, p, t, cfg);
-  a.partials = ws.partials();
-  a.group_partials = ws.group_partials();
-  a.tickets = ws.tickets();
-  a.out = out;
-  a.groups = p.groups;
-  a.flat = p.flat ? 1 : 0;
-  a.slots = p.poll ? ws.slots() : nullptr;
-  a.fan = ws.fan();
-  a.fan_slots = static_cast<unsigned>(ws.max_grid());
-  a.two_pass_epoch = p.single_pass ? 0 : 1;
-  a.xrank = static_cast<const XrankDesc*>(cfg.xrank);
-  impl_ = new Impl{a, table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][body_index(p)],
-                   p, op, acc, &ws};
-}
+    : impl_(new Impl{make_launches(in, n, t, op, acc, out, ws, cfg), op, acc, &ws}) {}
 
 BoundReduce::~BoundReduce() { delete impl_; }
 
 void BoundReduce::launch(hipStream_t stream, void* out) const {
-  kern::Args a = impl_->args;
-  if (out) a.out = out;
-  impl_->fn(a, impl_->plan.grid, stream);
-  MIREDUCE_HIP_THROW(hipGetLastError());
-  if (!impl_->plan.single_pass)
-    fold_partials(a.partials, impl_->plan.grid, impl_->acc, impl_->op, a.out, stream, fan_end(a, *impl_->ws));
+  run_launches(impl_->launches, out, impl_->op, impl_->acc, *impl_->ws, stream);
 }
 
-const LaunchPlan& BoundReduce::plan() const { return impl_->plan; }
+const LaunchPlan& BoundReduce::plan() const { return impl_->launches[0].plan; }
 
 unsigned BoundReduce::error() const { return impl_->ws->error(); }
 

@@ -96,6 +96,8 @@ struct Args {
   uint64_t x_ra;           // weighted split, precomputed on the host: common rounds (ntiles / grid at 0)
   uint64_t x_dd;           // extra rounds actually given to the favoured parity
   int two_pass_epoch;      // two-pass launch whose finalize ends the fan-in epoch (fan[0]; XcdAnchor)
+  const void* carry;       // segmented launches (polled fan-in): AccT[ncarry] results of the earlier
+  unsigned ncarry;         // segments (written by earlier kernels), folded in by this launch's finisher
 };
 
 // Polled fan-in: a published partial is two 8-byte words (epoch << 32 | 32 data bits), where the
@@ -768,6 +770,10 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
       __hip_atomic_store(sl + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (blockIdx.x != gridDim.x - 1) return;
+    // Segmented launches: the earlier segments' results (kernel boundaries ago: plain loads), one per
+    // lane, issued before the poll so their latency hides under it.
+    AccT carried = OpT::template identity<AccT>();
+    if (threadIdx.x < a.ncarry) carried = static_cast<const AccT*>(a.carry)[threadIdx.x];
     // The finisher: start the cross-rank descriptor loads and the sticky-error load now, they land
     // while it polls.
     XrankLane xl{};
@@ -834,7 +840,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     }
     // Any lane past the bound (or an earlier launch's sticky error) poisons this launch's result.
     const bool bad = __syncthreads_or(late) || fan_err != 0 || anchor_late;
-    t = block_reduce<OpT, AccT, BLOCK>(t, lds);
+    t = block_reduce<OpT, AccT, BLOCK>(OpT::apply(t, carried), lds);
     if (fan_e == 0xffffffffu) {  // the epoch wraps after this launch: invalidate every slot first
       __syncthreads();
       for (unsigned i = threadIdx.x; i < 2u * a.fan_slots; i += BLOCK)

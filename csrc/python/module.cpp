@@ -56,14 +56,18 @@ py::dict plan_dict(const LaunchPlan& p) {
   d["head"] = p.head;
   d["nvec"] = p.nvec;
   d["tail"] = p.tail;
+  d["segments"] = p.segments;
+  d["segment_elems"] = p.segment_elems;
   return d;
 }
 
 constexpr int kSkewAuto = -2147483647 - 1;  // ReduceConfig::xcd_skew's "tuned default"
 
 ReduceConfig make_cfg(int block, int unroll, int wg_per_cu, int max_blocks, int groups,
-                      int policy, bool single_pass, int pipeline = -1, int window = -1, int xcd_skew = kSkewAuto) {
+                      int policy, bool single_pass, int pipeline = -1, int window = -1, int xcd_skew = kSkewAuto,
+                      int64_t segment_bytes = 0) {
   ReduceConfig c;
+  c.segment_bytes = segment_bytes;
   c.window = window;
   c.xcd_skew = xcd_skew;
   c.block = block;
@@ -180,9 +184,10 @@ PYBIND11_MODULE(_C, m) {
   py::class_<BoundReduce>(m, "BoundReduce")
       .def(py::init([](Workspace& ws, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out,
                        int block, int unroll, int wg_per_cu, int max_blocks, int groups, int policy,
-                       bool single_pass, int pipeline, uintptr_t xrank, int window, int xcd_skew) {
+                       bool single_pass, int pipeline, uintptr_t xrank, int window, int xcd_skew,
+                       int64_t segment_bytes) {
              ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline,
-                                         window, xcd_skew);
+                                         window, xcd_skew, segment_bytes);
              cfg.xrank = as_ptr<const void>(xrank);
              return new BoundReduce(as_ptr<const void>(in), n, static_cast<DType>(dtype), static_cast<Op>(op),
                                     static_cast<DType>(acc), as_ptr<void>(out), ws, cfg);
@@ -191,7 +196,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("out_ptr"), py::arg("block") = 0, py::arg("unroll") = 0, py::arg("wg_per_cu") = 0,
            py::arg("max_blocks") = 0, py::arg("groups") = 0, py::arg("policy") = -1,
            py::arg("single_pass") = true, py::arg("pipeline") = -1, py::arg("xrank") = 0, py::arg("window") = -1,
-           py::arg("xcd_skew") = kSkewAuto,
+           py::arg("xcd_skew") = kSkewAuto, py::arg("segment_bytes") = 0,
            py::keep_alive<1, 2>())
       .def("launch", [](const BoundReduce& b, uintptr_t stream, uintptr_t out) { b.launch(as_stream(stream), as_ptr<void>(out)); },
            py::arg("stream"), py::arg("out_ptr") = 0)
@@ -282,9 +287,9 @@ PYBIND11_MODULE(_C, m) {
          uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks, int groups,
          int policy, bool single_pass, int pipeline, uint64_t fanin_bound_ticks, int debug_delay_wg,
          uint64_t debug_delay_ticks, int window, uintptr_t xrank, uintptr_t wg_stamps, int xcd_skew,
-         uint64_t debug_delay_anchor_ticks) {
+         uint64_t debug_delay_anchor_ticks, int64_t segment_bytes) {
         ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline, window,
-                                    xcd_skew);
+                                    xcd_skew, segment_bytes);
         cfg.xrank = as_ptr<const void>(xrank);
         cfg.debug_wg_stamps = as_ptr<uint64_t>(wg_stamps);
         cfg.fanin_bound_ticks = fanin_bound_ticks;
@@ -302,24 +307,26 @@ PYBIND11_MODULE(_C, m) {
       py::arg("groups") = 0, py::arg("policy") = -1, py::arg("single_pass") = true,
       py::arg("pipeline") = -1, py::arg("fanin_bound_ticks") = 0, py::arg("debug_delay_wg") = -1,
       py::arg("debug_delay_ticks") = 0, py::arg("window") = -1, py::arg("xrank") = 0, py::arg("wg_stamps") = 0,
-      py::arg("xcd_skew") = kSkewAuto, py::arg("debug_delay_anchor_ticks") = 0);
+      py::arg("xcd_skew") = kSkewAuto, py::arg("debug_delay_anchor_ticks") = 0, py::arg("segment_bytes") = 0);
 
   m.def(
       "plan",
       [](uintptr_t in, uint64_t n, int dtype, int num_cus, int max_grid, int block, int unroll,
          int wg_per_cu, int max_blocks, int groups, int policy, bool single_pass, int pipeline, int window,
-         int op, int xcd_skew) {
+         int op, int xcd_skew, int64_t segment_bytes) {
         MIREDUCE_REQUIRE(op >= 0 && op < kNumOps, "op out of range");
-        return plan_dict(plan_reduce(as_ptr<const void>(in), n, static_cast<DType>(dtype),
-                                     make_cfg(block, unroll, wg_per_cu, max_blocks, groups,
-                                              policy, single_pass, pipeline, window, xcd_skew),
-                                     num_cus, max_grid, static_cast<Op>(op)));
+        const ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline,
+                                          window, xcd_skew, segment_bytes);
+        LaunchPlan p = plan_reduce(as_ptr<const void>(in), n, static_cast<DType>(dtype), cfg, num_cus, max_grid,
+                                   static_cast<Op>(op));
+        plan_segmentation(n, static_cast<DType>(dtype), cfg, p, std::min(256, max_grid));
+        return plan_dict(p);
       },
       py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("num_cus") = 256,
       py::arg("max_grid") = 16384, py::arg("block") = 0, py::arg("unroll") = 0,
       py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0, py::arg("groups") = 0,
       py::arg("policy") = -1, py::arg("single_pass") = true, py::arg("pipeline") = -1, py::arg("window") = -1,
-      py::arg("op") = 0, py::arg("xcd_skew") = kSkewAuto);
+      py::arg("op") = 0, py::arg("xcd_skew") = kSkewAuto, py::arg("segment_bytes") = 0);
 
   m.def(
       "reduce_partials",

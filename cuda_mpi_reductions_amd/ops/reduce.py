@@ -99,6 +99,7 @@ class KernelConfig:
     pipelined: Optional[bool] = None    # None: tuned choice
     window: Optional[int] = None        # loads in flight per thread: None tuned, 0 hipcc's schedule, 2 | 4
     xcd_skew: Optional[int] = None      # XCD-weighted split, permille of rounds (+: odd XCCs more); None tuned
+    segment_bytes: int = 0              # segmented launches: 0 auto (8 GiB above 16 GiB), < 0 one launch, > 0 size
 
     @property
     def policy(self) -> int:
@@ -116,6 +117,7 @@ class KernelConfig:
             pipeline=-1 if self.pipelined is None else int(bool(self.pipelined)),
             window=-1 if self.window is None else int(self.window),
             xcd_skew=XCD_SKEW_AUTO if self.xcd_skew is None else int(self.xcd_skew),
+            segment_bytes=int(self.segment_bytes),
         )
 
 

@@ -210,8 +210,9 @@ def test_late_xcd_anchor_poisons_and_reports(dt, single_pass):
     exp = x.sum().item()
     red = Reducer(dev)
     out = torch.zeros(1, dtype=default_acc_dtype(dt, "sum"), device=dev)
+    # (208 MB is only ~25 rounds per workgroup: the default 20 permille rounds to no skew, so ask for 100)
     plan = _launch(C, red, x, out, single_pass=single_pass, fanin_bound_ticks=1 * TICKS_PER_MS,
-                   debug_delay_anchor_ticks=20 * TICKS_PER_MS)
+                   debug_delay_anchor_ticks=20 * TICKS_PER_MS, xcd_skew=100)
     assert plan["xskew"] != 0 and plan["window"] == 4, plan
     torch.cuda.synchronize()
     word = red.ws.error()
@@ -220,7 +221,7 @@ def test_late_xcd_anchor_poisons_and_reports(dt, single_pass):
     assert (math.isnan(got) if dt.is_floating_point else got == 0), got  # never a plausible wrong sum
     msg = red.check()
     assert msg is not None and "XCD anchor" in msg, msg
-    _launch(C, red, x, out, single_pass=single_pass)
+    _launch(C, red, x, out, single_pass=single_pass, xcd_skew=100)
     torch.cuda.synchronize()
     assert red.check() is None
     got = out.item()

@@ -494,3 +494,76 @@ def test_xcd_weighted_split_follows_the_xccs(monkeypatch, permille, stream, sing
         assert len(fav) == len(other) == grid // 2, (len(fav), len(other))
         assert int(fav.min()) > int(other.max()), (fav.tolist()[:8], other.tolist()[:8])
         assert int(v[:, 2].sum()) == n // 2 // (plan["block"] * plan["unroll"])  # every full tile once
+
+
+# ---------------------------------------------------------------- segmented launches (round 5)
+
+@pytest.mark.parametrize("dt,op,acc", [(torch.float64, "sum", torch.float64), (torch.float64, "min", torch.float64),
+                                       (torch.int64, "sum", torch.int64), (torch.int32, "sum", torch.int64),
+                                       (torch.float32, "max", torch.float32), (torch.int64, "max", torch.int64)],
+                         ids=lambda v: str(v).replace("torch.", ""))
+@pytest.mark.parametrize("misalign", [0, 1])
+def test_segmented_launches_match_the_reference(dt, op, acc, misalign):
+    # A reduction split into consecutive launches (ReduceConfig::segment_bytes; auto above 16 GiB):
+    # every earlier segment's result is carried into the last launch's finisher. Forced here onto a
+    # 320 MB array in 8 MiB segments (~38 launches), through reduce() and through a bound launch,
+    # on an odd count at an odd offset so segment edges cut vectors and tiles.
+    n = 40_000_003
+    base = torch.empty(n + misalign, dtype=dt, device=DEV)
+    fill_(base, "fullrange" if not dt.is_floating_point else "uniform", seed=91 + misalign)
+    x = base[misalign:]
+    red = Reducer(DEV, config=KernelConfig(segment_bytes=8 << 20))
+    out = red(x, op, acc)
+    plan = red.last_plan
+    assert plan["segments"] > 30 and plan["segment_elems"] * plan["segments"] >= n, plan
+    check(out.item(), x, op, acc, n)
+    b = red.bind(x, op, acc)
+    slot = torch.zeros(4, dtype=acc, device=DEV)
+    for i in range(4):  # back-to-back: carried results are rewritten by every launch
+        b.launch(torch.cuda.current_stream().cuda_stream, slot[i:i + 1].data_ptr())
+    torch.cuda.synchronize()
+    assert red.check() is None
+    for v in slot.tolist():
+        check(v, x, op, acc, n)
+
+
+def test_segmented_launch_with_fused_finish_world1():
+    # the last segment's launch does the fused cross-rank finish (world 1: bound, exchanges nothing)
+    from cuda_mpi_reductions_amd.parallel.xrank import close_channels, open_channel
+    dev = torch.device(DEV)
+    x = torch.empty(30_000_001, dtype=torch.float64, device=dev)
+    fill_(x, "uniform", seed=5)
+    ch = open_channel(dev, timeout_s=5.0)
+    red = Reducer(dev, config=KernelConfig(segment_bytes=16 << 20))
+    out = torch.zeros(1, dtype=torch.float64, device=dev)
+    b = red.bind(x, "sum", torch.float64, out=out, xrank=ch)
+    assert b.plan["segments"] > 10
+    for _ in range(3):
+        b.launch(torch.cuda.current_stream().cuda_stream, out.data_ptr())
+    torch.cuda.synchronize()
+    assert int(ch.error()) == 0 and red.check() is None
+    check(out.item(), x, "sum", torch.float64, x.numel())
+    del b
+    close_channels([ch], dev)
+
+
+def test_segmented_launch_poisons_on_a_late_workgroup():
+    # a fan-in failure in any segment poisons the final result (the sticky error word reaches the
+    # last segment's finisher) and is reported; the launch after the reset is exact
+    C = native()
+    from cuda_mpi_reductions_amd.ops import dtype_code, op_code
+    dev = torch.device(DEV)
+    x = torch.randint(1, 1 << 20, (20_000_000,), dtype=torch.int64, device=dev)
+    red = Reducer(dev)
+    out = torch.zeros(1, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    plan = C.reduce(red.ws, x.data_ptr(), x.numel(), dtype_code(x.dtype), op_code("sum"), dtype_code(torch.int64),
+                    out.data_ptr(), s, segment_bytes=16 << 20, fanin_bound_ticks=100_000, debug_delay_wg=0,
+                    debug_delay_ticks=5_000_000)
+    torch.cuda.synchronize()
+    assert plan["segments"] > 5 and out.item() == 0 and red.ws.error() & 1
+    assert red.check() is not None
+    C.reduce(red.ws, x.data_ptr(), x.numel(), dtype_code(x.dtype), op_code("sum"), dtype_code(torch.int64),
+             out.data_ptr(), s, segment_bytes=16 << 20)
+    torch.cuda.synchronize()
+    assert red.check() is None and out.item() == x.sum().item()

@@ -186,3 +186,24 @@ def test_env_skew_overrides_only_the_default(monkeypatch):
     assert C.plan(0, 10**9, F64)["xskew"] == 38
     assert C.plan(0, 10**9, F64, xcd_skew=0)["xskew"] == 0
     assert C.plan(0, 10**9, F64, xcd_skew=-20)["xskew"] == -19
+
+
+def test_segmented_launch_plan():
+    # round 5 (profiles/r5_hbmfill/): arrays above 16 GiB run as 8 GiB launches on the polled fan-in;
+    # segment_bytes > 0 forces a size (1 MiB multiples), < 0 one launch; two-pass never segments; at
+    # most min(256, max_grid) carried results (then the segments grow)
+    C = native()
+    F32 = 2
+    hbm = C.plan(0, 73 * 10**9, F32)                      # the HBM-filling fp32 config: 292 GB
+    assert hbm["segments"] == -(-73 * 10**9 // ((8 << 30) // 4)) and hbm["segment_elems"] == (8 << 30) // 4
+    assert C.plan(0, 10**9, F64)["segments"] == 1         # the 8 GB headline: one launch
+    assert C.plan(0, 2 * (8 << 30) // 8, F64)["segments"] == 1   # exactly 16 GiB: still one
+    assert C.plan(0, 2 * (8 << 30) // 8 + 1, F64)["segments"] == 3
+    forced = C.plan(0, 10**9, F64, segment_bytes=3 << 30)  # 8 GB in 3 GiB segments
+    assert forced["segments"] == 3 and forced["segment_elems"] == (3 << 30) // 8
+    assert C.plan(0, 10**9, F64, segment_bytes=(3 << 30) + 12345)["segment_elems"] == (3 << 30) // 8  # MiB-rounded
+    assert C.plan(0, 73 * 10**9, F32, segment_bytes=-1)["segments"] == 1
+    assert C.plan(0, 73 * 10**9, F32, single_pass=False)["segments"] == 1
+    tiny = C.plan(0, 10**9, F64, segment_bytes=1 << 20)    # 7630 x 1 MiB would carry too many: larger segments
+    assert tiny["segments"] <= 257 and tiny["segments"] * tiny["segment_elems"] >= 10**9
+    assert C.plan(0, 10**9, F64, segment_bytes=1 << 20, max_grid=64)["segments"] <= 65

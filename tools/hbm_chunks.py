@@ -9,16 +9,17 @@ ahead — over 292 GB by GBs — and the concurrently read addresses spread over
 8 GB launch cannot drift that far. This tool measures, on ONE array filling most of HBM, in
 interleaved rounds:
 
-* ``whole``: one launch over the whole array (the config as shipped);
-* ``chunk<G>``: the same bytes as back-to-back launches over G-GB slices (each slice a fresh,
-  aligned start for every workgroup), partials folded afterwards — same total work, bounded drift;
+* ``whole``: one launch over the whole array (``segment_bytes=-1``: the round-4 plan);
+* ``seg<G>``: the library's segmented launches (ReduceConfig::segment_bytes = G GiB): the same
+  bytes as back-to-back launches over G-GiB segments, the earlier results carried into the last
+  launch — same total work, bounded drift (``seg8`` is the round-5 default above 16 GiB);
 * ``slice<k>``: one 8 GB launch at the array's start / middle / end (is some region of HBM slower?);
 
 plus the per-workgroup end-time spread of the whole-array launch (ReduceConfig::debug_wg_stamps:
 how far the workgroups drifted apart by the end). All results are checked against the whole-array
 value. GB = 1e9 B.
 
-    python tools/hbm_chunks.py --fraction 0.9 --rounds 3 --chunks 8,32
+    python tools/hbm_chunks.py --fraction 0.9 --rounds 3 --segments 4,8,16
 """
 from __future__ import annotations
 
@@ -42,7 +43,7 @@ def main(argv=None) -> int:
     ap.add_argument("--fraction", type=float, default=0.9, help="of the free HBM to fill")
     ap.add_argument("--dtype", default="float32", choices=("float32", "float64"))
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--chunks", default="8,32", help="chunk sizes in GB (comma list)")
+    ap.add_argument("--segments", default="4,8,16", help="segment sizes in GiB (comma list)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args(argv)
     C = native()
@@ -59,12 +60,13 @@ def main(argv=None) -> int:
     s = torch.cuda.current_stream(dev).cuda_stream
     gb = n * es / 1e9
     print(f"[hbm] {n} {a.dtype} = {gb:.1f} GB", flush=True)
-    chunks = [float(v) for v in a.chunks.split(",") if v]
+    segs = [int(v) for v in a.segments.split(",") if v]
     outs = torch.zeros(4096, dtype=acc, device=dev)
 
     def launch(view, out, **kw):
-        C.reduce(red.ws, view.data_ptr(), view.numel(), dtype_code(dt), op_code("sum"), dtype_code(acc),
-                 out.data_ptr(), s, **kw)
+        kw.setdefault("segment_bytes", -1)
+        return C.reduce(red.ws, view.data_ptr(), view.numel(), dtype_code(dt), op_code("sum"), dtype_code(acc),
+                        out.data_ptr(), s, **kw)
 
     def timed(fn) -> float:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -80,14 +82,6 @@ def main(argv=None) -> int:
     ref = float(outs[0].item())
     tol = 1e-6 * abs(ref) + 1e-3
 
-    def chunked(g):
-        per = int(g * 1e9) // es
-        per -= per % 4096
-        k = (n + per - 1) // per
-        for i in range(k):
-            launch(x[i * per:min(n, (i + 1) * per)], outs[1 + i:2 + i])
-        return k
-
     results = {}
     slice_n = int(8e9) // es
     slices = {"slice_start": 0, "slice_mid": (n // 2) - (n // 2) % 4096, "slice_end": n - slice_n}
@@ -95,11 +89,9 @@ def main(argv=None) -> int:
         t = timed(lambda: launch(x, outs[:1]))
         ok = abs(float(outs[0].item()) - ref) <= tol
         results.setdefault("whole", []).append((gb / t, ok))
-        for g in chunks:
-            kk = {}
-            t = timed(lambda: kk.setdefault("k", chunked(g)))
-            tot = float(outs[1:1 + kk["k"]].double().sum().item())
-            results.setdefault(f"chunk{g:g}", []).append((gb / t, abs(tot - ref) <= tol))
+        for g in segs:
+            t = timed(lambda: launch(x, outs[:1], segment_bytes=g << 30))
+            results.setdefault(f"seg{g}", []).append((gb / t, abs(float(outs[0].item()) - ref) <= tol))
         for name, off in slices.items():
             v = x[off:off + slice_n]
             t = timed(lambda: launch(v, outs[:1]))
@@ -107,8 +99,7 @@ def main(argv=None) -> int:
         launch(x, outs[:1])
     # end-time spread of the whole-array launch's workgroups
     stamps = torch.zeros(3 * red.ws.max_grid, dtype=torch.int64, device=dev)
-    plan = C.reduce(red.ws, x.data_ptr(), n, dtype_code(dt), op_code("sum"), dtype_code(acc), outs.data_ptr(), s,
-                    wg_stamps=stamps.data_ptr())
+    plan = launch(x, outs[:1], wg_stamps=stamps.data_ptr())
     torch.cuda.synchronize(dev)
     g = plan["grid"]
     st = stamps[:3 * g].view(g, 3).cpu()

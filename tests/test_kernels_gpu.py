@@ -506,7 +506,7 @@ def test_xcd_weighted_split_follows_the_xccs(monkeypatch, permille, stream, sing
 def test_segmented_launches_match_the_reference(dt, op, acc, misalign):
     # A reduction split into consecutive launches (ReduceConfig::segment_bytes; auto above 16 GiB):
     # every earlier segment's result is carried into the last launch's finisher. Forced here onto a
-    # 320 MB array in 8 MiB segments (~38 launches), through reduce() and through a bound launch,
+    # 160-320 MB array in 8 MiB segments (20-39 launches), through reduce() and through a bound launch,
     # on an odd count at an odd offset so segment edges cut vectors and tiles.
     n = 40_000_003
     base = torch.empty(n + misalign, dtype=dt, device=DEV)
@@ -515,7 +515,7 @@ def test_segmented_launches_match_the_reference(dt, op, acc, misalign):
     red = Reducer(DEV, config=KernelConfig(segment_bytes=8 << 20))
     out = red(x, op, acc)
     plan = red.last_plan
-    assert plan["segments"] > 30 and plan["segment_elems"] * plan["segments"] >= n, plan
+    assert plan["segments"] >= 19 and plan["segment_elems"] * plan["segments"] >= n, plan  # 160-320 MB / 8 MiB
     check(out.item(), x, op, acc, n)
     b = red.bind(x, op, acc)
     slot = torch.zeros(4, dtype=acc, device=DEV)

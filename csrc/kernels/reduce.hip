@@ -252,11 +252,15 @@ Workspace::Workspace(int device, int max_grid) : max_grid_(max_grid) {
   const size_t tbytes = static_cast<size_t>(kMaxGroups + 1) * kTicketStride * sizeof(unsigned);
   MIREDUCE_HIP_THROW(hipMalloc(reinterpret_cast<void**>(&tickets_), tbytes));
   MIREDUCE_HIP_THROW(hipMemset(tickets_, 0, tbytes));
-  // polled fan-in slots: uncached, so the finisher's polls see every XCD's stores
+  // polled fan-in slots: uncached, so the finisher's polls see every XCD's stores.
+  // MIREDUCE_SLOTS=coarse (A/B runs, tools/launch_floor.hip): ordinary device memory instead, relying
+  // on the agent-scope atomics alone for cross-XCD visibility.
+  const char* sm = std::getenv("MIREDUCE_SLOTS");
+  const unsigned flags = sm && std::strcmp(sm, "coarse") == 0 ? hipDeviceMallocDefault : hipDeviceMallocUncached;
   MIREDUCE_HIP_THROW(hipExtMallocWithFlags(reinterpret_cast<void**>(&slots_), static_cast<size_t>(max_grid) * 16,
-                                           hipDeviceMallocUncached));
+                                           flags));
   MIREDUCE_HIP_THROW(hipMemset(slots_, 0, static_cast<size_t>(max_grid) * 16));
-  MIREDUCE_HIP_THROW(hipExtMallocWithFlags(reinterpret_cast<void**>(&fan_), 256, hipDeviceMallocUncached));
+  MIREDUCE_HIP_THROW(hipExtMallocWithFlags(reinterpret_cast<void**>(&fan_), 256, flags));
   MIREDUCE_HIP_THROW(hipMemset(fan_, 0, 256));
   MIREDUCE_HIP_THROW(hipDeviceSynchronize());
   MIREDUCE_HIP_THROW(hipSetDevice(prev));

@@ -553,7 +553,8 @@ def test_segmented_launch_poisons_on_a_late_workgroup():
     C = native()
     from cuda_mpi_reductions_amd.ops import dtype_code, op_code
     dev = torch.device(DEV)
-    x = torch.randint(1, 1 << 20, (20_000_000,), dtype=torch.int64, device=dev)
+    g = torch.Generator(device="cpu").manual_seed(31)  # (CPU RNG: an earlier graph capture may own the GPU's)
+    x = torch.randint(1, 1 << 20, (20_000_000,), generator=g, dtype=torch.int64).to(dev)
     red = Reducer(dev)
     out = torch.zeros(1, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream().cuda_stream

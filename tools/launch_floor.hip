@@ -6,9 +6,11 @@
 //   args1                  one workgroup that reads the production kernel's Args (by value, ~200 B
 //                          of kernarg) and stores one word: + the kernarg fetch;
 //   poll768                768 workgroups that each publish a tagged slot and a finisher that polls
-//                          them (the production fan-in alone, no data);
+//                          them (the production fan-in alone, no data); _coarse: the words in
+//                          ordinary device memory instead of uncached;
 //   reduce_<n>             the production kern::reduce_stream (tuned plan, polled fan-in) over n
-//                          doubles, its result checked against a host sum.
+//                          doubles, its result checked against a host sum (_coarse: on a Workspace
+//                          made with MIREDUCE_SLOTS=coarse).
 //   build: make launch_floor     run: build/bin/launch_floor [--rounds=7] [--launches=200]
 #include <hip/hip_runtime.h>
 
@@ -104,6 +106,9 @@ int main(int argc, char** argv) {
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   Workspace ws(0, 16384);
+  setenv("MIREDUCE_SLOTS", "coarse", 1);  // the A/B workspace: fan-in words in ordinary device memory
+  Workspace ws_coarse(0, 16384);
+  unsetenv("MIREDUCE_SLOTS");
   const std::vector<uint64_t> sizes = {1024, 1ull << 24, 125000000};
   const uint64_t nmax = sizes.back();
   double* x = nullptr;
@@ -122,6 +127,12 @@ int main(int argc, char** argv) {
   uint64_t* pslots = nullptr;
   CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&pslots), 16384 * 8, hipDeviceMallocUncached));
   CK(hipMemset(pslots, 0, 16384 * 8));
+  unsigned* cfan = nullptr;
+  uint64_t* cslots = nullptr;
+  CK(hipMalloc(&cfan, 64));
+  CK(hipMemset(cfan, 0, 64));
+  CK(hipMalloc(&cslots, 16384 * 8));
+  CK(hipMemset(cslots, 0, 16384 * 8));
   kern::Args dummy{};
   dummy.out = scratch;
 
@@ -137,11 +148,17 @@ int main(int argc, char** argv) {
   vars.push_back({"poll768", [&](hipStream_t st) {
                     hipLaunchKernelGGL(poll_kernel, dim3(768), dim3(256), 0, st, pslots, pfan, scratch);
                   }, 0});
+  vars.push_back({"poll768_coarse", [&](hipStream_t st) {
+                    hipLaunchKernelGGL(poll_kernel, dim3(768), dim3(256), 0, st, cslots, cfan, scratch);
+                  }, 0});
+  const size_t fixed = vars.size();
   std::vector<std::unique_ptr<BoundReduce>> bound;
   for (uint64_t n : sizes) {
-    bound.emplace_back(new BoundReduce(x, n, DType::Float64, Op::Sum, DType::Float64, out, ws));
-    BoundReduce* b = bound.back().get();
-    vars.push_back({"reduce_" + std::to_string(n), [b](hipStream_t st) { b->launch(st); }, n});
+    for (int coarse = 0; coarse < 2; ++coarse) {
+      bound.emplace_back(new BoundReduce(x, n, DType::Float64, Op::Sum, DType::Float64, out, coarse ? ws_coarse : ws));
+      BoundReduce* b = bound.back().get();
+      vars.push_back({"reduce_" + std::to_string(n) + (coarse ? "_coarse" : ""), [b](hipStream_t st) { b->launch(st); }, n});
+    }
   }
   std::vector<std::vector<double>> us(vars.size());
   std::vector<size_t> order(vars.size());
@@ -170,13 +187,13 @@ int main(int argc, char** argv) {
     std::sort(v.begin(), v.end());
     std::string plan;
     if (vars[k].n) {
-      const LaunchPlan& p = bound[k - 4]->plan();
+      const LaunchPlan& p = bound[k - fixed]->plan();
       plan = std::to_string(p.block) + "x" + std::to_string(p.unroll) + " grid " + std::to_string(p.grid) +
              " window " + std::to_string(p.window) + " xskew " + std::to_string(p.xskew);
     }
     std::printf("%-14s %10.3f %10.3f  %s\n", vars[k].name.c_str(), v[v.size() / 2], v.front(), plan.c_str());
   }
-  unsigned err = ws.error();
+  unsigned err = ws.error() | ws_coarse.error();
   std::printf("fan-in error word %u, results %s\n", err, ok ? "verified" : "WRONG");
   return ok && err == 0 ? 0 : 1;
 }

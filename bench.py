@@ -1233,7 +1233,7 @@ def _topology(ctx) -> dict:
                            (pm.error or "every pair of GPUs")}
 
 
-HEADLINE_RESERVE_S = 40.0  # run budget kept after the headline phase (extras window, teardown)
+HEADLINE_RESERVE_S = 25.0  # run budget kept after the headline phase (teardown; the extras fit or are skipped)
 EXTRAS_RESERVE_S = 25.0  # run budget kept after the extras (teardown, the parent's grace)
 EXTRAS_MIN_S = 15.0  # an extras window shorter than this is skipped (agreed over ranks)
 NONROOT_GRACE_S = 10.0  # non-root ranks' headline deadline is this much later than rank 0's
@@ -1454,8 +1454,9 @@ def main(argv=None) -> int:
     # (direct collective first: no RCCL), then the RCCL step candidates, so a hang costs the fewest
     # extras; the watchdog prints the line with the summary of what has completed. Extras that no
     # longer fit in the run budget are skipped (agreed over ranks).
-    extras_deadline = _deadline(args, args.extras_deadline, EXTRAS_RESERVE_S, floor=0.0)
-    do_extras = -pdist.max_over_ranks(-float(extras_deadline >= EXTRAS_MIN_S), ctx) > 0.5  # AND over ranks
+    room = _budget_left(args) - EXTRAS_RESERVE_S  # what the run budget leaves for the extras
+    extras_deadline = max(0.01, min(args.extras_deadline, room))
+    do_extras = -pdist.max_over_ranks(-float(room >= EXTRAS_MIN_S), ctx) > 0.5  # AND over ranks
     extras = record.extras if record is not None else {}
     guard = _ExtrasWatchdog(record, max(extras_deadline, 1.0), rc)
 

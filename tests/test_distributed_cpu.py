@@ -344,3 +344,19 @@ def test_bench_maxloc_config_two_cpu_ranks(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["verified"] is True and d["config"]["op"] == "MAXLOC" and d["n_gpus"] == 2
+
+
+def test_bench_budget_too_small_for_extras_skips_them(tmp_path):
+    # every deadline is cut to the run budget; when the headline (slowed by an
+    # injected 8 s straggler) leaves less than the extras' minimum window, the extras are skipped on
+    # every rank (agreed) and the line says so
+    side = tmp_path / "x.json"
+    r = torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "3", "--warmup", "1",
+                     "--elements", "200003", "--budget", "45", "--inject-fault", "delay=8000@0:1",
+                     "--extras-file", str(side)], cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["verified"] is True and "run budget" in d["summary"]["extras_skipped"], d["summary"]
+    assert "decomposition" not in json.loads(side.read_text())

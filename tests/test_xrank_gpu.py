@@ -367,8 +367,10 @@ def test_bench_extras_deadline_keeps_the_headline(tmp_path):
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = _json(r)
-    assert d["verified"] is True and "did not finish" in d["reduce_c_vector"]["error"]
-    assert "did not finish" in d["summary"]["extras_error"]
+    assert d["verified"] is True and "did not finish" in d["summary"]["extras_error"]
+    assert "extras_skipped" not in d["summary"]  # an explicit short deadline cuts the extras, not skips them
+    if "reduce_c_vector" in d:  # (the deadline may pass before the table starts)
+        assert "did not finish" in d["reduce_c_vector"]["error"]
 
 
 def test_bench_extras_hang_in_rccl_candidate_keeps_the_headline(tmp_path, monkeypatch):

@@ -1458,7 +1458,8 @@ def main(argv=None) -> int:
     extras_deadline = max(0.01, min(args.extras_deadline, room))
     do_extras = -pdist.max_over_ranks(-float(room >= EXTRAS_MIN_S), ctx) > 0.5  # AND over ranks
     extras = record.extras if record is not None else {}
-    guard = _ExtrasWatchdog(record, max(extras_deadline, 1.0), rc)
+    # (skipped extras run nothing: their guard only covers writing the record)
+    guard = _ExtrasWatchdog(record, extras_deadline if do_extras else 10.0, rc)
 
     def rearm() -> None:  # the finished headline + the extras so far, should the process be killed now
         if record is not None:

@@ -41,9 +41,15 @@ TICKS_PER_US = 100.0  # gfx950 wall clock: 100 MHz
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--fraction", type=float, default=0.9, help="of the free HBM to fill")
+    ap.add_argument("--elements", type=float, default=0, help="array size in elements (overrides --fraction)")
+    ap.add_argument("--slices", action=argparse.BooleanOptionalAction, default=True,
+                    help="also time 8 GB slices at the start / middle / end")
+    ap.add_argument("--stamps", action=argparse.BooleanOptionalAction, default=True,
+                    help="also read the whole-array launch's per-workgroup end stamps")
     ap.add_argument("--dtype", default="float32", choices=("float32", "float64"))
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--segments", default="4,8,16", help="segment sizes in GiB (comma list)")
+    ap.add_argument("--segments", default="4,8,16", help="segment sizes in GiB (comma list; fractions allowed)")
+    ap.add_argument("--reps", type=int, default=1, help="back-to-back reductions per timed sample")
     ap.add_argument("--json", default=None)
     a = ap.parse_args(argv)
     C = native()
@@ -51,8 +57,9 @@ def main(argv=None) -> int:
     dt = getattr(torch, a.dtype)
     es = torch.empty(0, dtype=dt).element_size()
     free, _ = torch.cuda.mem_get_info(dev)
-    n = int(free * a.fraction) // es
-    n -= n % 4096
+    n = int(a.elements) if a.elements else int(free * a.fraction) // es
+    if not a.elements:
+        n -= n % 4096
     x = torch.empty(n, dtype=dt, device=dev)
     fill_(x, "uniform", seed=5)
     acc = default_acc_dtype(dt, "sum")
@@ -60,7 +67,7 @@ def main(argv=None) -> int:
     s = torch.cuda.current_stream(dev).cuda_stream
     gb = n * es / 1e9
     print(f"[hbm] {n} {a.dtype} = {gb:.1f} GB", flush=True)
-    segs = [int(v) for v in a.segments.split(",") if v]
+    segs = [float(v) for v in a.segments.split(",") if v]
     outs = torch.zeros(4096, dtype=acc, device=dev)
 
     def launch(view, out, **kw):
@@ -84,19 +91,24 @@ def main(argv=None) -> int:
 
     results = {}
     slice_n = int(8e9) // es
-    slices = {"slice_start": 0, "slice_mid": (n // 2) - (n // 2) % 4096, "slice_end": n - slice_n}
+    slices = {"slice_start": 0, "slice_mid": (n // 2) - (n // 2) % 4096, "slice_end": n - slice_n} \
+        if a.slices and n >= 2 * slice_n else {}
     for r in range(a.rounds):
-        t = timed(lambda: launch(x, outs[:1]))
+        R = a.reps
+        t = timed(lambda: [launch(x, outs[:1]) for _ in range(R)]) / R
         ok = abs(float(outs[0].item()) - ref) <= tol
         results.setdefault("whole", []).append((gb / t, ok))
         for g in segs:
-            t = timed(lambda: launch(x, outs[:1], segment_bytes=g << 30))
-            results.setdefault(f"seg{g}", []).append((gb / t, abs(float(outs[0].item()) - ref) <= tol))
+            t = timed(lambda: [launch(x, outs[:1], segment_bytes=int(g * (1 << 30))) for _ in range(R)]) / R
+            results.setdefault(f"seg{g:g}", []).append((gb / t, abs(float(outs[0].item()) - ref) <= tol))
         for name, off in slices.items():
             v = x[off:off + slice_n]
             t = timed(lambda: launch(v, outs[:1]))
             results.setdefault(name, []).append((slice_n * es / 1e9 / t, True))
         launch(x, outs[:1])
+    spread, by_xcc, plan = {}, {}, None
+    if not a.stamps:
+        return _report(a, n, gb, plan, results, spread, by_xcc)
     # end-time spread of the whole-array launch's workgroups
     stamps = torch.zeros(3 * red.ws.max_grid, dtype=torch.int64, device=dev)
     plan = launch(x, outs[:1], wg_stamps=stamps.data_ptr())
@@ -110,14 +122,19 @@ def main(argv=None) -> int:
     for xcc in sorted(set(st[:, 1].tolist())):
         m = st[:, 1] == xcc
         by_xcc[int(xcc)] = round(float(ends[m].mean()), 1)
+    return _report(a, n, gb, plan, results, spread, by_xcc)
+
+
+def _report(a, n, gb, plan, results, spread, by_xcc) -> int:
     out = {"n": n, "dtype": a.dtype, "gb": round(gb, 2), "plan": plan, "rounds": a.rounds,
            "gbps": {k: [round(v, 1) for v, _ in vs] for k, vs in results.items()},
            "verified": all(ok for vs in results.values() for _, ok in vs),
            "wg_end_spread_us": spread, "wg_end_mean_by_xcc_us": by_xcc}
     for k, vs in results.items():
         print(f"[hbm] {k:12s} GB/s {' '.join('%.1f' % v for v, _ in vs)}  verified {all(ok for _, ok in vs)}")
-    print(f"[hbm] whole-array workgroup end spread (us after the first): p50 {spread['p50']:.0f} "
-          f"p99 {spread['p99']:.0f} max {spread['max']:.0f}; mean by XCC {by_xcc}")
+    if spread:
+        print(f"[hbm] whole-array workgroup end spread (us after the first): p50 {spread['p50']:.0f} "
+              f"p99 {spread['p99']:.0f} max {spread['max']:.0f}; mean by XCC {by_xcc}")
     if a.json:
         with open(a.json, "a") as f:
             f.write(json.dumps(out) + "\n")

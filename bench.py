@@ -994,9 +994,11 @@ class _Record:
     row per measurement (mpi/reduce.c:81,95)."""
 
     def __init__(self, line: dict, detail: dict, path: str):
+        import threading
         self.line, self.detail, self.path = line, detail, path
         self.extras: dict = {}
         self.run = f"{int(time.time() * 1e3):x}-{os.getpid():x}"
+        self._lock = threading.Lock()  # the extras watchdog's thread may write while the main thread does
 
     def _snapshot(self) -> dict:
         for _ in range(5):  # the extras may be mid-update in the main thread: snapshot via JSON
@@ -1020,11 +1022,12 @@ class _Record:
         out = dict(self.line)
         out["summary"] = summary
         try:
-            os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
-            tmp = f"{self.path}.{os.getpid()}.tmp"
-            with open(tmp, "w") as f:
-                json.dump({**out, **self.detail, **ex}, f, indent=1)
-            os.replace(tmp, self.path)
+            with self._lock:
+                os.makedirs(os.path.dirname(self.path) or ".", exist_ok=True)
+                tmp = f"{self.path}.{os.getpid()}.tmp"
+                with open(tmp, "w") as f:
+                    json.dump({**out, **self.detail, **ex}, f, indent=1)
+                os.replace(tmp, self.path)
         except OSError as e:
             summary["extras_file"] = None
             summary["extras_file_error"] = f"{type(e).__name__}: {e}"[:160]

@@ -1202,6 +1202,12 @@ def _tune_plan(wl, ctx, args, fault, kernel, cands) -> "tuple[KernelConfig, dict
             g = round(local_bytes * T / mt["elapsed_local"] / 1e9, 3)
             res[key] = -1.0 if wl.check() is not None else max(res.get(key, 0.0), g)
     best = max(res, key=res.get)
+    # test hook (tests/test_xrank_gpu.py): MIREDUCE_PLAN_FOR_RANK="1=tuned default, XCD skew 0;..." makes
+    # the named ranks hold another candidate, so a heterogeneous job is exercised deterministically
+    for item in filter(None, os.environ.get("MIREDUCE_PLAN_FOR_RANK", "").split(";")):
+        r, _, key = item.partition("=")
+        if r.strip() == str(ctx.rank) and any(_plan_key(c) == key for c in cands) and res.get(key, 0.0) >= 0:
+            best = key
     b, u, w, win, skew = next(c for c in cands if _plan_key(c) == best)
     kernel = replace(kernel, block=b, unroll=u, wg_per_cu=w, window=None if win < 0 else win, xcd_skew=skew)
     wl.use_kernel(kernel, streams=1)  # (collective: every rank re-binds, each with its own plan)

@@ -66,6 +66,7 @@ struct Options {
   bool cold = false;          // flush L2 + Infinity Cache before every timed iteration
   int unroll = 0;
   int window = -1;  // streaming body's load window: -1 tuned, 0 hipcc's schedule, 2 | 4
+  int64_t segment_bytes = 0;  // segmented launches: 0 auto (8 GiB above 16 GiB), < 0 one launch, > 0 size
   int wg_per_cu = 0;
   int policy = -1;
   Pattern pattern = Pattern::SmallInt;  // rand() & 0xFF (reduction.cpp:698-705)
@@ -80,6 +81,7 @@ struct Options {
 const std::set<std::string> kKnown = {
     "method", "type", "n", "threads", "kernel", "maxblocks", "cpufinal", "cputhresh", "shmoo",
     "device", "qatest", "noprompt", "prompt", "help", "version", "quiet", "iterations", "acc", "unroll", "window",
+    "segment-bytes",
     "wg-per-cu", "policy", "pattern", "seed", "fill", "noverify", "json", "log", "master-log",
     "countdown", "shmoo-max", "trace", "timing", "cold", "arg"};
 
@@ -100,6 +102,7 @@ void usage() {
       "                   256 MB Infinity Cache and the L2s): HBM numbers for small arrays; per-iter timing\n"
       "  --iterations=100 --acc=TYPE --unroll=2|4|8 --wg-per-cu=N --policy=auto|nt|default\n"
       "  --window=0|2|4   streaming body: hipcc's load schedule (0) or an explicit window (default: tuned)\n"
+      "  --segment-bytes=N  arrays above 16 GiB run as 8 GiB launches (0, default); -1 one launch; N bytes\n"
       "  --pattern=smallint|uniform|fullrange|iotamod --seed=N --fill=host|device --noverify\n"
       "  --device=N --json=PATH --log=FILE|none --master-log=FILE|none (default SdkMasterLog.csv) --qatest\n"
       "  --prompt --countdown\n"
@@ -166,6 +169,7 @@ struct Runner {
     c.block = o.threads;
     c.unroll = o.unroll;
     c.window = o.window;
+    c.segment_bytes = o.segment_bytes;
     c.wg_per_cu = o.wg_per_cu;
     c.max_blocks = o.max_blocks;
     c.policy = o.policy;
@@ -593,6 +597,7 @@ int main(int argc, char** argv) {
     o.iterations = args.int_or<int>("iterations", o.iterations);
     o.unroll = args.int_or<int>("unroll", o.unroll);
     o.window = args.int_or<int>("window", o.window);
+    o.segment_bytes = args.int_or<int64_t>("segment-bytes", o.segment_bytes);
     o.wg_per_cu = args.int_or<int>("wg-per-cu", o.wg_per_cu);
     {
       const std::string pol = args.str_or("policy", "auto");

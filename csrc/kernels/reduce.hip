@@ -428,10 +428,12 @@ static Segments plan_segments(size_t n, size_t es, const ReduceConfig& cfg, cons
   const uint64_t quantum = kMiB / es;  // segments start on 1 MiB boundaries of the array
   uint64_t elems = std::max<uint64_t>(1, want / kMiB) * quantum;
   uint64_t count = (n + elems - 1) / elems;
-  if (count > static_cast<uint64_t>(max_carry) + 1) {  // fewer, larger segments
-    elems = ((n + max_carry) / (static_cast<uint64_t>(max_carry) + 1) + quantum - 1) / quantum * quantum;
-    count = (n + elems - 1) / elems;
-  }
+  if (count > static_cast<uint64_t>(max_carry) + 1) count = static_cast<uint64_t>(max_carry) + 1;  // larger ones
+  if (count <= 1) return sg;
+  // equal segments (whole MiB each, the last one the rest): no short tail segment, so the last launch
+  // — whose finisher folds the carried results — always has a multi-workgroup polled plan
+  elems = ((n + count - 1) / count + quantum - 1) / quantum * quantum;
+  count = (n + elems - 1) / elems;
   if (count <= 1) return sg;
   sg.count = static_cast<int>(count);
   sg.elems = elems;
@@ -496,6 +498,9 @@ std::vector<Launch> make_launches(const void* in, size_t n, DType t, Op op, DTyp
     v.push_back(make_launch(ink, nk, t, op, c, last ? out : carry + k * as, ws, cfg, last ? cfg.xrank : nullptr,
                             last ? carry : nullptr, last ? static_cast<unsigned>(sg.count - 1) : 0u));
   }
+  // the carried results are folded by the last launch's polled finisher only
+  MIREDUCE_REQUIRE(v.back().plan.poll && v.back().plan.grid > 1, "segmented reduction: the last segment's plan "
+                   "has no polled multi-workgroup fan-in (segment too small)");
   v[0].plan.segments = sg.count;
   v[0].plan.segment_elems = sg.elems;
   return v;

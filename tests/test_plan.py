@@ -195,13 +195,17 @@ def test_segmented_launch_plan():
     C = native()
     F32 = 2
     hbm = C.plan(0, 73 * 10**9, F32)                      # the HBM-filling fp32 config: 292 GB
-    assert hbm["segments"] == -(-73 * 10**9 // ((8 << 30) // 4)) and hbm["segment_elems"] == (8 << 30) // 4
+    assert hbm["segments"] == -(-73 * 10**9 // ((8 << 30) // 4)) == 34
+    # equal whole-MiB segments of at most 8 GiB (no short tail segment)
+    e = hbm["segment_elems"]
+    assert e <= (8 << 30) // 4 and (e * 4) % (1 << 20) == 0 and 73 * 10**9 - 33 * e > 0.99 * e
     assert C.plan(0, 10**9, F64)["segments"] == 1         # the 8 GB headline: one launch
     assert C.plan(0, 2 * (8 << 30) // 8, F64)["segments"] == 1   # exactly 16 GiB: still one
     assert C.plan(0, 2 * (8 << 30) // 8 + 1, F64)["segments"] == 3
-    forced = C.plan(0, 10**9, F64, segment_bytes=3 << 30)  # 8 GB in 3 GiB segments
-    assert forced["segments"] == 3 and forced["segment_elems"] == (3 << 30) // 8
-    assert C.plan(0, 10**9, F64, segment_bytes=(3 << 30) + 12345)["segment_elems"] == (3 << 30) // 8  # MiB-rounded
+    forced = C.plan(0, 10**9, F64, segment_bytes=3 << 30)  # 8 GB in (at most) 3 GiB segments: 3 equal ones
+    assert forced["segments"] == 3 and forced["segment_elems"] <= (3 << 30) // 8
+    assert (forced["segment_elems"] * 8) % (1 << 20) == 0 and forced["segment_elems"] * 3 >= 10**9
+    assert C.plan(0, 10**9, F64, segment_bytes=(3 << 30) + 12345)["segment_elems"] == forced["segment_elems"]
     assert C.plan(0, 73 * 10**9, F32, segment_bytes=-1)["segments"] == 1
     assert C.plan(0, 73 * 10**9, F32, single_pass=False)["segments"] == 1
     tiny = C.plan(0, 10**9, F64, segment_bytes=1 << 20)    # 7630 x 1 MiB would carry too many: larger segments

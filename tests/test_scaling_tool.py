@@ -156,7 +156,10 @@ def test_compact_lines_merge_their_sidecars(tmp_path):
     lines = []
     for n, run in ((1, "r1"), (8, "r8")):
         ln = _line(n, 7300.0 * n * (0.95 if n > 1 else 1), 8.0 / (7.3 * n))
-        ln["summary"] = {"run": run, "extras_file": f"/elsewhere/bench_extras_n{n}.json"}
+        ln["summary"] = {"run": run, "extras_file": f"/elsewhere/bench_extras_n{n}.json",
+                         "plans": "0-7: tuned default" if n == 8 else "0: tuned default"}
+        ln["verified"] = True
+        ln["config"]["collective"] = "fused"
         full = dict(ln)
         full["decomposition"] = {"local_ms_per_step": 0.14 if n == 8 else 1.09, "exchange_us_per_step": 4.0,
                                  "skew_us_per_step": 1.0, "scaling_efficiency_vs_local": 0.97}
@@ -177,3 +180,4 @@ def test_compact_lines_merge_their_sidecars(tmp_path):
     row8 = [ln for ln in (out / "scaling.md").read_text().splitlines() if "| 8 |" in ln]
     cells = [c.strip() for c in row8[0].strip("|").split("|")] if len(row8) == 1 else []
     assert cells[8] == "1" and cells[9] == "0.1400", row8  # one run (line + sidecar), local ms merged
+    assert cells[-3:] == ["fused", "yes", "0-7: tuned default"], row8  # combine, verified, per-rank plans

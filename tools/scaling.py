@@ -137,7 +137,11 @@ def summarise(results):
         for n, rs in sorted(per_n.items()):
             ms = [float(r["ms_per_step"]) for r in rs if r.get("ms_per_step") is not None]
             out[k][n] = {"gbps": sum(float(r["value"]) for r in rs) / len(rs),
-                         "ms": sum(ms) / len(ms) if ms else None, "runs": len(rs)}
+                         "ms": sum(ms) / len(ms) if ms else None, "runs": len(rs),
+                         "verified": all(r.get("verified") is not False for r in rs),
+                         "combine": "/".join(sorted({str((r.get("config") or {}).get("collective", "")) for r in rs})),
+                         "plans": "; ".join(sorted({str((r.get("summary") or {}).get("plans"))
+                                                     for r in rs if (r.get("summary") or {}).get("plans")}))}
             out[k][n].update(_decomposition(rs))
     return out
 
@@ -229,8 +233,9 @@ def efficiency(per_n):
 def write(summary, out_dir):
     os.makedirs(out_dir, exist_ok=True)
     md = ["| config | dtype | op | N | GB/s (whole node) | ms/step | speed-up | efficiency | runs "
-          "| local ms/step | exchange us/step | skew us/step | vs local | fused wait us (min-max rank) |",
-          "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
+          "| local ms/step | exchange us/step | skew us/step | vs local | fused wait us (min-max rank) "
+          "| combine | verified | plans (per rank) |",
+          "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for (model, dt, op), per_n in sorted(summary.items()):
         with open(os.path.join(out_dir, f"{dt}_{op}.txt"), "w") as f:
             f.write("\n")  # getAvgs.sh:5-6 starts each results file with a blank line
@@ -246,7 +251,8 @@ def write(summary, out_dir):
                    (("local_ms", "%.4f"), ("exchange_us", "%.2f"), ("skew_us", "%.2f"), ("vs_local", "%.3f"))]
             wait = "" if v.get("wait_min_us") is None else "%.2f-%.2f" % (v["wait_min_us"], v["wait_max_us"])
             md.append(f"| {model} | {dt} | {op} | {n} | {v['gbps']:.1f} | {ms} | {sp} | {ef} | {v['runs']} | "
-                      + " | ".join(dec) + f" | {wait} |")
+                      + " | ".join(dec) + f" | {wait} | {v.get('combine', '')} | "
+                      + ("yes" if v.get("verified", True) else "**NO**") + f" | {v.get('plans', '')} |")
     text = "\n".join(md) + "\n"
     with open(os.path.join(out_dir, "scaling.md"), "w") as f:
         f.write(text)

@@ -1356,26 +1356,49 @@ def main(argv=None) -> int:
             at_stage("plan tuning")
             kernel, plan_tuning = _tune_plan(wl, ctx, args, fault, kernel, cands)
 
-    at_stage("timed steps")
-    slots = wl.new_slots(W + K)
-    m = _measure(wl, slots, ctx, args, fault, serial=not args.pipelined, warmup=W)
+    def timed(label: str) -> tuple:
+        """The K timed steps, the device error words and the verification of every slot written."""
+        at_stage(label)
+        slots = wl.new_slots(W + K)
+        m = _measure(wl, slots, ctx, args, fault, serial=not args.pipelined, warmup=W)
+        err = wl.check()  # device error words (fan-in, fused finish), agreed over ranks
+        seen = _ranks_seen(ctx)
+        if seen != ctx.world_size:
+            err = (err + "; " if err else "") + f"the process group joined {seen} ranks, not {ctx.world_size}"
+        at_stage("verification")
+        verified, ref = None, None
+        if not args.no_verify:
+            ok, ref = _verify_slots(wl, slots[:m["written"]], ctx)
+            verified = ok and err is None
+            if not verified and ctx.is_root:
+                print(f"[bench] VERIFICATION FAILED: {ref or ''} {err or ''}", file=sys.stderr)
+        elif err is not None:
+            verified = False
+        if err is not None and ctx.is_root:
+            print(f"[bench] device error: {err}", file=sys.stderr)
+        return m, err, seen, verified, ref
+
+    m, err, seen, verified, ref = timed("timed steps")
+    fused_failed = None
+    if verified is False and args.collective == "auto" and collective == "fused" and ctx.world_size > 1:
+        # The fused finish passed its canary and self-check but failed on the headline's own steps:
+        # the number is re-measured over RCCL (same data, same plan) if the run budget has room, and
+        # the sidecar keeps why. Agreed over ranks (the verdict and the budget check both are).
+        fused_failed = (f"fused finish failed on the headline steps ({err or 'wrong result: ' + str(ref)[:120]}); "
+                        "re-measured over RCCL")[:300]
+        room = _budget_left(args) - HEADLINE_RESERVE_S - 30.0
+        if -pdist.max_over_ranks(-float(room > 0), ctx) > 0.5:
+            if ctx.is_root:
+                print(f"[bench] {fused_failed}", file=sys.stderr)
+            wl.use_collective("rccl", streams=lanes)
+            collective, collective_note = "rccl", fused_failed
+            m, err, seen, verified, ref = timed("timed steps (RCCL after the fused finish failed)")
+        else:
+            fused_failed += " — no run budget left for it"
+            if ctx.is_root:
+                print(f"[bench] {fused_failed}", file=sys.stderr)
     m_lanes = len(wl.lanes) if wl.lanes else 1
     m_issues = wl.issues_collective
-    err = wl.check()  # device error words (fan-in, fused finish), agreed over ranks
-    seen = _ranks_seen(ctx)
-    if seen != ctx.world_size:
-        err = (err + "; " if err else "") + f"the process group joined {seen} ranks, not {ctx.world_size}"
-    at_stage("verification")
-    verified = None
-    if not args.no_verify:
-        ok, ref = _verify_slots(wl, slots[:m["written"]], ctx)
-        verified = ok and err is None
-        if not verified and ctx.is_root:
-            print(f"[bench] VERIFICATION FAILED: {ref or ''} {err or ''}", file=sys.stderr)
-    elif err is not None:
-        verified = False
-    if err is not None and ctx.is_root:
-        print(f"[bench] device error: {err}", file=sys.stderr)
 
     gbps = _gbps(wl, K, m["elapsed"])
     ms = m["elapsed"] / K * 1e3
@@ -1428,7 +1451,8 @@ def main(argv=None) -> int:
             line["device_error"] = err[:300]
         detail = {
             "config_detail": {
-                "collective_choice": ("auto: fused finish passed its self-check on every rank"
+                "collective_choice": (f"auto: {fused_failed}" if fused_failed else
+                                      "auto: fused finish passed its self-check on every rank"
                                       if args.collective == "auto" and collective == "fused" else
                                       f"auto; fused unavailable: {collective_note}" if collective_note else
                                       "auto" if args.collective == "auto" else "explicit (--collective)"),

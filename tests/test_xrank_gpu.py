@@ -311,6 +311,21 @@ def test_bench_fused_corrupt_rank_fails_verification(tmp_path, monkeypatch):
     assert d["verified"] is False
 
 
+def test_bench_auto_remeasures_over_rccl_when_fused_fails_the_headline(tmp_path, monkeypatch):
+    # --collective auto: the fused finish passes its canary and self-check, then rank 1's result is
+    # wrong on a timed step (the injected fault fires once). The headline is re-measured over the
+    # process group's all-reduce, verifies, and the sidecar says why.
+    monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    r = torchrun(2, [BENCH, "--no-vector-extras", "--gpus", "2", "--backend", "gloo", "--steps", "6",
+                     "--warmup", "2", "--elements", "20000003", "--inject-fault", "corrupt@1:3"], cwd=tmp_path,
+                 timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "fused finish failed on the headline steps" in r.stderr
+    d = bench_record(r.stdout)
+    assert d["verified"] is True and d["config"]["collective"] == "rccl"
+    assert "fused finish failed on the headline steps" in d["config"]["collective_choice"]
+
+
 # ---------------------------------------------------------------- the N=8 shapes, rehearsed
 # Eight ranks share the one GPU of the test box: the world-8 mailbox indexing of the fused finish,
 # the W=8 instantiation of the direct kernel and bench.py's 8-rank flow (not xGMI speed).

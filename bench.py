@@ -949,6 +949,23 @@ def _collect_verified(obj, out: list) -> list:
     return out
 
 
+def _reduce_c_means(table: list) -> dict:
+    """reduce.c's table as the driver's record can keep it: per impl, one ``"DATATYPE OP GiB/s"``
+    row per collective in reduce.c's order, averaged over the retries the way getAvgs.sh averages
+    each results file (mpi/getAvgs.sh:3-14, reduce.c:71-97); a row with an unverified retry is
+    marked ``!``. NODES is the line's ``n_gpus``."""
+    acc: dict = {}
+    for t in table:
+        if not isinstance(t, dict) or t.get("gibps") is None or "dtype" not in t:
+            continue
+        e = acc.setdefault(t["impl"], {}).setdefault((t["dtype"], t["op"]), [0.0, 0, True])
+        e[0] += float(t["gibps"])
+        e[1] += 1
+        e[2] = e[2] and t.get("verified") is not False
+    return {impl: "; ".join(f"{dt} {op} {tot / n:.3f}" + ("" if ok else "!") for (dt, op), (tot, n, ok) in rows.items())
+            for impl, rows in acc.items()}
+
+
 def _summarise(ex: dict) -> dict:
     """The few extras numbers the printed line carries (the full record is the sidecar)."""
     s = {}
@@ -968,6 +985,9 @@ def _summarise(ex: dict) -> dict:
     v = ex.get("reduce_c_vector")
     if isinstance(v, dict):
         s["reduce_c_gibps"] = {impl: (v.get(f"reduce_{impl}") or {}).get("gibps") for impl in ("direct", "rccl")}
+        means = _reduce_c_means(v.get("table") or [])
+        if means:
+            s["reduce_c_rows"] = means
         if isinstance(v.get("peer_read"), dict):
             s["peer_node_gbps"] = v["peer_read"].get("node_gbps")
     if "torch_gbps" in ex:

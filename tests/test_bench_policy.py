@@ -101,6 +101,24 @@ def test_extras_watchdog_reports_the_extras_completed_so_far(tmp_path):
     assert full["value"] == 1.0 and full["summary"]["run"] == d["summary"]["run"]
 
 
+def test_reduce_c_rows_summary_averages_retries_in_reduce_c_order():
+    # the driver keeps the printed line: reduce.c's table rides in it as getAvgs-style means
+    b = _bench()
+    tab = [{"impl": "direct", "error": "x"}]
+    for x, g in enumerate((1.0, 2.0)):
+        for dt in ("INT", "DOUBLE"):
+            for op in ("MAX", "MIN", "SUM"):
+                tab.append({"retry": x, "dtype": dt, "op": op, "impl": "direct", "gibps": g, "verified": True})
+    tab.append({"dtype": "INT", "op": "SUM", "impl": "rccl", "gibps": None})
+    tab[3]["verified"] = False  # INT SUM, retry 0
+    rows = b._reduce_c_means(tab)
+    assert list(rows) == ["direct"]
+    assert rows["direct"] == ("INT MAX 1.500; INT MIN 1.500; INT SUM 1.500!; "
+                              "DOUBLE MAX 1.500; DOUBLE MIN 1.500; DOUBLE SUM 1.500")
+    s = b._summarise({"reduce_c_vector": {"table": tab, "reduce_direct": {"gibps": 1.5}}})
+    assert s["reduce_c_rows"] == rows and s["reduce_c_gibps"]["direct"] == 1.5
+
+
 class _StubWorkload:
     """Just what bench._selfcheck_slots reads: the op, slot allocation and the channel-free launch."""
 

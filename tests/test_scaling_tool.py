@@ -181,3 +181,23 @@ def test_compact_lines_merge_their_sidecars(tmp_path):
     cells = [c.strip() for c in row8[0].strip("|").split("|")] if len(row8) == 1 else []
     assert cells[8] == "1" and cells[9] == "0.1400", row8  # one run (line + sidecar), local ms merged
     assert cells[-3:] == ["fused", "yes", "0-7: tuned default"], row8  # combine, verified, per-rank plans
+
+
+def test_bare_lines_give_the_vector_table_from_their_summary(tmp_path):
+    # the driver keeps only the printed lines: reduce.c's per-N table comes from summary.reduce_c_rows
+    lines = []
+    for n in (1, 2, 8):
+        ln = _line(n, 7300.0 * n, 8.0 / (7.3 * n))
+        ln["summary"] = {"reduce_c_rows": {"direct": f"INT MAX {10.0 * n:.3f}; DOUBLE SUM {5.0 * n:.3f}!",
+                                           "rccl": f"INT MAX {8.0 * n:.3f}"}}
+        lines.append(json.dumps(ln))
+    src = tmp_path / "scale.jsonl"
+    src.write_text("\n".join(lines) + "\n")
+    v = scaling.summarise_vector(scaling.parse_text(src.read_text()))
+    assert v[("direct", "INT", "MAX")] == {2: {"gibps": 20.0, "runs": 1}, 8: {"gibps": 80.0, "runs": 1}}
+    assert v[("direct", "DOUBLE", "SUM")][8]["gibps"] == 40.0 and v[("rccl", "INT", "MAX")][2]["gibps"] == 16.0
+    out = tmp_path / "res"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling.py"), str(src), "--out", str(out)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert (out / "vector_direct" / "INT_MAX.txt").read_text() == "\nINT MAX 2 20.00000\nINT MAX 8 80.00000\n"

@@ -165,6 +165,19 @@ def _decomposition(rs) -> dict:
     return out
 
 
+def _rows_from_summary(rows) -> list:
+    """bench.py's ``summary.reduce_c_rows`` ({impl: "INT MAX 12.345; ...; DOUBLE SUM 9.876"}, each the
+    mean over the retries, ``!`` = a retry failed verification) as table entries."""
+    out = []
+    for impl, text in (rows or {}).items():
+        for item in str(text).split(";"):
+            parts = item.split()
+            if len(parts) == 3:
+                out.append({"impl": impl, "dtype": parts[0], "op": parts[1], "gibps": float(parts[2].rstrip("!")),
+                            "verified": not parts[2].endswith("!")})
+    return out
+
+
 def summarise_vector(results):
     """{(impl, DT, OP): {N: {"gibps": mean, "runs": k}}} from every result's reduce_c_vector.table
     (one entry per timed collective, RETRY_COUNT per (dtype, op), averaged like getAvgs.sh).
@@ -175,7 +188,10 @@ def summarise_vector(results):
     for r in results:
         if int(r.get("n_gpus", 0)) <= 1:
             continue
-        for row in ((r.get("reduce_c_vector") or {}).get("table") or []):
+        table = (r.get("reduce_c_vector") or {}).get("table")
+        if not table:  # a bare printed line (e.g. the driver's record): its summary's getAvgs-style means
+            table = _rows_from_summary((r.get("summary") or {}).get("reduce_c_rows"))
+        for row in table or []:
             if row.get("gibps") is None:
                 continue
             acc[(row["impl"], row["dtype"], row["op"])][int(r["n_gpus"])].append(float(row["gibps"]))

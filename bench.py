@@ -999,8 +999,12 @@ def _summarise(ex: dict) -> dict:
     return s
 
 
+EXTRAS_DIR_ENV = "MIREDUCE_EXTRAS_DIR"  # where the default sidecar goes (the tests give each run its own)
+
+
 def _default_extras_path(n: int) -> str:
-    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "gpurun_out", f"bench_extras_n{n}.json")
+    d = os.environ.get(EXTRAS_DIR_ENV) or os.path.join(os.path.dirname(os.path.abspath(__file__)), "gpurun_out")
+    return os.path.join(d, f"bench_extras_n{n}.json")
 
 
 class _Record:
@@ -1266,6 +1270,7 @@ HEADLINE_RESERVE_S = 25.0  # run budget kept after the headline phase (teardown;
 EXTRAS_RESERVE_S = 25.0  # run budget kept after the extras (teardown, the parent's grace)
 EXTRAS_MIN_S = 15.0  # an extras window shorter than this is skipped (agreed over ranks)
 NONROOT_GRACE_S = 10.0  # non-root ranks' headline deadline is this much later than rank 0's
+REMEASURE_MIN_S = 30.0  # headline time that must be left to re-measure over RCCL after a failed fused finish
 
 
 def _budget_left(args) -> float:
@@ -1317,6 +1322,7 @@ def main(argv=None) -> int:
     # reports it (stage named) rather than being torn down by a peer that gave up first.
     watch = _PhaseWatchdog("headline phase", headline_deadline + (0.0 if rank_env == 0 else NONROOT_GRACE_S), 2,
                            diag)
+    headline_ends = time.time() + headline_deadline  # (rank 0's watchdog)
     # fault site "init": before this rank arms anything or joins the group (a rank that exits here
     # leaves no line of its own; one that hangs here keeps the others in the rendezvous)
     fault.at(rank_env, fault.spec.step, "init", "process-group init")
@@ -1404,17 +1410,17 @@ def main(argv=None) -> int:
         # The fused finish passed its canary and self-check but failed on the headline's own steps:
         # the number is re-measured over RCCL (same data, same plan) if the run budget has room, and
         # the sidecar keeps why. Agreed over ranks (the verdict and the budget check both are).
-        fused_failed = (f"fused finish failed on the headline steps ({err or 'wrong result: ' + str(ref)[:120]}); "
-                        "re-measured over RCCL")[:300]
-        room = _budget_left(args) - HEADLINE_RESERVE_S - 30.0
+        why = f"fused finish failed on the headline steps ({err or 'wrong result: ' + str(ref)[:120]})"
+        room = min(_budget_left(args) - HEADLINE_RESERVE_S, headline_ends - time.time()) - REMEASURE_MIN_S
         if -pdist.max_over_ranks(-float(room > 0), ctx) > 0.5:
+            fused_failed = f"{why}; re-measured over RCCL"[:300]
             if ctx.is_root:
                 print(f"[bench] {fused_failed}", file=sys.stderr)
             wl.use_collective("rccl", streams=lanes)
             collective, collective_note = "rccl", fused_failed
             m, err, seen, verified, ref = timed("timed steps (RCCL after the fused finish failed)")
         else:
-            fused_failed += " — no run budget left for it"
+            fused_failed = f"{why}; no time left in the headline phase to re-measure over RCCL"[:300]
             if ctx.is_root:
                 print(f"[bench] {fused_failed}", file=sys.stderr)
     m_lanes = len(wl.lanes) if wl.lanes else 1

@@ -25,3 +25,10 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _own_bench_sidecar_dir(tmp_path, monkeypatch):
+    """bench.py's default sidecar (bench_extras_n<N>.json) goes to this test's own directory:
+    concurrent tests (pytest -n) must not overwrite each other's, nor the repo's gpurun_out/."""
+    monkeypatch.setenv("MIREDUCE_EXTRAS_DIR", str(tmp_path))

@@ -201,3 +201,18 @@ def test_bare_lines_give_the_vector_table_from_their_summary(tmp_path):
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     assert (out / "vector_direct" / "INT_MAX.txt").read_text() == "\nINT MAX 2 20.00000\nINT MAX 8 80.00000\n"
+
+
+def test_driver_record_line_in_the_stdout_tail(tmp_path):
+    # the driver keeps the contract keys in `parsed` and the printed line whole in `run.stdout_tail`:
+    # the tool reads the line (summary included) and counts the run once
+    ln = _line(8, 57000.0, 0.14)
+    ln["summary"] = {"run": "abc", "reduce_c_rows": {"direct": "INT MAX 2500.000"}}
+    parsed = {k: v for k, v in ln.items() if k != "summary"}
+    rec = {"n": 5, "runs": [{"n_gpus": 8, "parsed": parsed,
+                             "run": {"stdout_tail": "[bench] x\n" + json.dumps(ln) + "\n"}}]}
+    src = tmp_path / "SCALE.json"
+    src.write_text(json.dumps(rec))
+    rs = scaling.dedupe(scaling.parse_text(src.read_text()))
+    assert len(rs) == 1 and rs[0]["summary"]["run"] == "abc"
+    assert scaling.summarise_vector(rs)[("direct", "INT", "MAX")][8]["gibps"] == 2500.0

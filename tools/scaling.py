@@ -49,7 +49,9 @@ _DT = {"fp64": "DOUBLE", "float64": "DOUBLE", "fp32": "FLOAT", "float32": "FLOAT
 
 
 def _walk(obj):
-    """Yield every dict in a JSON document that looks like a bench.py result."""
+    """Yield every dict in a JSON document that looks like a bench.py result — also the whole JSON
+    lines inside string values (the driver's records keep the printed line in a stdout tail, and
+    only the contract keys of it in ``parsed``)."""
     if isinstance(obj, dict):
         if "n_gpus" in obj and "value" in obj and "metric" in obj:
             yield obj
@@ -59,6 +61,14 @@ def _walk(obj):
     elif isinstance(obj, list):
         for v in obj:
             yield from _walk(v)
+    elif isinstance(obj, str) and '"metric"' in obj:
+        for line in obj.splitlines():
+            line = line.strip()
+            if line.startswith("{"):
+                try:
+                    yield from _walk(json.loads(line))
+                except ValueError:
+                    continue
 
 
 def parse_text(text: str):
@@ -113,7 +123,15 @@ def dedupe(results):
             out.append(r)
         elif len(r) > len(out[seen[run]]):
             out[seen[run]] = r
-    return out
+    # a record without a run id that repeats a run's headline (the driver's ``parsed`` copy of a
+    # line also found whole in its stdout tail) is the same run
+    ided = {_headline(r) for r in out if (r.get("summary") or {}).get("run") if isinstance(r.get("summary"), dict)}
+    return [r for r in out if (isinstance(r.get("summary"), dict) and r["summary"].get("run"))
+            or _headline(r) not in ided]
+
+
+def _headline(r) -> tuple:
+    return (r.get("metric"), r.get("n_gpus"), r.get("value"), r.get("ms_per_step"))
 
 
 def key_of(r):
@@ -138,7 +156,8 @@ def summarise(results):
             ms = [float(r["ms_per_step"]) for r in rs if r.get("ms_per_step") is not None]
             out[k][n] = {"gbps": sum(float(r["value"]) for r in rs) / len(rs),
                          "ms": sum(ms) / len(ms) if ms else None, "runs": len(rs),
-                         "verified": all(r.get("verified") is not False for r in rs),
+                         "verified": (False if any(r.get("verified") is False for r in rs) else
+                                      True if all(r.get("verified") is True for r in rs) else None),
                          "combine": "/".join(sorted({str((r.get("config") or {}).get("collective", "")) for r in rs})),
                          "plans": "; ".join(sorted({str((r.get("summary") or {}).get("plans"))
                                                      for r in rs if (r.get("summary") or {}).get("plans")}))}
@@ -268,7 +287,7 @@ def write(summary, out_dir):
             wait = "" if v.get("wait_min_us") is None else "%.2f-%.2f" % (v["wait_min_us"], v["wait_max_us"])
             md.append(f"| {model} | {dt} | {op} | {n} | {v['gbps']:.1f} | {ms} | {sp} | {ef} | {v['runs']} | "
                       + " | ".join(dec) + f" | {wait} | {v.get('combine', '')} | "
-                      + ("yes" if v.get("verified", True) else "**NO**") + f" | {v.get('plans', '')} |")
+                      + {True: "yes", False: "**NO**"}.get(v.get("verified"), "?") + f" | {v.get('plans', '')} |")
     text = "\n".join(md) + "\n"
     with open(os.path.join(out_dir, "scaling.md"), "w") as f:
         f.write(text)

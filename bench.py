@@ -750,16 +750,28 @@ def _measure(wl, slots, ctx, args, fault, serial: bool, warmup: int, allow_graph
     elif probe:  # no graphs here (CPU rehearsal, --launch eager): the same probe over eager steps
         perr = _replay_probe(wl, ctx, args, fault, serial, step, capture=False)
         launch = f"eager (replay probe failed: {perr})" if perr else "eager; replay probe ok"
+    probe_window = os.environ.get("MIREDUCE_WINDOW_PROBE") == "1" and dev.type == "cuda"  # diagnostic
     _sync(dev)
     pdist.barrier(ctx)
     _sync(dev)
+    if probe_window:
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     t0 = time.perf_counter()
+    if probe_window:
+        ev[0].record()
     if sg is not None:
         sg.run()
     else:
         run(warmup, K)
+    if probe_window:
+        ev[1].record()
+        t_enq = time.perf_counter()
     _sync(dev)
     t1 = time.perf_counter()
+    if probe_window:
+        gpu = ev[0].elapsed_time(ev[1]) * 1e-3
+        print(f"[window] rank {ctx.rank} site {site} K {K}: host {(t1 - t0) * 1e6:.1f} us, gpu {gpu * 1e6:.1f} us, "
+              f"enqueue {(t_enq - t0) * 1e6:.1f} us, host - gpu {(t1 - t0 - gpu) * 1e6:.1f} us", file=sys.stderr)
     pdist.barrier(ctx)
     elapsed = pdist.max_over_ranks(t1 - t0, ctx)
     fastest = -pdist.max_over_ranks(-(t1 - t0), ctx)

@@ -17,7 +17,9 @@ event with ``query()`` instead of a blocking synchronize), ``eager`` (the K boun
 one by one, no graph) and ``split`` (a one-step graph, then a (K-1)-step one: the GPU can start
 while the longer graph is still being submitted), ``barrier`` (bench.py's bracket: an RCCL
 barrier of a 1-rank process group, then synchronize) and ``barrier_settle`` (the same, then 0.25 s
-for ProcessGroupNCCL's watchdog to retire the barrier's work before t0).
+for ProcessGroupNCCL's watchdog to retire the barrier's work before t0); ``bench`` (bench.py's
+sequence: the untimed replay of the same graph, synchronize, barrier, synchronize, t0) and
+``bench_nosync`` (the same without the first synchronize: the barrier queues behind the replay).
 
     python tools/window_overhead.py --elements 125000000 --steps 20,200 --rounds 5
 """
@@ -45,11 +47,13 @@ def main(argv=None) -> int:
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--json", default=None)
     ap.add_argument("--variants", default="plain,warm,spin,eager,split,barrier,barrier_settle")
+    ap.add_argument("--fused", action="store_true", help="bind the fused cross-rank finish (a 1-rank channel), "
+                    "as bench.py's headline step does")
     a = ap.parse_args(argv)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     variants = a.variants.split(",")
-    if any(v.startswith("barrier") for v in variants):  # bench.py's bracket: an RCCL barrier first
+    if any(v.startswith(("barrier", "bench")) for v in variants):  # bench.py's bracket: an RCCL barrier first
         from cuda_mpi_reductions_amd.parallel import dist as pdist
         ctx = pdist.init()
     n = int(a.elements)
@@ -57,7 +61,11 @@ def main(argv=None) -> int:
     fill_(x, "uniform", seed=3)
     red = Reducer(dev)
     slots = torch.zeros(1024, dtype=torch.float64, device=dev)
-    b = red.bind(x, "sum", torch.float64, out=slots[:1])
+    ch = None
+    if a.fused:
+        from cuda_mpi_reductions_amd.parallel.xrank import open_channel
+        ch = open_channel(dev)
+    b = red.bind(x, "sum", torch.float64, out=slots[:1], xrank=ch)
     stream = torch.cuda.current_stream(dev)
     ks = [int(k) for k in a.steps.split(",")]
     def step(j):
@@ -79,6 +87,11 @@ def main(argv=None) -> int:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 if how == "warm":
                     tiny.add_(1)
+                if how.startswith("bench"):  # bench.py: the untimed replay of the same graph first
+                    graphs[k].run()
+                    if how == "bench":
+                        torch.cuda.synchronize(dev)
+                    pdist.barrier(ctx)  # (bench_nosync: the barrier queues behind the replay)
                 torch.cuda.synchronize(dev)
                 if how.startswith("barrier"):
                     pdist.barrier(ctx)

@@ -486,12 +486,14 @@ def test_bench_fused_canary_two_ranks_one_gpu(tmp_path, monkeypatch, fault):
         assert d["config"]["collective"] == "fused", d["config"]["collective_choice"]
 
 
-def test_bench_ranks_hold_different_plans_and_verify(tmp_path, monkeypatch):
+@pytest.mark.parametrize("plan", ["tuned default, XCD skew 0", "tuned default, XCD skew -20", "256x4x2 window 2"])
+def test_bench_ranks_hold_different_plans_and_verify(tmp_path, monkeypatch, plan):
     # plan tuning is per rank. Two ranks sharing the GPU, each with a 1 GB shard
-    # (so the candidates are timed); rank 1 is made to hold another plan (skew 0) than rank 0 would
-    # pick — the fused finish combines launches of different plans and every step still verifies.
+    # (so the candidates are timed); rank 1 is made to hold another plan than rank 0 would pick —
+    # every candidate the tuner can choose (the self-check ran with the default plan before tuning)
+    # must combine with the fused finish, next to a rank of another plan, and verify every step.
     monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
-    monkeypatch.setenv("MIREDUCE_PLAN_FOR_RANK", "1=tuned default, XCD skew 0")
+    monkeypatch.setenv("MIREDUCE_PLAN_FOR_RANK", f"1={plan}")
     side = tmp_path / "x.json"
     r = torchrun(2, [BENCH, "--no-vector-extras", "--no-candidates", "--gpus", "2", "--backend", "gloo", "--steps", "8",
                      "--warmup", "2", "--elements", "250000000", "--tune-steps", "6", "--extras-file", str(side)],
@@ -500,6 +502,6 @@ def test_bench_ranks_hold_different_plans_and_verify(tmp_path, monkeypatch):
     d = _json(r)
     assert d["verified"] is True and d["config"]["collective"] == "fused"
     pt = d["plan_tuning"]
-    assert len(pt["plan_by_rank"]) == 2 and pt["plan_by_rank"][1] == "tuned default, XCD skew 0", pt
+    assert len(pt["plan_by_rank"]) == 2 and pt["plan_by_rank"][1] == plan, pt
     assert all(len(t) == 5 for t in pt["gbps_by_rank"])
     assert d["summary"]["plans"].count(" x") == (1 if pt["plan_by_rank"][0] == pt["plan_by_rank"][1] else 2)

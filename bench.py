@@ -1064,7 +1064,7 @@ class _Record:
                 with open(tmp, "w") as f:
                     json.dump({**out, **self.detail, **ex}, f, indent=1)
                 os.replace(tmp, self.path)
-        except OSError as e:
+        except (OSError, TypeError, ValueError) as e:  # the line must still print
             summary["extras_file"] = None
             summary["extras_file_error"] = f"{type(e).__name__}: {e}"[:160]
         return out

@@ -994,6 +994,11 @@ def _summarise(ex: dict) -> dict:
         s["local_gbps"] = dec.get("local_gbps")
         s["efficiency_vs_local"] = dec.get("scaling_efficiency_vs_local")
         s["exchange_us"] = dec.get("exchange_us_per_step")
+        if dec.get("skew_us_per_step") is not None:
+            s["skew_us"] = dec["skew_us_per_step"]
+        w = dec.get("exchange_wait_us")
+        if isinstance(w, dict) and w.get("min_rank_median") is not None:  # device-timed push -> all partials
+            s["wait_us"] = [w["min_rank_median"], w["max_rank_median"]]
     v = ex.get("reduce_c_vector")
     if isinstance(v, dict):
         s["reduce_c_gibps"] = {impl: (v.get(f"reduce_{impl}") or {}).get("gibps") for impl in ("direct", "rccl")}
@@ -1485,6 +1490,11 @@ def main(argv=None) -> int:
             "launcher": launcher,
             "native_source_hash": C.source_hash(),
         }
+        if args.collective == "auto" and collective != "fused" and (fused_failed or collective_note):
+            # why the fused finish is not the combine: in `config`, whose values the driver's record keeps
+            line["config"]["collective_reason"] = (fused_failed or collective_note)[:120]
+        if ctx.world_size > 1 and isinstance(topo, dict) and topo.get("peer_access"):
+            line["config"]["peer_access"] = str(topo["peer_access"])[:80]
         if err is not None:
             line["device_error"] = err[:300]
         detail = {

@@ -324,6 +324,9 @@ def test_bench_auto_remeasures_over_rccl_when_fused_fails_the_headline(tmp_path,
     d = bench_record(r.stdout)
     assert d["verified"] is True and d["config"]["collective"] == "rccl"
     assert "fused finish failed on the headline steps" in d["config"]["collective_choice"]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    # the reason rides in the printed line's config (the driver's record keeps config values)
+    assert line["config"]["collective_reason"].startswith("fused finish failed on the headline steps")
 
 
 # ---------------------------------------------------------------- the N=8 shapes, rehearsed
@@ -339,6 +342,8 @@ def test_bench_eight_ranks_fused_on_one_gpu(tmp_path, monkeypatch):
     d = _json(r)
     assert d["verified"] is True and d["n_gpus"] == 8 and d["config"]["parallelism"] == "dp8"
     assert d["config"]["launch"].startswith("graph")
+    lo, hi = d["summary"]["wait_us"]  # the device-timed exchange wait, min / max rank median
+    assert 0 <= lo <= hi and d["config"]["peer_access"]
 
 
 def test_bench_eight_ranks_auto_on_one_gpu(tmp_path, monkeypatch):

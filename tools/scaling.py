@@ -130,6 +130,14 @@ def dedupe(results):
             or _headline(r) not in ided]
 
 
+def _combine(r) -> str:
+    """The cross-rank combine a run used, with why the fused finish was not it (bench.py's
+    ``config.collective_reason``, shortened)."""
+    c = r.get("config") or {}
+    why = c.get("collective_reason")
+    return str(c.get("collective", "")) + (f" ({str(why)[:60]})" if why else "")
+
+
 def _headline(r) -> tuple:
     return (r.get("metric"), r.get("n_gpus"), r.get("value"), r.get("ms_per_step"))
 
@@ -158,7 +166,7 @@ def summarise(results):
                          "ms": sum(ms) / len(ms) if ms else None, "runs": len(rs),
                          "verified": (False if any(r.get("verified") is False for r in rs) else
                                       True if all(r.get("verified") is True for r in rs) else None),
-                         "combine": "/".join(sorted({str((r.get("config") or {}).get("collective", "")) for r in rs})),
+                         "combine": "/".join(sorted({_combine(r) for r in rs})),
                          "plans": "; ".join(sorted({str((r.get("summary") or {}).get("plans"))
                                                      for r in rs if (r.get("summary") or {}).get("plans")}))}
             out[k][n].update(_decomposition(rs))

@@ -119,6 +119,15 @@ def test_reduce_c_rows_summary_averages_retries_in_reduce_c_order():
     assert s["reduce_c_rows"] == rows and s["reduce_c_gibps"]["direct"] == 1.5
 
 
+def test_summary_carries_the_decomposition_skew_and_exchange_wait():
+    b = _bench()
+    dec = {"local_gbps": 7300.0, "scaling_efficiency_vs_local": 0.97, "exchange_us_per_step": 4.2,
+           "skew_us_per_step": 1.5, "exchange_wait_us": {"min_rank_median": 2.1, "max_rank_median": 3.4}}
+    s = b._summarise({"decomposition": dec})
+    assert s["skew_us"] == 1.5 and s["wait_us"] == [2.1, 3.4] and s["exchange_us"] == 4.2
+    assert "wait_us" not in b._summarise({"decomposition": {"local_gbps": 1.0}})
+
+
 class _StubWorkload:
     """Just what bench._selfcheck_slots reads: the op, slot allocation and the channel-free launch."""
 

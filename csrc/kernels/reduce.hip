@@ -158,6 +158,12 @@ bool balance_leftover() {
 // dealt round-robin): a partition with one XCD (CPX, 32 CUs) has no parity to balance, and one of 2-4
 // XCDs (DPX / QPX) was never measured, so the default skew is 0 there (an explicit skew still applies).
 constexpr int kSpxCus = 256;
+// The tuned default's extra rounds for the favoured XCD parity (arrays of >= kSkewOffsetMinRounds
+// rounds per workgroup): kSkewOffsetRounds + kSkewSharePermille of the rounds.
+constexpr uint64_t kSkewOffsetMinRounds = 64;
+constexpr int64_t kSkewOffsetRounds = 2;
+constexpr int64_t kSkewSharePermille = 18;
+
 int tuned_xcd_skew(DType t, const LaunchPlan& p, int num_cus) {
   const size_t es = dtype_size(t);
   if (num_cus < kSpxCus) return 0;
@@ -354,12 +360,20 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
       p.grid > 1) {
     // (the env override replaces the tuned default only: a caller's explicit skew — e.g. bench.py's
     // plan-tuning candidates — is what it says)
-    int permille = cfg.xcd_skew == (-2147483647 - 1) ? tuned_xcd_skew(t, p, num_cus) : cfg.xcd_skew;
-    if (const char* e = std::getenv("MIREDUCE_XCD_SKEW"); e && cfg.xcd_skew == (-2147483647 - 1))
+    bool tuned = cfg.xcd_skew == (-2147483647 - 1);
+    int permille = tuned ? tuned_xcd_skew(t, p, num_cus) : cfg.xcd_skew;
+    if (const char* e = std::getenv("MIREDUCE_XCD_SKEW"); e && tuned) {
       permille = std::atoi(e);
+      tuned = false;
+    }
     const uint64_t tile = static_cast<uint64_t>(p.block) * static_cast<uint64_t>(p.unroll);
     const uint64_t rounds = tile ? p.nvec / tile / static_cast<uint64_t>(p.grid) : 0;
-    const int64_t d = (static_cast<int64_t>(rounds) * permille + (permille >= 0 ? 500 : -500)) / 1000;
+    int64_t d = (static_cast<int64_t>(rounds) * permille + (permille >= 0 ? 500 : -500)) / 1000;
+    if (tuned && permille > 0 && rounds >= kSkewOffsetMinRounds)
+      // The tuned default is a fixed offset plus a share of the rounds, not a flat share: the
+      // optimum measured 4-5 extra rounds at the 1 GB N=8 shard (119 rounds: 20 permille gives 2,
+      // 0.3-0.6 % slower), ~6 at 2 GB and 19 at 8 GB (profiles/r5_skew/).
+      d = (static_cast<int64_t>(rounds) * kSkewSharePermille + 500) / 1000 + kSkewOffsetRounds;
     // the common rounds must stay >= 1 (the kernel resolves the anchor at their end)
     const uint64_t ad = static_cast<uint64_t>(d < 0 ? -d : d), ntiles = tile ? p.nvec / tile : 0;
     const uint64_t g = static_cast<uint64_t>(p.grid);

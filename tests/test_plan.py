@@ -56,7 +56,8 @@ def test_tuned_defaults_by_size():
     # XCD-weighted split (profiles/r4_xcd/, r4_skew/): 20 permille of the rounds extra for the
     # workgroups on odd XCCs in the 8- and 4-byte window-4 plans; explicit values override; no
     # window -> no skew
-    assert big["xskew"] == 19 and mid["xskew"] == 2     # 953 and 119 rounds per workgroup
+    assert big["xskew"] == 19 and mid["xskew"] == 4     # 953 and 119 rounds per workgroup: 2 + 18 permille
+    assert C.plan(0, 250_000_000, F64)["xskew"] == 6 and C.plan(0, 1 << 25, F64)["xskew"] == 1  # 238 / 32 rounds
     assert C.plan(0, 10**9, F64, xcd_skew=0)["xskew"] == 0 and C.plan(0, 10**9, F64, xcd_skew=-40)["xskew"] == -38
     assert small["xskew"] == 0
     f32 = C.plan(0, 2 * 10**9, 2)          # fp32 SUM 8 GB: window 4, the same skew (profiles/r4_shard/)

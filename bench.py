@@ -70,13 +70,18 @@ def _no_line(n: int, why: str) -> dict:
 
 
 def _is_result_line(line: str) -> bool:
-    if not line.startswith("{"):
-        return False
-    try:
-        d = json.loads(line)
-    except ValueError:
-        return False
-    return isinstance(d, dict) and "metric" in d and "value" in d
+    """Whether a relayed stdout line holds a result line — also behind a fragment: a rank's line
+    written on the signal path (write(2)) can follow an unterminated piece of Python's buffered
+    stdout on the same line."""
+    i = line.find("{")
+    while i >= 0:
+        try:
+            d = json.loads(line[i:])
+        except ValueError:
+            i = line.find("{", i + 1)
+            continue
+        return isinstance(d, dict) and "metric" in d and "value" in d
+    return False
 
 
 def _relay_child(child, budget_end: float, n: int) -> int:
@@ -242,6 +247,15 @@ def parse_args(argv=None):
                    help="at N > 1, skip the fused finish's canary (the same exchange run first in throw-away "
                         "helper processes, so a fault of the peer mapping cannot take the benchmark down)")
     p.add_argument("--canary-timeout", type=float, default=90.0, help="seconds each canary helper may take")
+    p.add_argument("--agree-timeout", type=float, default=60.0,
+                   help="seconds an optional headline stage (canary verdicts, fused self-check, plan tuning) waits "
+                        "for every rank's report; a rank missing past it is dead or hung: rank 0 prints a diagnostic "
+                        "line naming the stage and every rank exits with 2 (cut to end before the headline deadline)")
+    p.add_argument("--rehearse-stages", action="store_true",
+                   help="CPU ranks (--device cpu): also run the GPU-only headline stages in their CPU form — the "
+                        "canary (dry helpers), the fused finish's self-check and timed steps over its CPU twin "
+                        "(store mailboxes, same timeout semantics) and per-rank plan tuning over the host reducer — "
+                        "so their failure boundaries are testable on gloo (tests/test_fault_injection.py)")
     p.add_argument("--xrank-timeout", type=float, default=30.0,
                    help="fused finish: seconds a kernel waits for a peer's partial before flagging the channel")
     p.add_argument("--tune-steps", type=int, default=0,
@@ -290,9 +304,10 @@ def parse_args(argv=None):
                         "fewer, longer graphs leave fewer bubbles); 0 = auto: every timed step in one graph "
                         "(<= 4096) for the in-kernel fused finish, 128 when steps issue RCCL collectives")
     p.add_argument("--inject-fault", default=None,
-                   help="failure-detection test: KIND[@RANK][:STEP][/SITE], KIND = exit|hang|corrupt|delay=<ms>|"
+                   help="failure-detection test: KIND[@RANK][:STEP][/SITE], KIND = exit|hang|raise|corrupt|delay=<ms>|"
                         "mailbox, SITE = step (headline; steps count warm-up first; forces eager issue) | extras "
-                        "(the after-headline candidates)")
+                        "(the after-headline candidates) | init | capture | teardown | canary | selfcheck | tune "
+                        "(utils/fault.py)")
     p.add_argument("--pg-timeout", type=float, default=120.0, help="process-group collective timeout (s)")
     p.add_argument("--budget", type=float, default=DEFAULT_BUDGET_S,
                    help="seconds the whole run may take, from process start (self-spawned ranks: from the "
@@ -839,62 +854,133 @@ def _replay_probe(wl, ctx, args, fault, serial: bool, step, capture: bool) -> "s
     return "; ".join(f"rank {r}: {m}" for r, m in enumerate(errs) if m)[:300] or "failed on another rank"
 
 
-def _try_fused(wl, ctx, canary: bool = True, canary_timeout: float = 90.0) -> "str | None":
-    """Switch the workload to the fused in-kernel finish and check it on every rank: 3 steps, no
-    channel timeout or fan-in error, results equal to torch's reference. On any failure (agreed over
-    ranks) switch back to RCCL and return the reason. At N > 1 a canary runs the same exchange in
-    throw-away helper processes first (parallel/canary.py): a fault of the peer mapping there
-    cannot take this process — and the headline — down with it."""
-    if canary and ctx.world_size > 1:
+def _agree_timeout(args) -> float:
+    """The bound of an optional stage's agreement: --agree-timeout, cut so that a lost rank is
+    reported by the agreement (its stage named) before the headline deadline would fire."""
+    left = getattr(args, "_headline_ends", None)
+    cap = (left - time.time() - 5.0) if left else args.agree_timeout
+    return max(1.0, min(args.agree_timeout, cap))
+
+
+def _try_fused(wl, ctx, args, fault, at_stage=lambda name: None) -> "str | None":
+    """Switch the workload to the fused in-kernel finish and check it on every rank; on any failure
+    switch back to RCCL (every rank together) and return the reason. Three stages, each behind a
+    failure boundary agreed over ranks (an optional 0.5 % path must never cost
+    the one-shot N-GPU measurement):
+
+    * ``canary`` (N > 1): the same exchange in throw-away helper processes first
+      (parallel/canary.py) — a fault of the peer mapping there cannot take this process, and the
+      headline, down with it; the helpers' verdicts are agreed through a bounded store exchange;
+    * channel setup: collective by construction (``open_channel`` raises on every rank together);
+    * ``fused self-check``: 3 fused steps, this rank's error words and the same kernel's partial
+      without a channel — all LOCAL, inside a try — then one bounded agreement
+      (:func:`parallel.dist.agree`) of every rank's report, from which every rank derives the same
+      verdict. A rank whose part raised reports the error; one that died or hangs makes the others
+      raise :class:`parallel.dist.PeerLost` (main() prints the diagnostic line naming the stage)
+      instead of waiting in a collective until the process-group timeout.
+
+    Fault sites ``canary`` / ``selfcheck`` (utils/fault.py) fire inside these stages."""
+    agree_s = _agree_timeout(args)
+    if args.canary and ctx.world_size > 1:
+        at_stage("canary")
         from cuda_mpi_reductions_amd.parallel.canary import fused_canary
-        err = fused_canary(ctx, timeout_s=canary_timeout, dry=ctx.device.type != "cuda")
+        err = fused_canary(ctx, timeout_s=args.canary_timeout, dry=ctx.device.type != "cuda", fault=fault,
+                           agree_timeout_s=agree_s)
         if err is not None:
             return f"canary: {err}"[:300]
+    at_stage("fused self-check")
     try:
         wl.use_collective("fused", streams=1)  # collective; raises on every rank if any rank cannot map
     except Exception as e:  # noqa: BLE001
         wl.use_collective("rccl", streams=1)
         return f"setup: {e}"[:300]
-    slots = wl.new_slots(3)
-    for i in range(3):
-        wl.step(slots[i:i + 1])
-    _sync(ctx.device)
-    err = wl.check()
-    if err is None:
-        ok, ref = _selfcheck_slots(wl, slots, ctx)
-        if not ok:
-            err = f"self-check mismatch: {ref}"
-    if err is not None:
-        wl.use_collective("rccl", streams=1)
-    return err
+    mine = {"error": None}
+    try:
+        fault.at(ctx.rank, fault.spec.step, "selfcheck", "fused self-check")
+        slots = wl.new_slots(3)
+        for i in range(3):
+            wl.step(slots[i:i + 1])
+        mine.update(_selfcheck_report(wl, slots))
+    except Exception as e:  # noqa: BLE001 - this rank's report carries it; every rank falls back together
+        mine["error"] = f"{type(e).__name__}: {e}"[:200]
+        print(f"[bench] rank {ctx.rank}: fused self-check failed here: {mine['error']}", file=sys.stderr, flush=True)
+    rows = pdist.agree(ctx, "fused self-check", mine, _agree_timeout(args))
+    if (mine.get("counts") or [0])[0]:
+        wl.reset_fanin()  # this rank's sticky fan-in error was reported: clear it
+    ok, ref = _selfcheck_verdict(rows, wl.cfg.op, wl.new_slots(1).dtype)
+    if ok:
+        return None
+    wl.use_collective("rccl", streams=1)  # every rank: the verdict is the same everywhere
+    return ref["reason"][:300]
 
 
-def _selfcheck_slots(wl, slots: torch.Tensor, ctx) -> tuple:
-    """The fused finish's self-check value: this rank's partial from the SAME kernel launched
-    without a channel, combined over the process group (what the fused exchange replaces). It
-    tests the exchange, not the kernel, and needs no torch pass over the array before the timed
-    steps: the full torch reference still checks every timed slot afterwards (``_verify_slots``).
-    Every slot must match on every rank (AND over ranks)."""
+def _py(v):
+    """A tensor element as a JSON-exact Python number (float repr round-trips; ints are exact)."""
+    return float(v) if isinstance(v, float) else int(v)
+
+
+def _selfcheck_report(wl, slots: torch.Tensor) -> dict:
+    """This rank's part of the fused self-check, local only: its error words (the fused finish's
+    and the fan-in's), the SAME kernel's partial launched without a channel (what the exchange
+    combines), and the slots the fused steps wrote."""
     loc = wl.new_slots(1)
     wl.local(loc)
-    _sync(ctx.device)
-    floating = loc.dtype.is_floating_point
-    host = loc.to(torch.float64 if floating else torch.int64).cpu()
-    mag = host.abs().to(torch.float64)
-    if ctx.world_size > 1:
-        dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
-        t, m = host.to(dev), mag.to(dev)
-        torch.distributed.all_reduce(t, op=pdist.reduce_op(wl.cfg.op))
-        torch.distributed.all_reduce(m)
-        host, mag = t.cpu(), m.cpu()
-    expect = host.item()
+    if loc.is_cuda:
+        torch.cuda.synchronize(loc.device)
+    counts = wl.error_counts() if hasattr(wl, "error_counts") else [0, 0, 0, 0]
+    p = _py(loc.cpu().item())
+    return {"counts": counts, "partial": p, "mag": abs(float(p)), "slots": [_py(v) for v in slots.cpu().tolist()]}
+
+
+def _selfcheck_verdict(rows: list, op: str, acc: torch.dtype) -> tuple:
+    """(ok, ref) from every rank's :func:`_selfcheck_report` (the same on every rank): any rank's
+    error, any device error word, or any slot that differs from the fold of the ranks' channel-free
+    partials fails it — exactly for MIN/MAX and integers, within a few ulps of the accumulator for
+    floating SUM (the partials fold in another order)."""
+    errs = [f"rank {r}: {row['error']}" for r, row in enumerate(rows) if row.get("error")]
+    if errs:
+        return False, {"reason": "self-check: " + "; ".join(errs)}
+    from cuda_mpi_reductions_amd.models import ScalarReduction
+    counts = [sum(int(row["counts"][k]) for row in rows) for k in range(4)]
+    dev_err = ScalarReduction.describe_errors(counts)
+    if dev_err:
+        return False, {"reason": dev_err}
+    parts = [row["partial"] for row in rows]
+    if op in ("min",):
+        expect = min(parts)
+    elif op in ("max", "amax"):
+        expect = max(parts)
+    else:
+        expect = parts[0]
+        for v in parts[1:]:
+            expect = expect + v
+    floating = acc.is_floating_point
     tol = 0.0
-    if floating and wl.cfg.op in ("sum", "sumsq"):  # the partials fold in another order: a few ulps
-        tol = 8.0 * ctx.world_size * torch.finfo(loc.dtype).eps * mag.item()
-    got = slots.to(torch.float64 if floating else torch.int64).cpu()
-    ok = bool(((got - expect).abs() <= tol).all().item()) if floating else bool((got == expect).all().item())
-    ok = -pdist.max_over_ranks(-float(ok), ctx) > 0.5
-    return ok, {"got": got.tolist(), "expected": expect, "tolerance": tol}
+    if floating and op in ("sum", "sumsq"):
+        tol = 8.0 * len(rows) * torch.finfo(acc).eps * sum(row["mag"] for row in rows)
+    bad = []
+    for r, row in enumerate(rows):
+        for v in row["slots"]:
+            if floating:
+                if not abs(float(v) - float(expect)) <= tol:  # (NaN: never within)
+                    bad.append((r, v))
+            elif int(v) != int(expect):
+                bad.append((r, v))
+    ref = {"got": rows[0]["slots"], "expected": expect, "tolerance": tol}
+    if bad:
+        ref["reason"] = f"self-check mismatch: {ref} (rank, slot) {bad[:4]}"
+        return False, ref
+    return True, ref
+
+
+def _selfcheck_slots(wl, slots: torch.Tensor, ctx, timeout_s: float = 60.0) -> tuple:
+    """The fused finish's self-check value: this rank's partial from the SAME kernel launched
+    without a channel, combined over the ranks (what the fused exchange replaces). It tests the
+    exchange, not the kernel, and needs no torch pass over the array before the timed steps: the
+    full torch reference still checks every timed slot afterwards (``_verify_slots``). Every slot
+    must match on every rank; the reports are agreed through one bounded store exchange."""
+    rows = pdist.agree(ctx, "fused self-check", _selfcheck_report(wl, slots), timeout_s)
+    return _selfcheck_verdict(rows, wl.cfg.op, slots.dtype)
 
 
 def _verify_slots(wl, written: torch.Tensor, ctx) -> tuple:
@@ -1216,49 +1302,126 @@ def _exchange_wait(wl, ctx, args, fault, cap: int = 4096, allow_graph: bool = Tr
             "errors": [r["error"] for r in rows if r["error"]] or None}
 
 
+def _time_local(launch, slots: torch.Tensor, T: int, dev: torch.device) -> float:
+    """Seconds this rank alone takes for T launches of ``launch`` (2 eager warm-ups; on GPUs the T
+    launches are replayed from one captured graph, uploaded by an untimed replay; eager if the
+    capture fails or on CPU). No collective: the candidates of every rank are timed independently
+    (each GPU streams its own HBM)."""
+    for i in range(2):
+        launch(slots[i:i + 1])
+    _sync(dev)
+    sg = None
+    if dev.type == "cuda":
+        sg = StepGraph(lambda j: launch(slots[2 + j:3 + j]), T, dev, chunk=T, serial=True)
+        if sg.capture(group_agree=False, settle_s=0.0):  # kernels only: the NCCL stream stays out
+            sg.run()
+            _sync(dev)
+        else:
+            sg = None
+    t0 = time.perf_counter()
+    if sg is not None:
+        sg.run()
+    else:
+        for j in range(T):
+            launch(slots[2 + j:3 + j])
+    _sync(dev)
+    el = time.perf_counter() - t0
+    if sg is not None:
+        sg.reset()
+    return el
+
+
 def _tune_plan(wl, ctx, args, fault, kernel, cands) -> "tuple[KernelConfig, dict]":
     """Streaming-kernel plan for this rank's shard, chosen PER RANK: every candidate is measured on
-    every rank at once (between barriers), kernel-only — the step's own local launch without the
-    combine (``wl.local_step``: one lane, serial, graph replay) — in two rounds, best of each (a
-    first candidate measured while the driver works on memory released just before it runs slow:
-    profiles/r3_selfcheck/), and each rank keeps the plan that is fastest on ITS GPU. The step time
-    of the N-GPU job is the max over ranks of (local + combine), so per-rank choice
-    strictly dominates one plan for all: max_r min_p t(r, p) <= min_p max_r t(r, p). A candidate
-    whose fan-in flagged an error on any rank is out for every rank (-1, sticky; the error words
-    are agreed over ranks). Returns this rank's kernel config and the record (``chosen`` = rank 0's
-    plan, ``plan_by_rank`` = every rank's, ``gbps_by_rank`` = every rank's table)."""
+    every rank, kernel-only — the step's own local launch without the combine (a prepared launch on
+    a workspace of its own, no channel: ``wl.local_launcher``), graph-replayed — in two rounds, best
+    of each (a first candidate measured while the driver works on memory released just before it
+    runs slow: profiles/r3_selfcheck/), and each rank keeps the plan that is fastest on ITS GPU. The
+    step time of the N-GPU job is the max over ranks of (local + combine), so per-rank
+    choice strictly dominates one plan for all: max_r min_p t(r, p) <= min_p max_r t(r, p).
+
+    Failure boundary: the measurement is LOCAL (no collective, the bound
+    combine untouched) and inside a try; then one bounded agreement (:func:`parallel.dist.agree`)
+    of every rank's table. A candidate whose fan-in flagged an error on any rank is out for every
+    rank; if any rank's tuning raised, EVERY rank keeps the tuned default (already bound) and the
+    record says why; a rank that died or hangs makes the others raise PeerLost (main() prints the
+    line naming the stage). Only then, with every rank's choice known, are the chosen plans bound
+    (one collective re-bind, skipped when every rank keeps the default); if that re-bind fails
+    anywhere, every rank returns to the default plan. Fault site ``tune`` fires before the
+    candidates are measured. Returns this rank's kernel config and the record (``chosen`` = rank
+    0's plan, ``plan_by_rank`` = every rank's, ``gbps_by_rank`` = every rank's table)."""
     T = max(4, args.tune_steps) if args.tune_steps else _auto_tune_steps(wl.bytes_total / ctx.world_size)
     local_bytes = wl.count * wl.x.element_size()
-    res = {}
-    for _round in range(2):
-        for c in cands:
-            key = _plan_key(c)
-            if res.get(key, 0.0) < 0:
-                continue
-            b, u, w, win, skew = c
-            wl.use_kernel(replace(kernel, block=b, unroll=u, wg_per_cu=w, window=None if win < 0 else win,
-                                  xcd_skew=skew), streams=1)
-            mt = _measure(wl, wl.new_slots(2 + T), ctx, args, fault, serial=True, warmup=2, steps=T,
-                          site="tune", step_fn=wl.local_step)
-            g = round(local_bytes * T / mt["elapsed_local"] / 1e9, 3)
-            res[key] = -1.0 if wl.check() is not None else max(res.get(key, 0.0), g)
-    best = max(res, key=res.get)
-    # test hook (tests/test_xrank_gpu.py): MIREDUCE_PLAN_FOR_RANK="1=tuned default, XCD skew 0;..." makes
-    # the named ranks hold another candidate, so a heterogeneous job is exercised deterministically
-    for item in filter(None, os.environ.get("MIREDUCE_PLAN_FOR_RANK", "").split(";")):
-        r, _, key = item.partition("=")
-        if r.strip() == str(ctx.rank) and any(_plan_key(c) == key for c in cands) and res.get(key, 0.0) >= 0:
-            best = key
-    b, u, w, win, skew = next(c for c in cands if _plan_key(c) == best)
-    kernel = replace(kernel, block=b, unroll=u, wg_per_cu=w, window=None if win < 0 else win, xcd_skew=skew)
-    wl.use_kernel(kernel, streams=1)  # (collective: every rank re-binds, each with its own plan)
-    rows = [{"chosen": best, "gbps": res}]
-    if ctx.world_size > 1:
-        rows = [None] * ctx.world_size
-        torch.distributed.all_gather_object(rows, {"chosen": best, "gbps": res})
-    return kernel, {"steps": T, "measure": "kernel-only local launch per rank (GB/s of the rank's shard)",
-                    "chosen": rows[0]["chosen"], "plan_by_rank": [r["chosen"] for r in rows],
-                    "gbps_by_rank": [r["gbps"] for r in rows]}
+    default_key = _plan_key(cands[0])
+    res, err = {}, None
+    try:
+        fault.at(ctx.rank, fault.spec.step, "tune", "plan tuning")
+        launchers = {}
+        slots = wl.new_slots(2 + T)
+        for _round in range(2):
+            for c in cands:
+                key = _plan_key(c)
+                if res.get(key, 0.0) < 0:
+                    continue
+                b, u, w, win, skew = c
+                if key not in launchers:
+                    launchers[key] = wl.local_launcher(replace(kernel, block=b, unroll=u, wg_per_cu=w,
+                                                               window=None if win < 0 else win, xcd_skew=skew))
+                launch, error = launchers[key]
+                el = _time_local(launch, slots, T, ctx.device)
+                g = round(local_bytes * T / el / 1e9, 3)
+                res[key] = -1.0 if error() != 0 else max(res.get(key, 0.0), g)
+        launchers.clear()
+    except Exception as e:  # noqa: BLE001 - reported through the agreement; every rank keeps the default
+        err = f"{type(e).__name__}: {e}"[:200]
+        print(f"[bench] rank {ctx.rank}: plan tuning failed here: {err}", file=sys.stderr, flush=True)
+    forced = None
+    # test hook (tests/test_xrank_gpu.py, MIREDUCE_TEST=1 only): MIREDUCE_PLAN_FOR_RANK="1=tuned default,
+    # XCD skew 0;..." makes the named ranks hold another candidate, so a heterogeneous job is exercised
+    # deterministically; the record marks it (forced_by_env)
+    if os.environ.get("MIREDUCE_TEST") == "1":
+        for item in filter(None, os.environ.get("MIREDUCE_PLAN_FOR_RANK", "").split(";")):
+            r, _, key = item.partition("=")
+            if r.strip() == str(ctx.rank) and any(_plan_key(c) == key for c in cands):
+                forced = key
+    rows = pdist.agree(ctx, "plan tuning", {"error": err, "gbps": res, "forced": forced}, _agree_timeout(args))
+    rec = {"steps": T, "measure": "kernel-only local launch per rank (GB/s of the rank's shard)",
+           "gbps_by_rank": [r["gbps"] for r in rows]}
+    errs = [f"rank {r}: {row['error']}" for r, row in enumerate(rows) if row["error"]]
+    if errs:  # every rank keeps the tuned default plan, which the workload is still bound to
+        rec.update(chosen=default_key, plan_by_rank=[default_key] * ctx.world_size,
+                   error="; ".join(errs)[:300], fallback="tuned default on every rank")
+        return kernel, rec
+    out = {k for row in rows for k, v in row["gbps"].items() if v < 0}  # a fan-in error on any rank
+    picks = []
+    for row in rows:
+        ok = {k: v for k, v in row["gbps"].items() if k not in out}
+        best = max(ok, key=ok.get) if ok else default_key
+        if row["forced"] and row["forced"] not in out:
+            best = row["forced"]
+        picks.append(best)
+    if any(row["forced"] for row in rows):
+        rec["forced_by_env"] = {str(r): row["forced"] for r, row in enumerate(rows) if row["forced"]}
+    mine = picks[ctx.rank]
+    b, u, w, win, skew = next(c for c in cands if _plan_key(c) == mine)
+    chosen = replace(kernel, block=b, unroll=u, wg_per_cu=w, window=None if win < 0 else win, xcd_skew=skew)
+    if all(p == default_key for p in picks):
+        rec.update(chosen=picks[0], plan_by_rank=picks)
+        return kernel, rec
+    bind_err = None
+    try:
+        wl.use_kernel(chosen, streams=1)  # collective: every rank re-binds, each with its own plan
+    except Exception as e:  # noqa: BLE001
+        bind_err = f"{type(e).__name__}: {e}"[:200]
+    bad = [f"rank {r}: {row['error']}" for r, row in
+           enumerate(pdist.agree(ctx, "plan binding", {"error": bind_err}, _agree_timeout(args))) if row["error"]]
+    if bad:
+        wl.use_kernel(kernel, streams=1)
+        rec.update(chosen=default_key, plan_by_rank=[default_key] * ctx.world_size,
+                   error=("binding: " + "; ".join(bad))[:300], fallback="tuned default on every rank")
+        return kernel, rec
+    rec.update(chosen=picks[0], plan_by_rank=picks)
+    return chosen, rec
 
 
 def _plans_summary(plan_by_rank: list) -> str:
@@ -1300,7 +1463,39 @@ def _deadline(args, requested: float, reserve: float, floor: float = 5.0) -> flo
     return max(floor, min(requested, _budget_left(args) - reserve))
 
 
+_STATE: dict = {}  # what main() needs when a bounded agreement reports a lost rank (PeerLost)
+
+
 def main(argv=None) -> int:
+    """The bench; a rank found dead or hung by a bounded agreement (parallel.dist.PeerLost: no
+    collective can complete any more) ends the job here with exactly one line from rank 0 — the
+    diagnostic naming the stage during the headline phase, the verified headline (extras marked)
+    after it — and status 2 (headline phase) or the headline's status."""
+    try:
+        return _main(argv)
+    except pdist.PeerLost as e:
+        rec = _STATE.get("record")
+        line = rec.final(error=f"extras stopped: {e}") if rec is not None else \
+            (_STATE["diag"](str(e)) if _STATE.get("diag") else None)
+        if line is not None:
+            _emit(line)
+        import datetime
+        try:  # the other ranks wait (bounded) until rank 0 has printed: an early exit of theirs would
+            # make the launcher SIGTERM rank 0 first, and its line would be the generic armed one
+            store = pdist._store()
+            if line is not None:
+                store.set("mireduce/peer-lost-line", "1")
+            elif int(os.environ.get("RANK", "0")) != 0:
+                store.wait(["mireduce/peer-lost-line"], datetime.timedelta(seconds=NONROOT_GRACE_S))
+        except Exception:  # noqa: BLE001 - rank 0 gone too (the launcher's parent prints then)
+            pass
+        rc = _STATE.get("rc", 2) if _STATE.get("headline_done") else 2
+        print(f"[bench] {e}: exiting with {rc}", file=sys.stderr, flush=True)
+        sys.stderr.flush()
+        os._exit(rc)
+
+
+def _main(argv=None) -> int:
     args = parse_args(argv)
     C = native()  # fail loudly if the HIP extension is missing
     C.set_tracing(args.trace)
@@ -1334,6 +1529,7 @@ def main(argv=None) -> int:
     def at_stage(name: str) -> None:
         stage["now"] = name
         _arm(diag("the process was terminated (signal) during the headline phase"))
+    _STATE.update(diag=diag, record=None, headline_done=False)
 
     # Rank 0 owns the line, so the other ranks' deadline is a little later: on a common hang rank 0
     # reports it (stage named) rather than being torn down by a peer that gave up first.
@@ -1368,7 +1564,8 @@ def main(argv=None) -> int:
                           nontemporal=None if args.policy == "auto" else args.policy == "nt",
                           single_pass=not args.two_pass)
     collective = args.collective
-    fused_ok = dev.type == "cuda" and not args.two_pass and cfg.op not in LOC_OPS and not args.local_only
+    rehearse = args.rehearse_stages and dev.type == "cpu"  # the GPU-only stages in their CPU form
+    fused_ok = (dev.type == "cuda" or rehearse) and not args.two_pass and cfg.op not in LOC_OPS and not args.local_only
     if collective == "fused" and not fused_ok:
         raise SystemExit("--collective fused needs GPUs, the single-pass kernel and a non-LOC operator")
     lanes = max(1, args.streams) if args.pipelined else 1
@@ -1378,11 +1575,12 @@ def main(argv=None) -> int:
                          always_collective=not args.local_only, xrank_timeout_s=args.xrank_timeout,
                          fault=fault).setup()
     collective_note = None
+    args._headline_ends = headline_ends
     if collective == "auto":
         collective = "rccl"
         if fused_ok:
             at_stage("fused self-check")
-            collective_note = _try_fused(wl, ctx, canary=args.canary, canary_timeout=args.canary_timeout)
+            collective_note = _try_fused(wl, ctx, args, fault, at_stage)
             collective = "fused" if collective_note is None else "rccl"
             if collective_note and ctx.is_root:
                 print(f"[bench] fused finish unavailable, using RCCL: {collective_note}", file=sys.stderr)
@@ -1392,10 +1590,12 @@ def main(argv=None) -> int:
     plan_tuning = None
     explicit_plan = args.block or args.unroll or args.wg_per_cu or args.two_pass or args.policy != "auto"
     if args.collective == "auto" and collective == "fused" and lanes == 1 and not fault.on("step") \
-            and dev.type == "cuda" and not explicit_plan and args.plan_tune and hasattr(wl, "use_kernel"):
-        cands = _plan_candidates(wl.bytes_total / ctx.world_size, torch.empty((), dtype=cfg.dtype).element_size())
+            and (dev.type == "cuda" or rehearse) and not explicit_plan and args.plan_tune and hasattr(wl, "use_kernel"):
+        es = torch.empty((), dtype=cfg.dtype).element_size()
+        # (a CPU rehearsal times the large-shard candidate list over the host reducer)
+        cands = _plan_candidates(1 << 40 if rehearse else wl.bytes_total / ctx.world_size, es)
         if len(cands) > 1:
-            # kernel-only steps with bounded device waits: this cannot hang on a collective
+            # local, kernel-only measurements, then one bounded agreement: cannot hang on a collective
             at_stage("plan tuning")
             kernel, plan_tuning = _tune_plan(wl, ctx, args, fault, kernel, cands)
 
@@ -1493,6 +1693,9 @@ def main(argv=None) -> int:
         if args.collective == "auto" and collective != "fused" and (fused_failed or collective_note):
             # why the fused finish is not the combine: in `config`, whose values the driver's record keeps
             line["config"]["collective_reason"] = (fused_failed or collective_note)[:120]
+        if plan_tuning is not None and plan_tuning.get("error"):
+            # why every rank kept the tuned default plan (the tuning failed on some rank)
+            line["config"]["plan_reason"] = f"plan tuning fell back to the tuned default: {plan_tuning['error']}"[:160]
         if ctx.world_size > 1 and isinstance(topo, dict) and topo.get("peer_access"):
             line["config"]["peer_access"] = str(topo["peer_access"])[:80]
         if err is not None:
@@ -1529,6 +1732,7 @@ def main(argv=None) -> int:
     rc = 0 if verified in (None, True) else 1
     if not watch.finish():
         return 2  # (unreachable: the watchdog ended the process)
+    _STATE.update(record=record, rc=rc, headline_done=True)
 
     # ------------------------------------------------------------------ extras (watchdog; never the headline)
     # Order: the decomposition and the fused 2-lane candidate (kernels only), reduce.c's table

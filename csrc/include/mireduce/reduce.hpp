@@ -60,7 +60,7 @@ struct ReduceConfig {
   uint64_t debug_delay_ticks = 0;
   // Test hook: workgroup 0 of an XCD-weighted launch sleeps this many wall-clock ticks before it
   // publishes the XCD anchor (0: none); past fanin_bound_ticks every other workgroup gives up on
-  // it, the launch is poisoned and Workspace::error() has bit 2 set.
+  // it, the launch is poisoned and Workspace::error() has value 2 (bit 1) set.
   uint64_t debug_delay_anchor_ticks = 0;
   // Diagnostic hook (tools/xcd_balance.py): workgroup b writes [3b] the wall clock after its last
   // streamed tile was consumed, [3b+1] its XCC id, [3b+2] its tile count (device pointer; null: off).
@@ -123,7 +123,7 @@ class Workspace {
   // for workgroup 0's publish, so its tiles were not the split's (it then withholds its partial,
   // and in two-pass mode the finalize poisons the result). Non-zero: that launch and every later
   // one wrote a poisoned result (NaN, or the operator's identity for integers — for which this
-  // word, not the value, is the signal) until reset(). (Bit 1 is the word's value 2.)
+  // word, not the value, is the signal) until reset(). (Value 2 (bit 1): a late XCD anchor.)
   unsigned error() const;
   // Re-zero the tickets, fan-in slots and the sticky error (after an error or an aborted launch;
   // stream-ordered: no launch on this workspace may be running on another stream).

@@ -21,7 +21,7 @@
 // most one epoch ahead of the slowest peer: it needs that peer's partial to finish). A poll that
 // exceeds `timeout` sets a sticky error word instead of hanging (later launches then do not wait),
 // which XrankChannel::error() reports. A rank whose own fan-in failed pushes its partial with a
-// poison flag in the tag; its peers then set error bit 2 and poison their results too, so the
+// poison flag in the tag; its peers then set error value 2 (bit 1) and poison their results too, so the
 // failure is visible on every rank (integers are poisoned to the operator's identity, so the
 // error word is their only signal). Epochs are 31 bits (the 32nd tag bit is the flag) and wrap
 // keeping their parity.

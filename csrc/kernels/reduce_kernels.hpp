@@ -151,7 +151,7 @@ __device__ __forceinline__ T from_bits64(uint64_t b) {
 // partials, so their latency (a descriptor miss, ~0.5 us at N=1) is off the critical path.
 // Mailbox word tags: a 31-bit epoch plus the poison flag (bit 63 of the word): a rank whose own
 // result is poisoned pushes its (neutral) partial with the flag set, and every peer that folds it
-// sets error bit 2 on its own channel and poisons its result too — a failure on one rank is never
+// sets error value 2 (bit 1) on its own channel and poisons its result too — a failure on one rank is never
 // a plausible-looking value on another.
 constexpr unsigned kXrankEpochMask = 0x7fffffffu;
 constexpr uint64_t kXrankPoisonBit = 1ull << 63;
@@ -383,7 +383,7 @@ struct XcdAnchor {
   uint64_t* word;     // null: the split is complete up front (q); else q is run 0 (>= 1 tile) only
   unsigned favour;    // XCC parity taking the extra rounds (xskew > 0: odd)
   bool publish;       // workgroup 0
-  unsigned* err;      // sticky error word (Workspace fan[1]); bit 2: the anchor never arrived
+  unsigned* err;      // sticky error word (Workspace fan[1]); value 2 (bit 1): the anchor never arrived
   uint64_t bound;     // wait bound in wall-clock ticks
   uint64_t delay;     // test hook: workgroup 0 sleeps this long before publishing (0: none)
   uint64_t ntiles, grid, ra, dd, b;
@@ -405,7 +405,7 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
 // The anchored runs 1 and 2: `w` is the anchor as loaded; re-polled (bounded) while it is an earlier
 // launch's. Returns true (uniform) if the anchor never arrived within the bound: this workgroup then
 // streams the parity-0 tail, which need not match the other workgroups' — the split is no longer a
-// bijection, so the caller must poison the launch's result (sticky bit 2 of fan[1] is set here).
+// bijection, so the caller must poison the launch's result (sticky value 2 (bit 1) of fan[1] is set here).
 __device__ __forceinline__ bool resolve_anchor(TileSeq& q, const XcdAnchor& x, unsigned fan_raw, uint64_t w) {
   const uint64_t tag = static_cast<uint64_t>(fan_epoch(fan_raw)) << 32;
   bool late = false;
@@ -727,7 +727,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   AccT v = block_reduce<OpT, AccT, BLOCK>(acc[0], lds);
   AccT* partials = static_cast<AccT*>(a.partials);
   if (a.groups == 0) {  // two-pass mode: the finalize kernel (kernel boundary) reads these
-    // (a late anchor: the finalize sees fan[1] bit 2 after the kernel boundary and poisons the result)
+    // (a late anchor: the finalize sees fan[1] value 2 (bit 1) after the kernel boundary and poisons the result)
     if (threadIdx.x == 0) partials[blockIdx.x] = anchor_late ? poisoned<OpT, AccT>() : v;
     return;
   }
@@ -959,7 +959,7 @@ __global__ __launch_bounds__(256) void finalize(const AccT* __restrict__ partial
   AccT s = OpT::template identity<AccT>();
   for (uint64_t i = threadIdx.x; i < count; i += 256) s = OpT::apply(s, partials[i]);
   s = block_reduce<OpT, AccT, 256>(s, lds);
-  // a first-level workgroup's XCD anchor was late (sticky bit 2): its tiles were not the split's
+  // a first-level workgroup's XCD anchor was late (sticky value 2, bit 1): its tiles were not the split's
   const bool anchor_err = fan && (__hip_atomic_load(fan + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2u);
   if (threadIdx.x == 0) *out = anchor_err ? poisoned<OpT, AccT>() : s;
   if (fan) {

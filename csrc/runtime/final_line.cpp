@@ -55,6 +55,13 @@ bool is_ours(const struct sigaction& sa) {
 // The armed line (once), then whatever handled the signal before us: Python's SIGINT handler
 // (KeyboardInterrupt), faulthandler / a crash reporter, or the default action (re-raised).
 void on_signal(int sig, siginfo_t* info, void* uctx) {
+  const int k = slot_of(sig);
+  struct sigaction prev{};
+  if (k >= 0) prev = g_prev[k];
+  // A signal the process ignored before us stays ignored: it must not take the once-guard (the
+  // process lives on and its real line must still print), ADVICE r5. (install() skips ignored
+  // signals; this covers a disposition recorded otherwise.)
+  if (k >= 0 && !(prev.sa_flags & SA_SIGINFO) && prev.sa_handler == SIG_IGN) return;
   const int c = g_cur.load(std::memory_order_acquire);
   if (!g_emitted.exchange(true)) {
     if (c >= 0) write_all(g_buf[c], g_len[c]);
@@ -65,15 +72,11 @@ void on_signal(int sig, siginfo_t* info, void* uctx) {
     const struct timespec ts = {0, 1000000};
     for (int i = 0; i < 2000 && !g_written.load(std::memory_order_acquire); ++i) ::nanosleep(&ts, nullptr);
   }
-  const int k = slot_of(sig);
-  struct sigaction prev{};
-  if (k >= 0) prev = g_prev[k];
   if (k < 0 || (!(prev.sa_flags & SA_SIGINFO) && prev.sa_handler == SIG_DFL)) {
     ::signal(sig, SIG_DFL);
     ::raise(sig);
     return;
   }
-  if (!(prev.sa_flags & SA_SIGINFO) && prev.sa_handler == SIG_IGN) return;
   // chain: the previous handler runs as it would have (it stays installed for the next signal)
   ::sigaction(sig, &prev, nullptr);
   if (prev.sa_flags & SA_SIGINFO) prev.sa_sigaction(sig, info, uctx);
@@ -86,6 +89,8 @@ void install() {
   for (int i = 0; i < kNumSignals; ++i) {
     struct sigaction cur;
     if (::sigaction(kSignals[i], nullptr, &cur) != 0 || is_ours(cur)) continue;
+    // ignored (SIGHUP under nohup, SIGINT of a background job): not a termination, leave it so
+    if (!(cur.sa_flags & SA_SIGINFO) && cur.sa_handler == SIG_IGN) continue;
     g_prev[i] = cur;
     struct sigaction sa;
     std::memset(&sa, 0, sizeof sa);

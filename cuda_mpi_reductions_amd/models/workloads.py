@@ -108,6 +108,7 @@ NORTH_STAR = "xgmi_1b_double_sum"
 
 
 _nullcontext = contextlib.nullcontext
+_CPU_CHANNELS = [0]  # CPU twin channels opened by this process (every rank opens them in the same order)
 
 
 def _current_stream_handle(device: torch.device) -> int:
@@ -169,6 +170,7 @@ class ScalarReduction:
         self._fork = None
         self.bound = None  # lane 0's prepared launch, set by setup()
         self._local_bound = None  # lane 0's plan without a channel (local_step), made on first use
+        self._cpu_xrank = None  # CPU ranks: the fused finish's twin channel (_open_cpu_channel)
 
     # ------------------------------------------------------------------ setup
     def _size_for_hbm(self) -> int:
@@ -210,8 +212,57 @@ class ScalarReduction:
             self.reducer, self.bound = self.lanes[0][1], self.lanes[0][2]
             torch.cuda.synchronize(dev)
         elif self.collective == "fused":
-            raise RuntimeError("the fused cross-rank finish needs GPUs")
+            self._open_cpu_channel()
         return self
+
+    # ------------------------------------------------------------------ the fused finish's CPU twin
+    def _open_cpu_channel(self) -> None:
+        """CPU ranks (bench.py --rehearse-stages, tests): a twin of the fused cross-rank finish with
+        the same protocol and failure semantics as the in-kernel one (xrank.hpp): every step's
+        partial is pushed into a per-launch mailbox (a key of the job's rendezvous store, tagged with
+        the channel and the launch epoch), the peers' are waited for at most ``xrank_timeout_s``
+        (then the result is poisoned and the sticky error set; later launches look once) and folded
+        in rank order. Opening is collective and agreed (a rank failing to create its mailbox — the
+        ``mailbox`` fault — fails every rank's open, as ``parallel.xrank.open_channel`` does)."""
+        _CPU_CHANNELS[0] += 1
+        ok = self.fault is None or not self.fault.mailbox(self.ctx.rank)
+        rows = pdist.agree(self.ctx, "xrank open", {"ok": ok}, timeout_s=max(30.0, self.xrank_timeout_s))
+        bad = [r for r, row in enumerate(rows) if not row["ok"]]
+        if bad:
+            self._cpu_xrank = None
+            raise RuntimeError(f"fused finish (CPU twin): rank(s) {bad} could not create a mailbox")
+        self._cpu_xrank = {"id": _CPU_CHANNELS[0], "epoch": 0, "err": 0}
+
+    def _poisoned(self) -> float:
+        if self.acc.is_floating_point:
+            return float("nan")
+        info = torch.iinfo(self.acc)
+        return {"min": info.max, "max": info.min}.get(self.cfg.op, 0)
+
+    def _cpu_exchange(self, out: torch.Tensor) -> None:
+        ch = self._cpu_xrank
+        ch["epoch"] += 1
+        if self.ctx.world_size == 1:
+            return
+        import datetime
+        import json
+        store = pdist._store()
+        base = f"mireduce/xrank/{ch['id']}/{ch['epoch']}/"
+        store.set(base + str(self.ctx.rank), json.dumps(out.reshape(-1)[0].item()))
+        keys = [base + str(r) for r in range(self.ctx.world_size)]
+        limit = 0.001 if ch["err"] else self.xrank_timeout_s  # a sticky error: a peer is gone, look once
+        try:
+            store.wait(keys, datetime.timedelta(seconds=limit))
+        except Exception:  # noqa: BLE001 - a peer's partial missed the timeout
+            ch["err"] |= 1
+            out.fill_(self._poisoned())
+            return
+        vals = [json.loads(store.get(k)) for k in keys]
+        op = self.cfg.op
+        acc = vals[0]
+        for v in vals[1:]:  # rank order: deterministic, like the kernel's lane-ordered fold
+            acc = min(acc, v) if op == "min" else max(acc, v) if op in ("max", "amax") else acc + v
+        out.fill_(acc)
 
     def use_collective(self, collective: str, streams: Optional[int] = None) -> None:
         """Re-bind for another cross-rank combine (e.g. fall back from ``fused`` to ``rccl``) and/or
@@ -220,7 +271,10 @@ class ScalarReduction:
         if collective not in COLLECTIVES:
             raise ValueError(f"collective must be one of {COLLECTIVES}")
         if self.ctx.device.type != "cuda":
+            self._cpu_xrank = None
             self.collective = collective
+            if collective == "fused":
+                self._open_cpu_channel()
             return
         dev = self.ctx.device
         torch.cuda.synchronize(dev)
@@ -293,6 +347,23 @@ class ScalarReduction:
             out.sub_(1) if self.cfg.op == "min" else out.add_(1)
         return None
 
+    def local_launcher(self, kernel: KernelConfig):
+        """(launch, error) for this rank's local reduction with another streaming-kernel plan —
+        ``launch(out)`` enqueues it on the current stream (one prepared launch on a workspace of
+        its own, no channel: capturable), ``error()`` reads that workspace's sticky fan-in error word.
+        Purely local (no collective, the bound combine untouched): bench.py's per-rank plan tuning
+        measures candidates with it on every rank independently."""
+        if self.ctx.device.type != "cuda":
+            return (lambda out: self.local(out)), (lambda: 0)
+        red = Reducer(self.ctx.device, config=kernel)
+        bound = red.bind(self.x, self.cfg.op, self.acc, out=self._bound_out)
+        dev = self.ctx.device
+
+        def launch(out: torch.Tensor) -> None:
+            bound.launch(_current_stream_handle(dev), out.data_ptr())
+        launch.plan = red.last_plan  # (the record of a candidate)
+        return launch, (lambda: int(red.ws.error()))
+
     def fork(self) -> None:
         """Multi-lane steps: make every lane's stream follow the caller's current stream (call
         before a batch of steps; inside a graph capture this is the fork of the captured DAG)."""
@@ -317,6 +388,9 @@ class ScalarReduction:
             self.local(out)
             if corrupt:
                 out.sub_(1) if self.cfg.op == "min" else out.add_(1)
+            if self.collective == "fused" and self._cpu_xrank is not None:
+                self._cpu_exchange(out)
+                return None
             return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op) if self.issues_collective else None
         stream, _, bound, _ = self.lanes[self._next % len(self.lanes)]
         self._next += 1
@@ -329,33 +403,32 @@ class ScalarReduction:
                 return pdist.scalar_allreduce(out, self.cfg.op, async_op=async_op)
         return None
 
-    def check(self) -> Optional[str]:
-        """None, or what went wrong in the launches so far, agreed over ranks (collective when a
-        process group spans several ranks; call after the launches):
-
-        * the polled fan-in's sticky error (a launch's finisher reached its wait bound: that launch
-          and every later one on the workspace wrote a poisoned result; the workspaces are reset);
-        * the fused finish's error words (a peer's partial never arrived, or arrived poisoned
-          because that peer's fan-in failed — then every rank's result is poisoned too)."""
+    def error_counts(self) -> list:
+        """This rank's device-side error words as counts, read locally (no collective):
+        [workspaces whose polled fan-in reached its bound, workspaces that saw a late XCD anchor,
+        channels that timed out waiting for a peer, channels that received a poisoned partial]."""
         if self.ctx.device.type != "cuda":
-            return None
-        dev = self.ctx.device
-        torch.cuda.synchronize(dev)
+            late = 1 if self._cpu_xrank is not None and self._cpu_xrank["err"] & 1 else 0
+            return [0, 0, late, 0]
+        torch.cuda.synchronize(self.ctx.device)
         fan_words = [int(red.ws.error()) for _, red, _, _ in self.lanes]
-        fan = sum(int(w != 0) for w in fan_words)
-        anchor = sum(int(w & 2 != 0) for w in fan_words)
         words = [int(ch.error()) for ch in self.channels]
-        late = sum(int(w & 1 != 0) for w in words)  # a peer's partial missed the timeout
-        pois = sum(int(w & 2 != 0) for w in words)  # a peer pushed a poisoned partial
-        if self.ctx.world_size > 1:
-            t = torch.tensor([fan, late, pois, anchor], dtype=torch.int64,
-                             device=dev if self.ctx.backend == "nccl" else "cpu")
-            torch.distributed.all_reduce(t)
-            fan, late, pois, anchor = (int(v) for v in t.tolist())
-        if fan:
-            for _, red, _, _ in self.lanes:
-                red.ws.reset(_current_stream_handle(dev))
-            torch.cuda.synchronize(dev)
+        return [sum(int(w != 0) for w in fan_words), sum(int(w & 2 != 0) for w in fan_words),
+                sum(int(w & 1 != 0) for w in words), sum(int(w & 2 != 0) for w in words)]
+
+    def reset_fanin(self) -> None:
+        """Clear the sticky fan-in errors of every lane's workspace (after they were reported)."""
+        if self.ctx.device.type != "cuda":
+            return
+        dev = self.ctx.device
+        for _, red, _, _ in self.lanes:
+            red.ws.reset(_current_stream_handle(dev))
+        torch.cuda.synchronize(dev)
+
+    @staticmethod
+    def describe_errors(counts) -> Optional[str]:
+        """The message for (summed) :meth:`error_counts`; None when all are zero."""
+        fan, anchor, late, pois = (int(v) for v in counts)
         msgs = []
         if fan:
             msgs.append(f"polled fan-in: {fan} workspace(s) reached the wait bound (results poisoned; reset)")
@@ -368,6 +441,24 @@ class ScalarReduction:
             msgs.append(f"fused cross-rank finish: {pois} channel(s) received a peer's poisoned partial "
                         "(its fan-in failed; results poisoned on every rank)")
         return "; ".join(msgs) or None
+
+    def check(self) -> Optional[str]:
+        """None, or what went wrong in the launches so far, agreed over ranks (collective when a
+        process group spans several ranks; call after the launches):
+
+        * the polled fan-in's sticky error (a launch's finisher reached its wait bound: that launch
+          and every later one on the workspace wrote a poisoned result; the workspaces are reset);
+        * the fused finish's error words (a peer's partial never arrived, or arrived poisoned
+          because that peer's fan-in failed — then every rank's result is poisoned too)."""
+        counts = self.error_counts()
+        if self.ctx.world_size > 1:
+            dev = self.ctx.device
+            t = torch.tensor(counts, dtype=torch.int64, device=dev if self.ctx.backend == "nccl" else "cpu")
+            torch.distributed.all_reduce(t)
+            counts = [int(v) for v in t.tolist()]
+        if counts[0]:
+            self.reset_fanin()
+        return self.describe_errors(counts)
 
     # ------------------------------------------------------------------ verify
     def reference(self, chunk: int = 1 << 24):

@@ -123,12 +123,18 @@ def _helper() -> int:
 
 
 def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int = 1 << 20,
-                 kind: str = "fused") -> Optional[str]:
+                 kind: str = "fused", fault=None, agree_timeout_s: float = 60.0) -> Optional[str]:
     """Collective over the default process group: None if every rank's helper ran the exchange
     correctly, else the agreed reason ("rank r: ..." for each failing rank). ``kind``: ``fused``
     (the fused cross-rank finish) or ``direct`` (the direct one-kernel collective and the peer-read
     probe, parallel/direct.py). World 1 maps no peer memory: None without a helper. ``dry`` (CPU
-    tests): helpers rendezvous and all-reduce over gloo only."""
+    tests): helpers rendezvous and all-reduce over gloo only.
+
+    The verdicts are agreed through :func:`.dist.agree` (bounded by ``agree_timeout_s``): a rank
+    whose own part failed in Python still reports (its verdict is the error), and a rank that died
+    or hangs raises :class:`.dist.PeerLost` on the others instead of holding them in a collective.
+    ``fault`` (utils.fault, site ``canary``) fires after this rank's helper ended."""
+    from .dist import agree
     import torch.distributed as dist
     if ctx.world_size == 1 or not dist.is_initialized():
         return None
@@ -186,8 +192,13 @@ def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int 
                 mine = f"helper did not finish within {timeout_s:g} s"
         except OSError as e:
             mine = f"could not start the helper: {e}"[:300]
-    verdicts = [None] * ctx.world_size
-    dist.all_gather_object(verdicts, mine)  # (every helper has ended: rank 0's store may go)
+    try:
+        if fault is not None:
+            fault.at(ctx.rank, fault.spec.step, "canary", "fused-finish canary")
+    except Exception as e:  # noqa: BLE001 - this rank's part failed: its verdict says so
+        mine = f"{type(e).__name__}: {e}"[:300]
+    # (every helper has ended: rank 0's store may go)
+    verdicts = [row["verdict"] for row in agree(ctx, f"canary ({kind})", {"verdict": mine}, agree_timeout_s)]
     del server
     # the root causes first: helpers that crashed or hung, then the ones that only lost a peer
     first = [f"rank {r}: {m}" for r, m in enumerate(verdicts) if m and ("crashed" in m or "did not finish" in m)]
@@ -199,7 +210,7 @@ def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int 
 def direct_canary(ctx, timeout_s: float = 90.0, dry: bool = False) -> Optional[str]:
     """:func:`fused_canary` for the direct one-kernel collective (bench.py runs it before its
     reduce.c table's direct rows and the xGMI peer-read probe)."""
-    return fused_canary(ctx, timeout_s=timeout_s, dry=dry, kind="direct")
+    return fused_canary(ctx, timeout_s=timeout_s, dry=dry, kind="direct", agree_timeout_s=timeout_s)
 
 
 if __name__ == "__main__":

@@ -25,7 +25,8 @@ import torch
 import torch.distributed as dist
 
 __all__ = ["DistContext", "init", "shutdown", "shard", "reduce_op", "scalar_allreduce",
-           "vector_reduce", "vector_allreduce", "loc_allreduce", "barrier", "max_over_ranks"]
+           "vector_reduce", "vector_allreduce", "loc_allreduce", "barrier", "max_over_ranks", "agree",
+           "PeerLost"]
 
 # The fused ops exchange already-transformed partials (sum of x^2, max |x|) and combine them
 # like SUM / MAX across ranks.
@@ -197,3 +198,48 @@ def max_over_ranks(value: float, ctx: DistContext) -> float:
                      device=ctx.device if ctx.backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+class PeerLost(RuntimeError):
+    """A bounded agreement (:func:`agree`) ended without every rank's report: the ``missing``
+    ranks died or hang, so no collective of the job can complete any more."""
+
+    def __init__(self, stage: str, missing: list, timeout_s: float):
+        self.stage, self.missing, self.timeout_s = stage, list(missing), timeout_s
+        who = ", ".join(str(r) for r in self.missing)
+        super().__init__(f"{stage}: rank(s) {who} did not report within {timeout_s:g} s (dead or hung)")
+
+
+_agree_seq = [0]
+
+
+def _store():
+    from torch.distributed import distributed_c10d as c10d
+    return c10d._get_default_store()
+
+
+def agree(ctx: DistContext, stage: str, payload: dict, timeout_s: float = 60.0) -> list:
+    """Every rank's ``payload`` (JSON-serialisable), in rank order, exchanged through the job's
+    rendezvous store instead of a process-group collective — so the wait is BOUNDED: a rank that
+    died or hangs is detected after ``timeout_s`` (:class:`PeerLost` names it) rather than waited on
+    until the process-group timeout, and a rank whose part of a stage raised still reports (its
+    payload carries the error). Every rank must call it the same number of times in the same order
+    (the keys carry a per-process sequence number). Used by bench.py's optional headline stages
+    (canary verdicts, the fused self-check, plan tuning), whose failure on any rank must turn into
+    an agreed fallback, not a hang (the reference ends every job by its wall
+    time, mpi/submit_all.sh:4)."""
+    import json
+    if ctx.world_size == 1 or not dist.is_initialized():
+        return [payload]
+    _agree_seq[0] += 1
+    base = f"mireduce/agree/{_agree_seq[0]}/{stage}/"
+    store = _store()
+    store.set(base + str(ctx.rank), json.dumps(payload))
+    keys = [base + str(r) for r in range(ctx.world_size)]
+    try:
+        store.wait(keys, datetime.timedelta(seconds=max(0.1, timeout_s)))
+    except Exception:  # noqa: BLE001 - a store timeout (DistStoreError / RuntimeError): find who is missing
+        missing = [r for r, k in enumerate(keys) if not store.check([k])]
+        if missing:
+            raise PeerLost(stage, missing, timeout_s) from None
+    return [json.loads(store.get(k)) for k in keys]

@@ -5,7 +5,7 @@ rank stalls until the SLURM walltime, mpi/submit_all.sh:4). Here every cross-ran
 deadline (process-group timeout, bootstrap deadline, RCCL async-error polling) and results are
 verified; ``--inject-fault`` provokes the failures those mechanisms exist for.
 
-Spec: ``KIND[@RANK][:STEP][/SITE]`` with KIND = exit | hang | corrupt | delay=<ms> | mailbox;
+Spec: ``KIND[@RANK][:STEP][/SITE]`` with KIND = exit | hang | raise | corrupt | delay=<ms> | mailbox;
 RANK defaults to 1, STEP to 0, SITE to ``step`` (also read from ``MIREDUCE_INJECT_FAULT``).
 
 * SITE ``step``: the measured steps of the headline (bench.py counts warm-up steps first);
@@ -19,6 +19,14 @@ RANK defaults to 1, STEP to 0, SITE to ``step`` (also read from ``MIREDUCE_INJEC
   ``init``: before the rank arms its result line or joins the process group (STEP ignored) — a
   rank that hangs there must still end the job within the headline deadline with exactly one
   diagnostic line (rank 0's, or the self-spawning parent's when rank 0 itself dies there).
+  ``canary`` / ``selfcheck`` / ``tune`` (STEP ignored): bench.py's optional headline stages — the
+  fused finish's canary (after this rank's helper ended, before the verdicts are agreed), its
+  self-check (before the three checked steps) and the per-rank plan tuning (before the candidates
+  are measured). A failure there on any rank must become an agreed fallback (RCCL combine / the
+  tuned default plan) with the headline still measured, or — for a rank that dies or hangs — one
+  diagnostic line naming the stage (bench.py, parallel.dist.agree).
+* KIND ``raise``: the rank raises :class:`InjectedFault` (a Python-level failure of that stage,
+  e.g. a plan the native layer rejects or an IPC error) instead of exiting or hanging.
 * KIND ``mailbox``: rank RANK fails to create its fused-finish mailbox
   (:func:`parallel.xrank.open_channel`); every rank must then agree on the RCCL fallback.
 """
@@ -30,10 +38,16 @@ import time
 from dataclasses import dataclass
 from typing import Optional
 
-__all__ = ["FaultSpec", "FaultInjector", "parse_fault_spec"]
+__all__ = ["FaultSpec", "FaultInjector", "InjectedFault", "parse_fault_spec"]
 
-KINDS = ("none", "exit", "hang", "corrupt", "delay", "mailbox")
-SITES = ("step", "extras", "teardown", "capture", "init")
+KINDS = ("none", "exit", "hang", "raise", "corrupt", "delay", "mailbox")
+SITES = ("step", "extras", "teardown", "capture", "init", "canary", "selfcheck", "tune")
+# sites that fire once per run wherever they are reached (their STEP is ignored)
+_STEPLESS = ("capture", "init", "teardown", "canary", "selfcheck", "tune")
+
+
+class InjectedFault(RuntimeError):
+    """The exception a ``raise`` fault throws."""
 
 
 @dataclass(frozen=True)
@@ -68,7 +82,7 @@ def parse_fault_spec(spec: Optional[str]) -> FaultSpec:
         delay = _count(kind[len("delay="):], spec)
         kind = "delay"
     if kind not in KINDS[1:]:
-        raise ValueError(f"bad fault spec {spec!r}: kind must be exit, hang, corrupt, delay=<ms> or mailbox")
+        raise ValueError(f"bad fault spec {spec!r}: kind must be exit, hang, raise, corrupt, delay=<ms> or mailbox")
     return FaultSpec(kind, 1 if rank is None else _count(rank, spec), 0 if step is None else _count(step, spec), delay,
                      site)
 
@@ -98,7 +112,7 @@ class FaultInjector:
         """Fire once at (rank, step) of ``site``. Returns True iff the caller must corrupt its local
         result."""
         s = self.spec
-        if self.fired or not self.on(site) or rank != s.rank or (step != s.step and site != "capture"):
+        if self.fired or not self.on(site) or rank != s.rank or (step != s.step and site not in _STEPLESS):
             return False
         self.fired = True
         print(f"[fault] rank {rank} {s.kind} at {label or site} {step}", file=sys.stderr, flush=True)
@@ -108,6 +122,8 @@ class FaultInjector:
         if s.kind == "hang":
             while True:
                 time.sleep(1)
+        if s.kind == "raise":
+            raise InjectedFault(f"injected fault at {label or site} (rank {rank})")
         if s.kind == "delay":
             time.sleep(s.delay_ms / 1000.0)
             return False

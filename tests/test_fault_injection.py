@@ -26,6 +26,87 @@ def _json(r):
     return json.loads(lines[0]) if lines else None
 
 
+REHEARSE = ["--gpus", "4", "--device", "cpu", "--elements", "200003", "--steps", "6", "--warmup", "2",
+            "--rehearse-stages", "--canary-timeout", "30", "--agree-timeout", "8", "--xrank-timeout", "2",
+            "--no-decompose"]
+STAGE = {"canary": "canary", "selfcheck": "fused self-check", "tune": "plan tuning"}
+
+
+@pytest.mark.parametrize("site", ["canary", "selfcheck", "tune"])
+@pytest.mark.parametrize("kind", ["raise", "hang", "exit"])
+def test_optional_headline_stage_failure_on_one_of_four_ranks(tmp_path, site, kind):
+    # the optional headline stages (the fused finish's canary and self-check, the
+    # per-rank plan tuning) fail on rank 2 of 4 (gloo CPU ranks; --rehearse-stages runs them in their
+    # CPU form). Whatever the failure, the job prints exactly one line within the budget:
+    #   raise -> an agreed fallback (RCCL combine / the tuned default plan), named, and a verified number;
+    #   hang  -> the bounded agreement names the stage and the lost rank, no number, rc != 0;
+    #   exit  -> torchrun tears the job down and rank 0's armed line names the stage, rc != 0.
+    t0 = time.time()
+    r = torchrun(4, [BENCH, *REHEARSE, "--inject-fault", f"{kind}@2/{site}"], cwd=tmp_path, timeout=300)
+    took = time.time() - t0
+    lines = [ln for ln in r.stdout.splitlines() if "{" in ln]
+    assert len(lines) == 1, (r.stdout, r.stderr[-3000:])
+    d = json.loads(lines[0][lines[0].index("{"):])
+    assert d["n_gpus"] == 4 and took < 120, (took, d)
+    assert f"[fault] rank 2 {kind} at" in r.stderr
+    if kind == "raise":
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert d["verified"] is True and d["value"] > 0
+        if site == "tune":
+            assert d["config"]["collective"] == "fused"
+            assert "rank 2: InjectedFault" in d["config"]["plan_reason"], d["config"]
+            assert d["summary"]["plans"] == "tuned default x4"
+        else:
+            assert d["config"]["collective"] == "rccl"
+            reason = d["config"]["collective_reason"]
+            assert reason.startswith("canary: rank 2: InjectedFault" if site == "canary" else
+                                     "self-check: rank 2: InjectedFault"), reason
+    else:
+        assert r.returncode != 0
+        assert d["value"] is None and f"(stage: {STAGE[site]})" in d["error"], d
+        if kind == "hang":
+            assert "rank(s) 2 did not report within 8 s" in d["error"], d
+        else:
+            assert "terminated" in d["error"] or "rank(s) 2 did not report" in d["error"], d
+
+
+def test_rehearsed_stages_pass_cleanly_on_four_ranks(tmp_path):
+    # no fault: the CPU forms of the canary, the fused self-check (store mailboxes) and plan tuning
+    # all pass; the headline runs over the fused finish's twin and verifies
+    from helpers import bench_record
+    r = torchrun(4, [BENCH, *REHEARSE], cwd=tmp_path, timeout=300,
+                 env={"MIREDUCE_EXTRAS_DIR": str(tmp_path)})
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = bench_record(r.stdout)
+    assert d["verified"] is True and d["config"]["collective"] == "fused" and "plan_reason" not in d["config"]
+    pt = d["plan_tuning"]
+    assert len(pt["plan_by_rank"]) == 4 and all(len(t) == 5 for t in pt["gbps_by_rank"]) and "error" not in pt
+
+
+def test_agree_is_bounded_and_names_the_missing_rank(tmp_path):
+    # parallel.dist.agree: payloads in rank order; a rank that never reports is named after the
+    # timeout (PeerLost) instead of holding the others in a collective
+    script = tmp_path / "ag.py"
+    script.write_text(
+        "import sys, time\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "from cuda_mpi_reductions_amd.parallel import dist as pdist\n"
+        "ctx = pdist.init(backend='gloo', device_type='cpu')\n"
+        "out = open(f'r{ctx.rank}.txt', 'w')\n"
+        "rows = pdist.agree(ctx, 'one', {'r': ctx.rank * 10})\n"
+        "out.write(f\"rows {[x['r'] for x in rows]}\\n\"); out.flush()\n"
+        "if ctx.rank == 2:\n"
+        "    time.sleep(8); sys.exit(0)\n"
+        "try:\n"
+        "    pdist.agree(ctx, 'two', {}, timeout_s=2)\n"
+        "except pdist.PeerLost as e:\n"
+        "    out.write(f'lost {e.missing} {e.stage}\\n')\n"
+        "out.close()\n")
+    torchrun(3, [str(script)], cwd=tmp_path, timeout=120)
+    got = [(tmp_path / f"r{r}.txt").read_text().splitlines() for r in range(3)]
+    assert got[0] == got[1] == ["rows [0, 10, 20]", "lost [2] two"] and got[2] == ["rows [0, 10, 20]"], got
+
+
 def test_parse_fault_spec():
     assert parse_fault_spec(None) == FaultSpec()
     assert parse_fault_spec("exit") == FaultSpec("exit", 1, 0, 0)
@@ -34,6 +115,15 @@ def test_parse_fault_spec():
     assert parse_fault_spec("corrupt:5") == FaultSpec("corrupt", 1, 5, 0)
     assert parse_fault_spec("hang@1/teardown") == FaultSpec("hang", 1, 0, 0, "teardown")
     assert parse_fault_spec("delay=500@0/capture") == FaultSpec("delay", 0, 0, 500, "capture")
+    assert parse_fault_spec("raise@2/tune") == FaultSpec("raise", 2, 0, 0, "tune")
+    for site in ("canary", "selfcheck"):
+        assert parse_fault_spec(f"hang@3/{site}").site == site
+    from cuda_mpi_reductions_amd.utils.fault import InjectedFault
+    inj = FaultInjector(parse_fault_spec("raise@1/selfcheck"))
+    assert not inj.at(1, 0, "tune")
+    with pytest.raises(InjectedFault):
+        inj.at(1, 7, "selfcheck")  # (stepless site: any step)
+    assert not inj.at(1, 7, "selfcheck")  # fires once
     for bad in ("boom", "exit@", "exit@x", "hang:-1", "delay=", "corrupt@1:2x"):
         with pytest.raises(ValueError):
             parse_fault_spec(bad)
@@ -265,3 +355,16 @@ def test_final_line_reinstalls_over_a_later_handler():
         "print('alive', flush=True)\n")
     assert r.returncode == 0, r.stderr
     assert r.stdout.splitlines() == ['{"value": 5}', "lib-handler", "alive"], r.stdout
+
+
+def test_final_line_leaves_an_ignored_signal_ignored():
+    # SIGHUP ignored before the first arm (nohup) stays ignored — it must not print the
+    # armed line and take the once-guard; the process goes on and its real line is the one printed
+    r = _final_line_child(
+        "signal.signal(signal.SIGHUP, signal.SIG_IGN)\n"
+        "C.arm_final_line('{\"value\": null}')\n"
+        "os.kill(os.getpid(), signal.SIGHUP)\n"
+        "time.sleep(0.3)\n"
+        "print('emitted' if C.emit_final_line('{\"value\": 6}') else 'lost', flush=True)\n")
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.splitlines() == ['{"value": 6}', "emitted"], r.stdout

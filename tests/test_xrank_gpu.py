@@ -498,6 +498,7 @@ def test_bench_ranks_hold_different_plans_and_verify(tmp_path, monkeypatch, plan
     # every candidate the tuner can choose (the self-check ran with the default plan before tuning)
     # must combine with the fused finish, next to a rank of another plan, and verify every step.
     monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    monkeypatch.setenv("MIREDUCE_TEST", "1")  # the hook is honoured in test runs only
     monkeypatch.setenv("MIREDUCE_PLAN_FOR_RANK", f"1={plan}")
     side = tmp_path / "x.json"
     r = torchrun(2, [BENCH, "--no-vector-extras", "--no-candidates", "--gpus", "2", "--backend", "gloo", "--steps", "8",

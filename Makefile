@@ -1,7 +1,10 @@
 # mireduce native build (gfx950 / MI355X). Replaces the reference's cuda/C/common/common.mk +
 # cuda/C/src/reduction/Makefile (sm_10/13/20) and mpi/Makefile (mpixlc / mpicc).
 #
-#   make            library, python extension, apps (reduction, reduce_xgmi, bandwidth_test, reduce_mpi)
+#   make            shared library (build/lib/libmireduce.so: every kernel + the host runtime), the python
+#                   extension and the apps (reduction, reduce_xgmi, bandwidth_test, reduce_mpi), all linked
+#                   against that one library — the kernel table is not embedded in every binary
+#   make static     build/lib/libmireduce.a (the same objects, for static consumers)
 #   make python     only the python extension (cuda_mpi_reductions_amd/_C*.so)
 #   make asan       host-code ASan/UBSan build of the CPU-only apps + unit tests (GPU code untouched)
 #   make tsan       ThreadSanitizer build of the threaded host reference reducers (race_unit)
@@ -40,12 +43,18 @@ KERNEL_OBJ  := $(patsubst csrc/%.hip,$(BUILD)/obj/%.o,$(KERNEL_SRC))
 RUNTIME_OBJ := $(patsubst csrc/%.cpp,$(BUILD)/obj/%.o,$(RUNTIME_SRC))
 COMM_OBJ    := $(patsubst csrc/%.cpp,$(BUILD)/obj/%.o,$(COMM_SRC)) $(patsubst csrc/%.hip,$(BUILD)/obj/%.o,$(COMM_HIP))
 LIB         := $(BUILD)/lib/libmireduce.a
+SHLIB       := $(BUILD)/lib/libmireduce.so
 COMMLIB     := $(BUILD)/lib/libmireduce_comm.a
+# binaries in build/bin and the extension in cuda_mpi_reductions_amd/ find the library next to them
+LINK_BIN    := -L$(BUILD)/lib -lmireduce -Wl,-rpath,'$$ORIGIN/../lib'
+LINK_PY     := -L$(BUILD)/lib -lmireduce -Wl,-rpath,'$$ORIGIN/../$(BUILD)/lib'
 
 APPS := $(BUILD)/bin/reduction $(BUILD)/bin/reduce_xgmi $(BUILD)/bin/bandwidth_test
 MPI_APP := $(BUILD)/bin/reduce_mpi
 
-.PHONY: all python apps mpi clean asan tsan unit diag examples window_ab dyntail_ab i32sum_ab launch_floor
+.PHONY: all python apps mpi clean asan tsan unit diag examples window_ab dyntail_ab i32sum_ab launch_floor static shared
+static: $(LIB)
+shared: $(SHLIB)
 all: python apps mpi unit diag examples
 
 python: $(PYEXT)
@@ -79,6 +88,10 @@ $(LIB): $(KERNEL_OBJ) $(RUNTIME_OBJ)
 	rm -f $@
 	ar rcs $@ $^
 
+$(SHLIB): $(KERNEL_OBJ) $(RUNTIME_OBJ)
+	@mkdir -p $(dir $@)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $^ -Wl,-soname,libmireduce.so $(LDLIBS) -o $@
+
 $(COMMLIB): $(COMM_OBJ)
 	@mkdir -p $(dir $@)
 	rm -f $@
@@ -88,13 +101,12 @@ $(BUILD)/obj/python/module.o: csrc/python/module.cpp $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HOSTCXX) $(HOSTFLAGS) -I$(PY_INC) -I$(PYBIND_INC) -fvisibility=hidden -c $< -o $@
 
-$(PYEXT): $(BUILD)/obj/python/module.o $(LIB)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive \
-	    $(LDLIBS) -o $@
+$(PYEXT): $(BUILD)/obj/python/module.o $(SHLIB)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $< $(LINK_PY) $(LDLIBS) -o $@
 
-$(BUILD)/bin/%: csrc/apps/%.cpp $(LIB) $(COMMLIB) $(HEADERS)
+$(BUILD)/bin/%: csrc/apps/%.cpp $(SHLIB) $(COMMLIB) $(HEADERS)
 	@mkdir -p $(dir $@)
-	$(HOSTCXX) $(HOSTFLAGS) $< -Wl,--whole-archive $(LIB) $(COMMLIB) -Wl,--no-whole-archive \
+	$(HOSTCXX) $(HOSTFLAGS) $< -Wl,--whole-archive $(COMMLIB) -Wl,--no-whole-archive $(LINK_BIN) \
 	    -L$(ROCM)/lib -lrccl $(LDLIBS) -o $@
 
 # reduce.c parity app: plain C++ against MPICH (CPU buffers only; no HIP needed).
@@ -115,18 +127,18 @@ window_ab: $(BUILD)/bin/window_ab
 $(BUILD)/obj/tools/window_ab.o: tools/window_ab.hip $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
-$(BUILD)/bin/window_ab: $(BUILD)/obj/tools/window_ab.o $(LIB)
+$(BUILD)/bin/window_ab: $(BUILD)/obj/tools/window_ab.o $(SHLIB)
 	@mkdir -p $(dir $@)
-	$(HIPCC) --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive $(LDLIBS) -o $@
+	$(HIPCC) --offload-arch=$(ARCH) $< $(LINK_BIN) $(LDLIBS) -o $@
 
 # Experiment: a workgroup-level dynamic tail vs the static XCD-weighted split (tools/dyntail_ab.hip).
 dyntail_ab: $(BUILD)/bin/dyntail_ab
 $(BUILD)/obj/tools/dyntail_ab.o: tools/dyntail_ab.hip $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
-$(BUILD)/bin/dyntail_ab: $(BUILD)/obj/tools/dyntail_ab.o $(LIB)
+$(BUILD)/bin/dyntail_ab: $(BUILD)/obj/tools/dyntail_ab.o $(SHLIB)
 	@mkdir -p $(dir $@)
-	$(HIPCC) --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive $(LDLIBS) -o $@
+	$(HIPCC) --offload-arch=$(ARCH) $< $(LINK_BIN) $(LDLIBS) -o $@
 
 # Where the per-launch fixed cost goes: empty / args / fan-in-only kernels vs the production
 # reduction, graph-replayed (tools/launch_floor.hip).
@@ -134,24 +146,24 @@ launch_floor: $(BUILD)/bin/launch_floor
 $(BUILD)/obj/tools/launch_floor.o: tools/launch_floor.hip $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
-$(BUILD)/bin/launch_floor: $(BUILD)/obj/tools/launch_floor.o $(LIB)
+$(BUILD)/bin/launch_floor: $(BUILD)/obj/tools/launch_floor.o $(SHLIB)
 	@mkdir -p $(dir $@)
-	$(HIPCC) --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive $(LDLIBS) -o $@
+	$(HIPCC) --offload-arch=$(ARCH) $< $(LINK_BIN) $(LDLIBS) -o $@
 
 # Experiment: int32 SUM with dot2 half-sums (tools/i32sum_ab.hip).
 i32sum_ab: $(BUILD)/bin/i32sum_ab
 $(BUILD)/obj/tools/i32sum_ab.o: tools/i32sum_ab.hip $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
-$(BUILD)/bin/i32sum_ab: $(BUILD)/obj/tools/i32sum_ab.o $(LIB)
+$(BUILD)/bin/i32sum_ab: $(BUILD)/obj/tools/i32sum_ab.o $(SHLIB)
 	@mkdir -p $(dir $@)
-	$(HIPCC) --offload-arch=$(ARCH) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive $(LDLIBS) -o $@
+	$(HIPCC) --offload-arch=$(ARCH) $< $(LINK_BIN) $(LDLIBS) -o $@
 
 # C++ library consumer example (examples/cpp_consumer; the CMake build links it via find_package).
 examples: $(BUILD)/bin/cpp_consumer
-$(BUILD)/bin/cpp_consumer: examples/cpp_consumer/main.cpp $(LIB) $(HEADERS)
+$(BUILD)/bin/cpp_consumer: examples/cpp_consumer/main.cpp $(SHLIB) $(HEADERS)
 	@mkdir -p $(dir $@)
-	$(HOSTCXX) $(HOSTFLAGS) $< -Wl,--whole-archive $(LIB) -Wl,--no-whole-archive $(LDLIBS) -o $@
+	$(HOSTCXX) $(HOSTFLAGS) $< $(LINK_BIN) $(LDLIBS) -o $@
 
 # Native unit tests (host code only) and the bootstrap multi-process test.
 UNIT := $(BUILD)/bin/host_unit $(BUILD)/bin/bootstrap_test
@@ -163,9 +175,9 @@ $(BUILD)/bin/host_unit: tests/native/host_unit.cpp $(UNIT_SRCS) $(HEADERS)
 	g++ $(CXXSTD) -O2 -Wall -Icsrc/include -I$(BUILD)/gen -DMIREDUCE_NO_HIP tests/native/host_unit.cpp \
 	    $(UNIT_SRCS) -o $@
 
-$(BUILD)/bin/bootstrap_test: tests/native/bootstrap_test.cpp $(COMMLIB) $(LIB) $(HEADERS)
+$(BUILD)/bin/bootstrap_test: tests/native/bootstrap_test.cpp $(COMMLIB) $(SHLIB) $(HEADERS)
 	@mkdir -p $(dir $@)
-	$(HOSTCXX) $(HOSTFLAGS) $< -Wl,--whole-archive $(COMMLIB) $(LIB) -Wl,--no-whole-archive \
+	$(HOSTCXX) $(HOSTFLAGS) $< -Wl,--whole-archive $(COMMLIB) -Wl,--no-whole-archive $(LINK_BIN) \
 	    -L$(ROCM)/lib -lrccl $(LDLIBS) -o $@
 
 # Host sanitizers: CPU-only code paths under ASan+UBSan.

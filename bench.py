@@ -285,7 +285,6 @@ def parse_args(argv=None):
     p.add_argument("--block", type=int, default=0)
     p.add_argument("--unroll", type=int, default=0)
     p.add_argument("--wg-per-cu", type=int, default=0)
-    p.add_argument("--groups", type=int, default=0)
     p.add_argument("--policy", choices=["auto", "nt", "default"], default="auto")
     p.add_argument("--no-plan-tune", dest="plan_tune", action="store_false",
                    help="--collective auto on GPUs also measures the streaming-kernel plan for the shard "
@@ -1560,7 +1559,6 @@ def _main(argv=None) -> int:
     at_stage("setup")
 
     kernel = KernelConfig(block=args.block, unroll=args.unroll, wg_per_cu=args.wg_per_cu,
-                          groups=args.groups,
                           nontemporal=None if args.policy == "auto" else args.policy == "nt",
                           single_pass=not args.two_pass)
     collective = args.collective

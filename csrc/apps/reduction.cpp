@@ -483,7 +483,7 @@ bool run_test(Options& o, Workspace& ws, hipStream_t s) {
     j.set("app", "reduction").set("method", op_name(o.op)).set("type", dtype_cli_name(o.dtype))
         .set("acc", dtype_cli_name(o.acc)).set("n", o.n).set("bytes", static_cast<uint64_t>(bytes))
         .set("kernel", o.kernel).set("block", r.plan.block).set("grid", r.plan.grid).set("unroll", r.plan.unroll).set("window", r.plan.window).set("segments", static_cast<int64_t>(r.plan.segments))
-        .set("groups", r.plan.groups).set("nontemporal", r.plan.nontemporal).set("cpufinal", o.cpufinal)
+        .set("nontemporal", r.plan.nontemporal).set("cpufinal", o.cpufinal)
         .set("iterations", o.iterations).set("cold", o.cold).set("timing", o.batch_timing && !o.cold ? "batch" : "per-iter").set("avg_ms", t.avg_ms).set("median_ms", st.median).set("min_ms", st.min)
         .set("max_ms", st.max).set("std_ms", st.stddev).set("gb_per_s", secs > 0 ? bytes / secs / kGB : 0.0)
         .set("gib_per_s", secs > 0 ? bytes / secs / kGiB : 0.0).set("bytes_per_GB", kGB)

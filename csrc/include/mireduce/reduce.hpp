@@ -27,9 +27,7 @@ struct ReduceConfig {
   int unroll = 0;         // independent 16-byte loads in flight per thread: 2 | 4 | 8 | 16
   int wg_per_cu = 0;      // persistent-grid occupancy target
   int max_blocks = 0;     // hard cap on the grid (reference --maxblocks)
-  int groups = 0;         // fan-in shards of the arrival ticket (<= 64)
   int policy = -1;        // streaming-load cache policy: -1 auto, 0 default, 1 non-temporal (nt)
-  int pipeline = -1;      // software-pipelined body: -1 auto, 0 off, 1 on (BLOCK*UNROLL <= 8192)
   // Streaming body's load schedule: -1 auto (tuned), 0 hipcc's own, 2 or 4 = an explicit window of
   // that many 16-byte loads per thread, the next one issued before the oldest is consumed
   // (non-temporal policy, 256/512 threads, unroll 2..8 divisible by it; otherwise hipcc's).
@@ -72,15 +70,9 @@ struct LaunchPlan {
   int block = 0;
   int unroll = 0;
   int grid = 0;
-  int groups = 0;
   bool nontemporal = true;
-  bool pipelined = false;
   int window = 0;      // explicit load window per thread (0: hipcc's schedule)
-  bool single_pass = true;
-  bool poll = false;   // single-pass fan-in: polled tagged slots (default, no tickets)
-  bool flat = false;   // ticketed fan-in: flat (final arriver folds every partial) vs two-level
-  bool contiguous = false;  // body split: one contiguous run of tiles per workgroup vs interleaved
-  bool balanced = false;    // interleaved: leftover tiles split evenly over all workgroups
+  bool single_pass = true;  // polled single-pass fan-in vs a second finalize launch (two-pass)
   int xskew = 0;            // window body: extra rounds for odd (> 0) / even (< 0) workgroups
   uint64_t head = 0;   // scalar elements before the first 16-B aligned vector
   uint64_t nvec = 0;   // 16-byte vectors in the streaming body
@@ -98,13 +90,15 @@ constexpr int64_t kSegmentBytes = int64_t{8} << 30;
 // workspace allowing `max_carry` carried results (min(256, max_grid)).
 void plan_segmentation(size_t n, DType t, const ReduceConfig& cfg, LaunchPlan& whole, int max_carry = 256);
 
-// Device scratch for one reduction stream: per-workgroup partials, per-group partials, the
-// arrival tickets (zeroed once; the last arriver of each launch resets them), the polled fan-in's
-// epoch-tagged slots and its state words (epoch, sticky error). One Workspace must not be used by
-// two concurrently running reductions.
+// Device scratch for one reduction stream: per-workgroup partials (two-pass mode, segmented
+// launches' carried results), the polled fan-in's epoch-tagged slots and its state words (epoch,
+// sticky error, XCD anchor) in uncached memory. One Workspace must not be used by two concurrently
+// running reductions. `slot_memory` is for experiments only (tools/launch_floor.hip): the fan-in
+// words in ordinary (coarse-grained) device memory instead of uncached.
+enum class SlotMemory { Uncached, Coarse };
 class Workspace {
  public:
-  explicit Workspace(int device = -1, int max_grid = 16384);
+  explicit Workspace(int device = -1, int max_grid = 16384, SlotMemory slot_memory = SlotMemory::Uncached);
   ~Workspace();
   Workspace(const Workspace&) = delete;
   Workspace& operator=(const Workspace&) = delete;
@@ -113,8 +107,6 @@ class Workspace {
   int num_cus() const { return num_cus_; }
   int max_grid() const { return max_grid_; }
   void* partials() const { return partials_; }
-  void* group_partials() const { return group_partials_; }
-  unsigned* tickets() const { return tickets_; }
   uint64_t* slots() const { return slots_; }
   unsigned* fan() const { return fan_; }
   // Sticky error word of the launches on this workspace (synchronous read: call after they
@@ -125,7 +117,7 @@ class Workspace {
   // one wrote a poisoned result (NaN, or the operator's identity for integers — for which this
   // word, not the value, is the signal) until reset(). (Value 2 (bit 1): a late XCD anchor.)
   unsigned error() const;
-  // Re-zero the tickets, fan-in slots and the sticky error (after an error or an aborted launch;
+  // Re-zero the fan-in slots and the sticky error (after an error or an aborted launch;
   // stream-ordered: no launch on this workspace may be running on another stream).
   void reset(hipStream_t stream);
 
@@ -134,14 +126,9 @@ class Workspace {
   int num_cus_ = 256;
   int max_grid_ = 0;
   void* partials_ = nullptr;
-  void* group_partials_ = nullptr;
-  unsigned* tickets_ = nullptr;
   uint64_t* slots_ = nullptr;  // polled fan-in: [max_grid][2] tagged words, uncached
   unsigned* fan_ = nullptr;    // polled fan-in: [0] epoch, [1] sticky error, uncached
 };
-
-constexpr int kTicketStride = 32;  // one counter per 128-byte line
-constexpr int kMaxGroups = 64;
 
 // The tuned plan depends on the element type, the size and (for 4- and 2-byte types) the operator:
 // see tuned_defaults in reduce.hip.

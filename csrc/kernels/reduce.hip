@@ -15,8 +15,8 @@ namespace {
 using namespace detail;
 
 int block_index(int b) { return b == 256 ? 0 : (b == 512 ? 1 : (b == 1024 ? 2 : -1)); }
-// Table body slot of a plan: 0 hipcc's schedule, 1 pipelined, 2 / 3 explicit window 2 / 4.
-int body_index(const LaunchPlan& p) { return p.window == 2 ? 2 : (p.window == 4 ? 3 : (p.pipelined ? 1 : 0)); }
+// Table body slot of a plan: 0 hipcc's schedule, 1 / 2 explicit window 2 / 4.
+int body_index(const LaunchPlan& p) { return p.window == 2 ? 1 : (p.window == 4 ? 2 : 0); }
 int unroll_index(int u) { return u == 2 ? 0 : (u == 4 ? 1 : (u == 8 ? 2 : (u == 16 ? 3 : -1))); }
 
 // combo index: (op, dtype, acc) → 0..28
@@ -90,7 +90,7 @@ const Table& table() {
 //   8 GB f16 max        512 x 4 x 1 7.18, 256 x 4 x 2 7.14 (profiles/r1_session3/tune_half.txt)
 // Fewer, fatter workgroups beat the "fill every wave slot" grid (8 WG/CU: 6.91 TB/s at 8 GB).
 struct Defaults {
-  int block, unroll, wg_per_cu, policy, pipeline, window;
+  int block, unroll, wg_per_cu, policy, window;
 };
 Defaults tuned_defaults(size_t bytes, DType t, Op op) {
   constexpr size_t MB = 1ull << 20;
@@ -116,36 +116,17 @@ Defaults tuned_defaults(size_t bytes, DType t, Op op) {
   // window-4 plan at 7.13 and 256x8x2 window 2 at 7.25 (8 GB f16 MAX; the old 256x4x2: 7.16).
   const bool widening_int = t == DType::Int32 && (op == Op::Sum || op == Op::SumSq);
   const bool half_cmp = dtype_is_half(t) && op != Op::Sum && op != Op::SumSq;
-  if (dtype_size(t) == 8 && bytes > 192 * MB) return {256, 8, 1, 1, 0, 4};
-  if ((widening_int || half_cmp) && bytes > 192 * MB) return {256, 8, 2, 1, 0, 2};
-  if (dtype_size(t) <= 4 && bytes > 192 * MB) return {256, 8, 1, 1, 0, 4};
+  if (dtype_size(t) == 8 && bytes > 192 * MB) return {256, 8, 1, 1, 4};
+  if ((widening_int || half_cmp) && bytes > 192 * MB) return {256, 8, 2, 1, 2};
+  if (dtype_size(t) <= 4 && bytes > 192 * MB) return {256, 8, 1, 1, 4};
   // <= 192 MB: 256x4x3 with hipcc's schedule. (256x8x2 window 2 led tune.py's back-to-back launches
   // at 64-192 MiB by 0.5-4 %, but not the reduction app's per-iteration timing at the reference's
   // 2^24 doubles, warm or cold: profiles/r3_types/small/.)
-  return {256, 4, 3, 1, 0, 0};
+  return {256, 4, 3, 1, 0};
 }
-constexpr int kDefaultGroups = 8;
-constexpr int kOneGroupGrid = 64;
-
-// Fan-in shape of the single-pass finalisation: 0 tree, 1 flat (ticketed), 2 poll (default);
-// MIREDUCE_FANIN=poll|flat|tree overrides (A/B runs).
-int fanin_mode() {
-  static const int v = [] {
-    const char* e = std::getenv("MIREDUCE_FANIN");
-    if (e && std::strcmp(e, "tree") == 0) return 0;
-    if (e && std::strcmp(e, "flat") == 0) return 1;
-    return 2;
-  }();
-  return v;
-}
-
-// Balanced leftover: MIREDUCE_BALANCE=1 opts in (read per plan). Off by default: measured equal
-// within noise at 128 MiB - 4 GB for four plans (profiles/r2_small/balance_ab.txt) — the
-// bandwidth the idle workgroups free up already lets the few with an extra tile finish early.
-bool balance_leftover() {
-  const char* e = std::getenv("MIREDUCE_BALANCE");
-  return e && std::strcmp(e, "1") == 0;
-}
+// (Round 6 removed the measured-null plan options: the software-pipelined body, the ticketed
+// flat / tree fan-ins, the balanced leftover and the contiguous split — docs/TUNING.md keeps their
+// measurements: profiles/r1_bench/fanin_ab.txt, r2_small/balance_ab.txt, r1_session4/split_ab/.)
 
 // XCD-weighted split default (permille of the rounds per workgroup given extra to the workgroups
 // on odd XCCs; see plan_reduce, weighted_tiles and XcdAnchor). Measured per plan with the anchored
@@ -168,15 +149,6 @@ int tuned_xcd_skew(DType t, const LaunchPlan& p, int num_cus) {
   const size_t es = dtype_size(t);
   if (num_cus < kSpxCus) return 0;
   return (es == 8 || es == 4) && p.window == 4 ? 20 : 0;
-}
-
-// Work split of the streaming body; MIREDUCE_SPLIT=stride|contig overrides (A/B runs; read per
-// plan so one process can compare both).
-bool split_contiguous() {
-  const char* e = std::getenv("MIREDUCE_SPLIT");
-  if (e && std::strcmp(e, "contig") == 0) return true;
-  if (e && std::strcmp(e, "stride") == 0) return false;
-  return false;
 }
 
 // `fan` non-null: the second level of a two-pass reduce_stream launch, which ends its fan-in epoch
@@ -243,7 +215,7 @@ void combine_by_type(DType t, void* inout, const void* other, uint64_t n, hipStr
 
 // ----------------------------------------------------------------------------------------------
 
-Workspace::Workspace(int device, int max_grid) : max_grid_(max_grid) {
+Workspace::Workspace(int device, int max_grid, SlotMemory slot_memory) : max_grid_(max_grid) {
   MIREDUCE_REQUIRE(max_grid >= 1, "Workspace: max_grid must be positive");
   if (device < 0) MIREDUCE_HIP_THROW(hipGetDevice(&device));
   device_ = device;
@@ -254,15 +226,10 @@ Workspace::Workspace(int device, int max_grid) : max_grid_(max_grid) {
   MIREDUCE_HIP_THROW(hipGetDevice(&prev));
   MIREDUCE_HIP_THROW(hipSetDevice(device));
   MIREDUCE_HIP_THROW(hipMalloc(&partials_, static_cast<size_t>(max_grid) * 8));
-  MIREDUCE_HIP_THROW(hipMalloc(&group_partials_, static_cast<size_t>(kMaxGroups) * 8));
-  const size_t tbytes = static_cast<size_t>(kMaxGroups + 1) * kTicketStride * sizeof(unsigned);
-  MIREDUCE_HIP_THROW(hipMalloc(reinterpret_cast<void**>(&tickets_), tbytes));
-  MIREDUCE_HIP_THROW(hipMemset(tickets_, 0, tbytes));
-  // polled fan-in slots: uncached, so the finisher's polls see every XCD's stores.
-  // MIREDUCE_SLOTS=coarse (A/B runs, tools/launch_floor.hip): ordinary device memory instead, relying
-  // on the agent-scope atomics alone for cross-XCD visibility.
-  const char* sm = std::getenv("MIREDUCE_SLOTS");
-  const unsigned flags = sm && std::strcmp(sm, "coarse") == 0 ? hipDeviceMallocDefault : hipDeviceMallocUncached;
+  // polled fan-in slots: uncached, so the finisher's polls see every XCD's stores. SlotMemory::Coarse
+  // (experiments only, tools/launch_floor.hip): ordinary device memory instead, relying on the
+  // agent-scope atomics alone for cross-XCD visibility.
+  const unsigned flags = slot_memory == SlotMemory::Coarse ? hipDeviceMallocDefault : hipDeviceMallocUncached;
   MIREDUCE_HIP_THROW(hipExtMallocWithFlags(reinterpret_cast<void**>(&slots_), static_cast<size_t>(max_grid) * 16,
                                            flags));
   MIREDUCE_HIP_THROW(hipMemset(slots_, 0, static_cast<size_t>(max_grid) * 16));
@@ -274,8 +241,6 @@ Workspace::Workspace(int device, int max_grid) : max_grid_(max_grid) {
 
 Workspace::~Workspace() {
   (void)hipFree(partials_);
-  (void)hipFree(group_partials_);
-  (void)hipFree(tickets_);
   (void)hipFree(slots_);
   (void)hipFree(fan_);
 }
@@ -292,8 +257,6 @@ unsigned Workspace::error() const {
 }
 
 void Workspace::reset(hipStream_t stream) {
-  const size_t tbytes = static_cast<size_t>(kMaxGroups + 1) * kTicketStride * sizeof(unsigned);
-  MIREDUCE_HIP_THROW(hipMemsetAsync(tickets_, 0, tbytes, stream));
   MIREDUCE_HIP_THROW(hipMemsetAsync(slots_, 0, static_cast<size_t>(max_grid_) * 16, stream));
   // the epoch may stay: every slot is 0 now, and epochs start at 1
   MIREDUCE_HIP_THROW(hipMemsetAsync(fan_ + 1, 0, sizeof(unsigned), stream));
@@ -310,16 +273,15 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   p.single_pass = cfg.single_pass;
   MIREDUCE_REQUIRE(cfg.xrank == nullptr || cfg.single_pass,
                    "the fused cross-rank finish needs the single-pass kernel");
-  p.pipelined = (cfg.pipeline < 0 ? d.pipeline == 1 : cfg.pipeline == 1) && p.block * p.unroll <= 8192;
   MIREDUCE_REQUIRE(block_index(p.block) >= 0, "block must be 256, 512 or 1024");
   MIREDUCE_REQUIRE(unroll_index(p.unroll) >= 0, "unroll must be 2, 4, 8 or 16");
   MIREDUCE_REQUIRE(cfg.window == -1 || cfg.window == 0 || cfg.window == 2 || cfg.window == 4,
                    "window must be 0, 2 or 4");
-  {  // an explicit window where one is instantiated (non-temporal, not pipelined), else hipcc's schedule
+  {  // an explicit window where one is instantiated (non-temporal), else hipcc's schedule
     const int w = cfg.window < 0 ? d.window : cfg.window;
     const bool explicit_plan = cfg.block || cfg.unroll;  // a window tuned for the default plan only
     const int wd = cfg.window < 0 && explicit_plan ? 0 : w;
-    p.window = (wd > 0 && p.nontemporal && !p.pipelined && window_ok(p.block, p.unroll, wd)) ? wd : 0;
+    p.window = (wd > 0 && p.nontemporal && window_ok(p.block, p.unroll, wd)) ? wd : 0;
   }
   const size_t vec = 16 / es;
   const uintptr_t addr = reinterpret_cast<uintptr_t>(in);
@@ -341,23 +303,12 @@ LaunchPlan plan_reduce(const void* in, size_t n, DType t, const ReduceConfig& cf
   if (want > static_cast<uint64_t>(max_grid)) want = max_grid;
   if (want < 1) want = 1;
   p.grid = static_cast<int>(want);
-  // Arrival counters: one for small grids (<= kOneGroupGrid arrivals contend little, and the
-  // finisher then skips the second ticket round trip), kDefaultGroups shards above.
-  int groups = cfg.groups ? cfg.groups : (static_cast<int>(want) <= kOneGroupGrid ? 1 : kDefaultGroups);
-  if (groups > kMaxGroups) groups = kMaxGroups;
-  if (groups > p.grid) groups = p.grid;
-  p.groups = p.single_pass ? groups : 0;
-  p.poll = p.single_pass && fanin_mode() == 2;
-  p.flat = p.single_pass && fanin_mode() == 1;
-  p.contiguous = split_contiguous();
-  p.balanced = !p.contiguous && balance_leftover();
   // XCD-weighted split (window bodies, interleaved, even grids): permille of the rounds per
   // workgroup -> extra rounds for one parity. MIREDUCE_XCD_SKEW=<permille> overrides the tuned
   // default (A/B runs).
   // Launches with a fan-in epoch only (the polled fan-in, or two-pass: its finalize ends the epoch):
   // the kernel anchors the favoured parity to the XCDs with it.
-  if (p.window > 0 && !p.contiguous && !p.balanced && p.grid % 2 == 0 && (p.poll || !p.single_pass) &&
-      p.grid > 1) {
+  if (p.window > 0 && p.grid % 2 == 0 && p.grid > 1) {
     // (the env override replaces the tuned default only: a caller's explicit skew — e.g. bench.py's
     // plan-tuning candidates — is what it says)
     bool tuned = cfg.xcd_skew == (-2147483647 - 1);
@@ -394,8 +345,6 @@ static kern::Args make_args(const void* in, const LaunchPlan& p, DType t, const 
   a.head = p.head;
   a.nvec = p.nvec;
   a.tail = p.tail;
-  a.contig = p.contiguous ? 1 : 0;
-  a.balance = p.balanced ? 1 : 0;
   a.xskew = p.xskew;
   {  // the weighted split's common / extra rounds (weighted_tiles), precomputed here
     const uint64_t tile = static_cast<uint64_t>(p.block) * static_cast<uint64_t>(p.unroll);
@@ -434,7 +383,7 @@ struct Segments {
 };
 static Segments plan_segments(size_t n, size_t es, const ReduceConfig& cfg, const LaunchPlan& whole, int max_carry) {
   Segments sg;
-  if (!whole.poll || !whole.single_pass || cfg.segment_bytes < 0 || n == 0) return sg;
+  if (!whole.single_pass || cfg.segment_bytes < 0 || n == 0) return sg;
   const uint64_t bytes = static_cast<uint64_t>(n) * es;
   if (cfg.segment_bytes == 0 && bytes <= 2 * static_cast<uint64_t>(kSegmentBytes)) return sg;
   constexpr uint64_t kMiB = 1ull << 20;
@@ -470,12 +419,9 @@ Launch make_launch(const void* in, size_t n, DType t, Op op, int c, void* out, W
   const LaunchPlan& p = L.plan;
   kern::Args a = make_args(in, p, t, cfg);
   a.partials = ws.partials();
-  a.group_partials = ws.group_partials();
-  a.tickets = ws.tickets();
   a.out = out;
-  a.groups = p.groups;
-  a.flat = p.flat ? 1 : 0;
-  a.slots = p.poll ? ws.slots() : nullptr;
+  a.two_pass = p.single_pass ? 0 : 1;
+  a.slots = p.single_pass ? ws.slots() : nullptr;
   a.fan = ws.fan();
   a.fan_slots = static_cast<unsigned>(ws.max_grid());
   a.two_pass_epoch = p.single_pass ? 0 : 1;
@@ -513,8 +459,8 @@ std::vector<Launch> make_launches(const void* in, size_t n, DType t, Op op, DTyp
                             last ? carry : nullptr, last ? static_cast<unsigned>(sg.count - 1) : 0u));
   }
   // the carried results are folded by the last launch's polled finisher only
-  MIREDUCE_REQUIRE(v.back().plan.poll && v.back().plan.grid > 1, "segmented reduction: the last segment's plan "
-                   "has no polled multi-workgroup fan-in (segment too small)");
+  MIREDUCE_REQUIRE(v.back().plan.single_pass && v.back().plan.grid > 1, "segmented reduction: the last segment's "
+                   "plan has no polled multi-workgroup fan-in (segment too small)");
   v[0].plan.segments = sg.count;
   v[0].plan.segment_elems = sg.elems;
   return v;
@@ -595,7 +541,7 @@ LaunchPlan reduce_partials(const void* in, size_t n, DType t, Op op, DType acc, 
   p.xskew = 0;  // no workspace, so no fan-in epoch to anchor the XCD-weighted split with: equal rounds
   kern::Args a = make_args(in, p, t, c2);
   a.partials = partials;
-  a.groups = 0;
+  a.two_pass = 1;
   const LaunchFn fn = table().fn[c][block_index(p.block)][unroll_index(p.unroll)][p.nontemporal ? 1 : 0][body_index(p)];
   fn(a, p.grid, stream);
   MIREDUCE_HIP_THROW(hipGetLastError());
@@ -651,10 +597,8 @@ std::vector<std::string> compiled_variants() {
   for (int b : kBlocks)
     for (int u : kUnrolls)
       for (int nt = 0; nt < 2; ++nt) {
-        for (int pp = 0; pp < 2; ++pp)
-          if (!pp || b * u <= 8192)
-            v.push_back("block=" + std::to_string(b) + " unroll=" + std::to_string(u) +
-                        (nt ? " policy=nt" : " policy=default") + (pp ? " pipelined" : ""));
+        v.push_back("block=" + std::to_string(b) + " unroll=" + std::to_string(u) +
+                    (nt ? " policy=nt" : " policy=default"));
         for (int w : {2, 4})
           if (nt && window_ok(b, u, w))
             v.push_back("block=" + std::to_string(b) + " unroll=" + std::to_string(u) + " policy=nt window=" +

@@ -13,13 +13,15 @@
 //   * wave64 butterfly (__shfl_xor over 64 lanes) instead of the 32-lane volatile tail
 //     (reduction_kernel.cu:110-122 assumes warp lockstep — wrong on CDNA), then one LDS slot per
 //     wave;
-//   * single launch: each workgroup publishes its partial write-through (sc1), drains, and takes
-//     an agent-scope ticket on one of G sharded counters; the last arriver of each group takes a
-//     ticket on the top counter and the last of those folds every partial in one parallel sc1
-//     load round (threadFenceReduction_kernel.cu:116-171 idea, but with the gfx950
-//     release/acquire forms and a sharded fan-in: one counter for 2048 arrivals costs ~25 us,
-//     eight counters ~3 us). MIREDUCE_FANIN=tree selects the older two-level fold (each group's
-//     last arriver folds and republishes its group first).
+//   * single launch with a polled fan-in: every workgroup stores its partial as two epoch-tagged
+//     words (no ticket, no drain) and the last-indexed workgroup polls them all, folds them in slot
+//     order and finishes (threadFenceReduction_kernel.cu:116-171 idea, without its atomic ticket:
+//     one counter for 2048 arrivals costs ~25 us, the polled finish ~1.5 us); a two-pass mode
+//     (partials, then a one-workgroup finalize) serves the reference's multi-pass / --cpufinal paths.
+// Round 6 pruned the bodies measured as no gain (docs/TUNING.md): the software-pipelined body, the
+// strict load window (tools/window_ab.hip keeps it as a control), the contiguous and balanced-leftover
+// splits and the ticketed flat / tree fan-ins. One body per plan ships: hipcc's schedule of the plain
+// loop (<= 192 MB) or the explicit load window (above), over the interleaved (XCD-weighted) split.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -71,28 +73,22 @@ struct Args {
   uint64_t head;         // scalar elements before `body`
   uint64_t nvec;         // 16-byte vectors
   uint64_t tail;         // scalar elements after the body
-  void* partials;        // [gridDim.x] AccT
-  void* group_partials;  // [groups] AccT
-  unsigned* tickets;     // [(groups + 1) * kTicketStride]
+  void* partials;        // two-pass mode: [gridDim.x] AccT
   void* out;             // AccT[1]
-  int groups;            // 0: two-pass mode (write partials only)
-  int flat;              // 1: group last-arrivers only count; the final arriver folds every partial
-  int contig;            // 1: workgroup b streams one contiguous run of tiles; 0: tiles b, b+grid, ...
+  int two_pass;          // 1: write partials only (the finalize kernel folds them after a kernel boundary)
   const XrankDesc* xrank;  // non-null: fold the ranks' partials in-kernel before writing out (xrank.hpp)
-  uint64_t* slots;         // non-null: polled fan-in (no tickets), [gridDim.x][2] epoch-tagged words
+  uint64_t* slots;         // single pass: the polled fan-in's [gridDim.x][2] epoch-tagged words (Workspace)
   unsigned* fan;           // polled fan-in state (Workspace): [0] epoch = finished launches, [1] sticky error,
                            // [2..3] the XCD anchor of the weighted split (XcdAnchor)
   uint64_t fan_bound;      // polled fan-in: finisher's wait bound in wall-clock ticks
   unsigned fan_slots;      // polled fan-in: slots in the workspace (all zeroed when the epoch wraps)
-  int balance;             // 1 (interleaved split): whole rounds of tiles, then the leftover < grid
-                           // tiles split evenly over ALL workgroups (no one-tile tail on a few)
   int delay_wg;            // test hook (ReduceConfig::debug_delay_wg): this workgroup sleeps
   uint64_t delay_ticks;    // delay_ticks before publishing its partial; -1 = none
   uint64_t anchor_delay;   // test hook (ReduceConfig::debug_delay_anchor_ticks): workgroup 0 sleeps this
                            // long before publishing the XCD anchor; 0 = none
   uint64_t* wg_stamps;     // diagnostic (ReduceConfig::debug_wg_stamps): per-workgroup end stamps
-  int xskew;               // XCD-weighted split (window bodies, interleaved): |xskew| extra rounds of
-                           // tiles for the workgroups on odd (xskew > 0) or even (< 0) XCCs; 0 = equal
+  int xskew;               // XCD-weighted split (window bodies): |xskew| extra rounds of tiles for the
+                           // workgroups on odd (xskew > 0) or even (< 0) XCCs; 0 = equal
   uint64_t x_ra;           // weighted split, precomputed on the host: common rounds (ntiles / grid at 0)
   uint64_t x_dd;           // extra rounds actually given to the favoured parity
   int two_pass_epoch;      // two-pass launch whose finalize ends the fan-in epoch (fan[0]; XcdAnchor)
@@ -264,9 +260,10 @@ __device__ __forceinline__ void consume_tile(AccT (&acc)[UNROLL], const V (&v)[U
   }
 }
 
-// Explicit load window: the thread's loads over its tiles t0, t0+step, ... < t1 form one sequence
+// Explicit load window (stream_window_seq below): the thread's loads over its tiles form one sequence
 // held in WIN registers — each step issues the load WIN ahead and then consumes the oldest (so
-// WIN + 1 are in flight at each issue, WIN after each wait; STRICT consumes first: WIN at most);
+// WIN + 1 are in flight at each issue, WIN after each wait; the strict form that consumes first,
+// WIN at most, is kept as a control in tools/window_ab.hip);
 // a sched_barrier between steps pins the interleave (hipcc's own grouping of the plain body moves
 // with unrelated code in the kernel: profiles/r3_regress). Measured (profiles/r3_window/): the
 // loose form with ~18-20 loads in flight per CU is fastest (256x8x1 with 4: 8 GB 1092 vs 1112 us
@@ -284,43 +281,6 @@ __device__ __forceinline__ V ld_buf_nt(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
-}
-
-template <class OpT, class T, class AccT, class V, int N, int BLOCK, int UNROLL, int WIN, bool STRICT = true>
-__device__ __forceinline__ void stream_window(AccT (&acc)[UNROLL], const V* __restrict__ vin, uint64_t t0,
-                                              uint64_t t1, uint64_t step) {
-  static_assert(UNROLL % WIN == 0, "the window must divide the unroll");
-  constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
-  constexpr uint32_t kStride = BLOCK * 16;  // bytes between a lane's loads within a tile
-  if (t0 >= t1) return;
-  const uint32_t voff = threadIdx.x * 16;
-  __amdgpu_buffer_rsrc_t rp = tile_rsrc(vin + t0 * kTile);
-  V buf[WIN];
-#pragma unroll
-  for (int j = 0; j < WIN; ++j) buf[j] = ld_buf_nt<V>(rp, voff, j * kStride);
-  uint64_t t = t0;
-  for (; t + step < t1; t += step) {
-    const __amdgpu_buffer_rsrc_t rq = tile_rsrc(vin + (t + step) * kTile);
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-#pragma unroll
-      for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(buf[u % WIN], k)));
-      // STRICT: the consume completes before the next load issues (at most WIN in flight);
-      // otherwise hipcc hoists the load above the consume (WIN + 1 in flight at its issue).
-      if constexpr (STRICT) __builtin_amdgcn_sched_barrier(0);
-      const int j = u + WIN;
-      buf[u % WIN] = j < UNROLL ? ld_buf_nt<V>(rp, voff, j * kStride) : ld_buf_nt<V>(rq, voff, (j - UNROLL) * kStride);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    rp = rq;
-  }
-#pragma unroll
-  for (int u = 0; u < UNROLL; ++u) {  // the last tile: no loads of a next one
-#pragma unroll
-    for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(buf[u % WIN], k)));
-    const int j = u + WIN;
-    if (j < UNROLL) buf[u % WIN] = ld_buf_nt<V>(rp, voff, j * kStride);
-  }
 }
 
 // The tiles one workgroup streams as up to three arithmetic runs (the XCD-weighted split): run 0
@@ -538,15 +498,14 @@ __device__ __forceinline__ uint32_t stream_window_seq(AccT (&acc)[UNROLL], const
   return total;
 }
 
-// PIPE: software-pipelined body — tile t+grid's loads are issued before tile t is consumed, so
-// a wave always has UNROLL loads in flight while it computes (two register sets). The loop has
-// no per-load condition (the last tile is peeled), see cdna_hip_programming.md §5 trap (c).
-template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT, bool PIPE, int WIN = 0>
+// One streaming body per plan: WIN > 0 the explicit load window over the (XCD-weighted) interleaved
+// split, WIN == 0 hipcc's schedule of the plain loop over tiles b, b + grid, ... The loop has no
+// per-load condition (cdna_hip_programming.md §5 trap (c)).
+template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT, int WIN = 0>
 __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   using V = typename Vec16<T>::type;
   constexpr int N = Vec16<T>::N;
   __shared__ AccT lds[BLOCK / 64];
-  __shared__ int is_last;
 
   AccT acc[UNROLL];
 #pragma unroll
@@ -564,61 +523,13 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
   const V* __restrict__ vin = static_cast<const V*>(a.body);
   constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
   const uint64_t ntiles = a.nvec / kTile;
-  // This workgroup's full tiles: t0, t0 + step, ... < t1 (interleaved over the grid, or one
-  // contiguous run of ntiles / grid tiles each).
   const uint64_t grid = gridDim.x;
-  const bool balanced = a.balance && !a.contig;
-  const uint64_t full = balanced ? ntiles / grid * grid : ntiles;  // tiles streamed in whole rounds
-  const uint64_t t0 = a.contig ? blockIdx.x * ntiles / grid : blockIdx.x;
-  const uint64_t t1 = a.contig ? (blockIdx.x + 1) * ntiles / grid : full;
-  const uint64_t step = a.contig ? 1 : grid;
-  // Balanced mode: the leftover after the whole rounds (< grid tiles + the sub-tile remainder) is
-  // split into one even, contiguous piece per workgroup (< one tile each, so <= UNROLL loads per
-  // thread, their count `nl` uniform over the workgroup). With an explicit window the piece is
-  // loaded BEFORE the body and consumed after it: it costs no extra memory round trip at the end,
-  // where the kernel's last workgroups decide its duration.
-  V pre_v[WIN > 0 ? UNROLL : 1];
-  uint64_t pre_s0 = 0, pre_s1 = 0;
-  int pre_n = 0;
-  if constexpr (WIN > 0) {
-    if (balanced) {
-      const uint64_t l0 = full * kTile, left = a.nvec - l0;
-      pre_s0 = l0 + left * blockIdx.x / grid;
-      pre_s1 = l0 + left * (blockIdx.x + 1) / grid;
-      pre_n = static_cast<int>((pre_s1 - pre_s0 + BLOCK - 1) / BLOCK);
-#pragma unroll
-      for (int u = 0; u < UNROLL; ++u) {
-        if (u < pre_n) {
-          const uint64_t idx = pre_s0 + threadIdx.x + static_cast<uint64_t>(u) * BLOCK;
-          pre_v[u] = __builtin_nontemporal_load(vin + (idx < pre_s1 ? idx : pre_s0));
-        }
-      }
-    }
-  }
   uint32_t streamed = 0;  // full tiles of the window body (diagnostic stamps)
   bool anchor_late = false;  // the XCD anchor missed its bound: this workgroup's tiles may overlap others
-  if constexpr (PIPE) {
-    if (t0 < t1) {
-      V cur[UNROLL];
-      load_tile<V, BLOCK, UNROLL, NT>(cur, vin + t0 * kTile + threadIdx.x);
-      for (uint64_t tn = t0 + step; tn < t1; tn += step) {
-        V nxt[UNROLL];
-        load_tile<V, BLOCK, UNROLL, NT>(nxt, vin + tn * kTile + threadIdx.x);
-        consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, cur);
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) cur[u] = nxt[u];
-      }
-      consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, cur);
-    }
-  } else if constexpr (WIN > 0) {
-    // one window body for every split: contiguous runs, whole rounds (balanced), or interleaved
+  if constexpr (WIN > 0) {
     TileSeq q{};
     XcdAnchor x{};
-    if (a.contig || balanced) {
-      q.s0 = t0;
-      q.st0 = step;
-      q.n0 = t1 > t0 ? static_cast<uint32_t>((t1 - t0 + step - 1) / step) : 0u;
-    } else if (a.xskew != 0 && epoch && (grid & 1u) == 0 && a.x_ra > 0) {  // weighted, anchored to the XCDs
+    if (a.xskew != 0 && epoch && (grid & 1u) == 0 && a.x_ra > 0) {  // weighted, anchored to the XCDs
       q.s0 = blockIdx.x;
       q.st0 = grid;
       q.n0 = static_cast<uint32_t>(a.x_ra);
@@ -636,57 +547,19 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     // fan_raw (the launch's fan-in epoch, the anchor's tag) passed as is: a copy into the struct
     // would be a VGPR move that waits for its load before the first tile's loads issue
     streamed = stream_window_seq<OpT, T, AccT, V, N, BLOCK, UNROLL, WIN>(acc, vin, q, x, fan_raw, anchor_late);
-  } else if constexpr (WIN < 0) {  // strict window (experiments only: tools/window_ab.hip)
-    stream_window<OpT, T, AccT, V, N, BLOCK, UNROLL, -WIN, true>(acc, vin, t0, t1, step);
   } else {
-    for (uint64_t t = t0; t < t1; t += step) {
+    for (uint64_t t = blockIdx.x; t < ntiles; t += grid) {
       V v[UNROLL];
       load_tile<V, BLOCK, UNROLL, NT>(v, vin + t * kTile + threadIdx.x);
       consume_tile<OpT, T, AccT, V, N, UNROLL>(acc, v);
     }
   }
-  if (WIN > 0 && balanced) {  // the piece prefetched before the body
+  // Vectors past the last full tile, grid-strided.
+  for (uint64_t i = ntiles * kTile + static_cast<uint64_t>(blockIdx.x) * BLOCK + threadIdx.x; i < a.nvec;
+       i += static_cast<uint64_t>(gridDim.x) * BLOCK) {
+    const V v = vin[i];
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      if (u < pre_n && pre_s0 + threadIdx.x + static_cast<uint64_t>(u) * BLOCK < pre_s1) {
-#pragma unroll
-        for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(pre_v[u], k)));
-      }
-    }
-  } else if (balanced) {
-    // The leftover after the whole rounds (< grid tiles + the sub-tile remainder) as one even,
-    // contiguous piece per workgroup (< one tile each): every load issued unconditionally (an
-    // out-of-piece lane re-reads its piece's first vector and discards it), so no per-load branch
-    // serialises the wave (cdna_hip_programming.md §5 trap (c)).
-    const uint64_t l0 = full * kTile, left = a.nvec - l0;
-    const uint64_t s0 = l0 + left * blockIdx.x / grid, s1 = l0 + left * (blockIdx.x + 1) / grid;
-    for (uint64_t base = s0 + threadIdx.x; base < s1; base += kTile) {
-      V v[UNROLL];
-      bool ok[UNROLL];
-#pragma unroll
-      for (int u = 0; u < UNROLL; ++u) {
-        const uint64_t idx = base + static_cast<uint64_t>(u) * BLOCK;
-        ok[u] = idx < s1;
-        const V* p = vin + (ok[u] ? idx : base);
-        if constexpr (NT) v[u] = __builtin_nontemporal_load(p);
-        else v[u] = *p;
-      }
-#pragma unroll
-      for (int u = 0; u < UNROLL; ++u) {
-        if (ok[u]) {
-#pragma unroll
-          for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(v[u], k)));
-        }
-      }
-    }
-  } else {
-    // Vectors past the last full tile, grid-strided.
-    for (uint64_t i = ntiles * kTile + static_cast<uint64_t>(blockIdx.x) * BLOCK + threadIdx.x;
-         i < a.nvec; i += static_cast<uint64_t>(gridDim.x) * BLOCK) {
-      const V v = vin[i];
-#pragma unroll
-      for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], OpT::pre(elem<T, AccT>(v, k)));
-    }
+    for (int k = 0; k < N; ++k) acc[0] = OpT::apply(acc[0], OpT::pre(elem<T, AccT>(v, k)));
   }
   // Unaligned head and sub-vector tail (< N elements each), folded by the last workgroup.
   if (blockIdx.x == gridDim.x - 1) {
@@ -705,35 +578,30 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     uint64_t* st = a.wg_stamps + 3 * static_cast<uint64_t>(blockIdx.x);
     st[0] = t_end;
     st[1] = xcc & 0xfu;
-    st[2] = WIN > 0 ? streamed : a.contig ? t1 - t0 : (t1 > t0 ? (t1 - t0 + step - 1) / step : 0);
+    st[2] = WIN > 0 ? streamed : (ntiles > blockIdx.x ? (ntiles - blockIdx.x + grid - 1) / grid : 0);
   }
 
   // Fused cross-rank finish: this launch's epoch (counter + 1; only the finishing workgroup bumps
-  // the counter, and it runs last) and the sticky error word. Only the finisher needs them, and it
-  // loads them where their latency hides: the polled fan-in's finisher (known up front) right after
-  // publishing its own partial, under its poll of the others'; a one-workgroup launch just before
-  // the exchange. Only the ticketed fan-ins, whose finisher is whoever arrives last, load them in
-  // every workgroup — after the streaming body (not before: extra live values there change hipcc's
-  // load scheduling of the body — 76 -> 60 VGPRs and 7.3 -> 5.1 TB/s at 512 x 16). Loading them in
-  // every workgroup of the polled fan-in cost each workgroup the loads' round trip before its
-  // block barrier, i.e. ~1.4 us per fused step (bench.py decomposition, round 4).
+  // the counter, and it runs last) and the sticky error word. Only the finisher loads them, where
+  // their latency hides: the polled fan-in's finisher (known up front) right after publishing its
+  // own partial, under its poll of the others'; a one-workgroup launch just before the exchange.
+  // (Loading them in every workgroup cost each workgroup the loads' round trip before its block
+  // barrier, ~1.4 us per fused step, bench.py decomposition, round 4; loading them before the body
+  // changed hipcc's load scheduling of it: 76 -> 60 VGPRs and 7.3 -> 5.1 TB/s at 512 x 16.)
   unsigned xr_epoch = 0, xr_err = 0;
   auto load_xr = [&]() {
     xr_epoch = xrank_next_epoch(__hip_atomic_load(a.xrank->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     xr_err = __hip_atomic_load(a.xrank->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
-  if (a.xrank && !a.slots && gridDim.x > 1) load_xr();  // ticketed fan-in
 
   AccT v = block_reduce<OpT, AccT, BLOCK>(acc[0], lds);
-  AccT* partials = static_cast<AccT*>(a.partials);
-  if (a.groups == 0) {  // two-pass mode: the finalize kernel (kernel boundary) reads these
+  if (a.two_pass) {  // two-pass mode: the finalize kernel (kernel boundary) reads these
     // (a late anchor: the finalize sees fan[1] value 2 (bit 1) after the kernel boundary and poisons the result)
-    if (threadIdx.x == 0) partials[blockIdx.x] = anchor_late ? poisoned<OpT, AccT>() : v;
+    if (threadIdx.x == 0) static_cast<AccT*>(a.partials)[blockIdx.x] = anchor_late ? poisoned<OpT, AccT>() : v;
     return;
   }
 
-  // ---- one workgroup (small n): it is the last arriver by construction — no partial publish,
-  //      no tickets, no second load round.
+  // ---- one workgroup (small n): it is the finisher by construction — no partial publish, no poll.
   if (gridDim.x == 1) {
     if (threadIdx.x < 64) {
       bool xf = false;
@@ -744,203 +612,117 @@ __global__ __launch_bounds__(BLOCK) void reduce_stream(Args a) {
     return;
   }
 
-  // ---- polled fan-in (default): no tickets, no publish-then-drain wait. Every workgroup stores
-  // its partial as two tagged words (the data carries its own validity, as in the cross-rank
-  // mailbox) and exits; the last-indexed workgroup — with interleaved tiles one of the first to
-  // run out of work — polls all slots, folds them in slot order (deterministic), clears them and
-  // finishes. The finisher's path after the last partial lands is one store + one poll round,
-  // instead of store, drain, ticket (x2) and a load round. Slots live in uncached memory, so
-  // polls always see the other XCDs' stores.
-  if (a.slots) {
-    const unsigned fan_e = fan_epoch(fan_raw);
-    const uint64_t tag = static_cast<uint64_t>(fan_e) << 32;
-    // A workgroup whose XCD anchor was late (its tiles may double-count or skip others') does not
-    // publish: the finisher then reaches its bound and poisons the launch — never a plausible sum of
-    // the wrong tiles. (Publishing a flag instead would cost the finisher a load round trip after
-    // its poll on every launch, to order it after the slot stores.)
-    if (anchor_late && blockIdx.x != gridDim.x - 1) return;
-    if (threadIdx.x == 0) {
-      if (static_cast<int>(blockIdx.x) == a.delay_wg) {  // test hook: a slow workgroup
-        const uint64_t d0 = static_cast<uint64_t>(wall_clock64());
-        while (static_cast<uint64_t>(wall_clock64()) - d0 < a.delay_ticks) __builtin_amdgcn_s_sleep(127);
+  // ---- polled fan-in (every single-pass launch of more than one workgroup): no tickets, no
+  // publish-then-drain wait. Every workgroup stores its partial as two tagged words (the data
+  // carries its own validity, as in the cross-rank mailbox) and exits; the last-indexed workgroup —
+  // with interleaved tiles one of the first to run out of work — polls all slots, folds them in slot
+  // order (deterministic), and finishes. The finisher's path after the last partial lands is one
+  // store + one poll round. Slots live in uncached memory, so polls always see the other XCDs' stores.
+  const unsigned fan_e = fan_epoch(fan_raw);
+  const uint64_t tag = static_cast<uint64_t>(fan_e) << 32;
+  // A workgroup whose XCD anchor was late (its tiles may double-count or skip others') does not
+  // publish: the finisher then reaches its bound and poisons the launch — never a plausible sum of
+  // the wrong tiles. (Publishing a flag instead would cost the finisher a load round trip after its
+  // poll on every launch, to order it after the slot stores.)
+  if (anchor_late && blockIdx.x != gridDim.x - 1) return;
+  if (threadIdx.x == 0) {
+    if (static_cast<int>(blockIdx.x) == a.delay_wg) {  // test hook: a slow workgroup
+      const uint64_t d0 = static_cast<uint64_t>(wall_clock64());
+      while (static_cast<uint64_t>(wall_clock64()) - d0 < a.delay_ticks) __builtin_amdgcn_s_sleep(127);
+    }
+    const uint64_t bits = to_bits64(v);
+    uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(blockIdx.x);
+    __hip_atomic_store(sl, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(sl + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (blockIdx.x != gridDim.x - 1) return;
+  // Segmented launches: the earlier segments' results (kernel boundaries ago: plain loads), one per
+  // lane, issued before the poll so their latency hides under it.
+  AccT carried = OpT::template identity<AccT>();
+  if (threadIdx.x < a.ncarry) carried = static_cast<const AccT*>(a.carry)[threadIdx.x];
+  // The finisher: start the cross-rank descriptor loads and the sticky-error load now, they land
+  // while it polls.
+  XrankLane xl{};
+  if (a.xrank && threadIdx.x < 64) {
+    load_xr();
+    xl = xrank_prefetch(a.xrank, xr_epoch, xr_err);
+  }
+  const unsigned fan_err = __hip_atomic_load(a.fan + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  AccT t = OpT::template identity<AccT>();
+  // Bounded like every device-side wait here (all workgroups of this launch always publish, so a
+  // correct launch never reaches the bound; it keeps a stalled or misused launch from hanging the
+  // GPU, and reaching it is reported, never folded into a plausible-looking result).
+  const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
+  const uint64_t kBound = a.fan_bound;
+  bool late = false;
+  if (gridDim.x <= kPollSlots * BLOCK) {
+    // Each lane polls ALL its slots (<= kPollSlots) every round, so the finish costs one poll round
+    // trip after the last store lands, not one per slot.
+    uint64_t lo[kPollSlots], hi[kPollSlots];
+    unsigned pending = 0;
+#pragma unroll
+    for (int k = 0; k < kPollSlots; ++k)
+      if (threadIdx.x + k * BLOCK < gridDim.x) pending |= 1u << k;
+    while (pending) {
+#pragma unroll
+      for (int k = 0; k < kPollSlots; ++k) {
+        if (pending & (1u << k)) {
+          const uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(threadIdx.x + k * BLOCK);
+          lo[k] = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          hi[k] = __hip_atomic_load(sl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
-      const uint64_t bits = to_bits64(v);
-      uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(blockIdx.x);
-      __hip_atomic_store(sl, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(sl + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (blockIdx.x != gridDim.x - 1) return;
-    // Segmented launches: the earlier segments' results (kernel boundaries ago: plain loads), one per
-    // lane, issued before the poll so their latency hides under it.
-    AccT carried = OpT::template identity<AccT>();
-    if (threadIdx.x < a.ncarry) carried = static_cast<const AccT*>(a.carry)[threadIdx.x];
-    // The finisher: start the cross-rank descriptor loads and the sticky-error load now, they land
-    // while it polls.
-    XrankLane xl{};
-    if (a.xrank && threadIdx.x < 64) {
-      load_xr();
-      xl = xrank_prefetch(a.xrank, xr_epoch, xr_err);
-    }
-    const unsigned fan_err = __hip_atomic_load(a.fan + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    AccT t = OpT::template identity<AccT>();
-    // Bounded like every device-side wait here (all workgroups of this launch always publish, so
-    // a correct launch never reaches the bound; it keeps a stalled or misused launch from hanging
-    // the GPU, and reaching it is reported, never folded into a plausible-looking result).
-    const uint64_t t0 = static_cast<uint64_t>(wall_clock64());
-    const uint64_t kBound = a.fan_bound;
-    bool late = false;
-    if (gridDim.x <= kPollSlots * BLOCK) {
-      // Each lane polls ALL its slots (<= kPollSlots) every round, so the finish costs one poll
-      // round trip after the last store lands, not one per slot.
-      uint64_t lo[kPollSlots], hi[kPollSlots];
-      unsigned pending = 0;
 #pragma unroll
       for (int k = 0; k < kPollSlots; ++k)
-        if (threadIdx.x + k * BLOCK < gridDim.x) pending |= 1u << k;
-      while (pending) {
+        if ((pending & (1u << k)) && (lo[k] & ~0xffffffffull) == tag && (hi[k] & ~0xffffffffull) == tag)
+          pending &= ~(1u << k);
+      if (!pending) break;
+      if (static_cast<uint64_t>(wall_clock64()) - t0 > kBound) {
+        late = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
 #pragma unroll
-        for (int k = 0; k < kPollSlots; ++k) {
-          if (pending & (1u << k)) {
-            const uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(threadIdx.x + k * BLOCK);
-            lo[k] = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            hi[k] = __hip_atomic_load(sl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < kPollSlots; ++k)
-          if ((pending & (1u << k)) && (lo[k] & ~0xffffffffull) == tag && (hi[k] & ~0xffffffffull) == tag)
-            pending &= ~(1u << k);
-        if (!pending) break;
-        if (static_cast<uint64_t>(wall_clock64()) - t0 > kBound) {
+    for (int k = 0; k < kPollSlots; ++k)  // fold in slot order (deterministic)
+      if (threadIdx.x + k * BLOCK < gridDim.x)
+        t = OpT::apply(t, from_bits64<AccT>((lo[k] & 0xffffffffull) | (hi[k] << 32)));
+  } else {  // very large grids (user --maxblocks / wg-per-cu): slot by slot
+    for (unsigned i = threadIdx.x; i < gridDim.x; i += BLOCK) {
+      const uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(i);
+      uint64_t l, h;
+      for (;;) {
+        l = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h = __hip_atomic_load(sl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((l & ~0xffffffffull) == tag && (h & ~0xffffffffull) == tag) break;
+        if (late || static_cast<uint64_t>(wall_clock64()) - t0 > kBound) {
           late = true;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-#pragma unroll
-      for (int k = 0; k < kPollSlots; ++k)  // fold in slot order (deterministic)
-        if (threadIdx.x + k * BLOCK < gridDim.x)
-          t = OpT::apply(t, from_bits64<AccT>((lo[k] & 0xffffffffull) | (hi[k] << 32)));
-    } else {  // very large grids (user --maxblocks / wg-per-cu): slot by slot
-      for (unsigned i = threadIdx.x; i < gridDim.x; i += BLOCK) {
-        const uint64_t* sl = a.slots + 2 * static_cast<uint64_t>(i);
-        uint64_t l, h;
-        for (;;) {
-          l = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          h = __hip_atomic_load(sl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((l & ~0xffffffffull) == tag && (h & ~0xffffffffull) == tag) break;
-          if (late || static_cast<uint64_t>(wall_clock64()) - t0 > kBound) {
-            late = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        t = OpT::apply(t, from_bits64<AccT>((l & 0xffffffffull) | (h << 32)));
-      }
+      t = OpT::apply(t, from_bits64<AccT>((l & 0xffffffffull) | (h << 32)));
     }
-    // Any lane past the bound (or an earlier launch's sticky error) poisons this launch's result.
-    const bool bad = __syncthreads_or(late) || fan_err != 0 || anchor_late;
-    t = block_reduce<OpT, AccT, BLOCK>(OpT::apply(t, carried), lds);
-    if (fan_e == 0xffffffffu) {  // the epoch wraps after this launch: invalidate every slot first
-      __syncthreads();
-      for (unsigned i = threadIdx.x; i < 2u * a.fan_slots; i += BLOCK)
-        __hip_atomic_store(a.slots + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (threadIdx.x == 0)  // and the XCD anchor (XcdAnchor), tagged with the same epochs
-        __hip_atomic_store(reinterpret_cast<uint64_t*>(a.fan + 2), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-    }
-    if (threadIdx.x < 64) {
-      bool xf = false;
-      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xl, bad ? poisoned<OpT, AccT>() : t, bad, xf);
-      if (threadIdx.x == 0) {
-        *static_cast<AccT*>(a.out) = (bad || xf) ? poisoned<OpT, AccT>() : t;
-        if (bad) __hip_atomic_fetch_or(a.fan + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // every slot of this launch has been read (or abandoned): the next launch's epoch
-        __hip_atomic_store(a.fan, fan_e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    return;
   }
-
-  // ---- ticketed finalisation (MIREDUCE_FANIN=flat|tree; cdna_hip_programming.md §6 G16, sc1 form)
-  // Ordering rests on the gfx950 code hipcc emits for these relaxed agent-scope atomics (the full
-  // acq_rel form would add an L2 write-back per arrival). Generated for <SumOp,double,512,16,nt>
-  // and pinned by tests/test_isa_ordering.py:
-  //   global_store_dwordx2 v4, v[2:3], s[30:31] sc1     ; partial, write-through past L2
-  //   s_waitcnt vmcnt(0)                                ; ... acknowledged before
-  //   global_atomic_add v6, v4, v6, s[34:35] sc0        ; the (returning) ticket
-  //   s_barrier                                         ; is_last broadcast
-  //   global_load_dwordx2 v[8:9], v[8:9], off sc1       ; last arriver reads partials past L1
-  const unsigned G = static_cast<unsigned>(a.groups);
-  const unsigned g = blockIdx.x % G;  // group label only; correctness is placement-independent
-  if (threadIdx.x == 0) {
-    store_sc1(&partials[blockIdx.x], v);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned members = gridDim.x / G + (g < gridDim.x % G ? 1u : 0u);
-    const unsigned prev = __hip_atomic_fetch_add(&a.tickets[g * kTicketStride], 1u,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = (prev == members - 1);
+  // Any lane past the bound (or an earlier launch's sticky error) poisons this launch's result.
+  const bool bad = __syncthreads_or(late) || fan_err != 0 || anchor_late;
+  t = block_reduce<OpT, AccT, BLOCK>(OpT::apply(t, carried), lds);
+  if (fan_e == 0xffffffffu) {  // the epoch wraps after this launch: invalidate every slot first
+    __syncthreads();
+    for (unsigned i = threadIdx.x; i < 2u * a.fan_slots; i += BLOCK)
+      __hip_atomic_store(a.slots + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0)  // and the XCD anchor (XcdAnchor), tagged with the same epochs
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(a.fan + 2), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
   }
-  __syncthreads();
-  if (!is_last) return;
-
-  if (a.flat) {
-    // Flat fan-in: the group's last arriver only takes a ticket on the top counter; the last of
-    // those folds all gridDim.x partials at once (one parallel sc1 load round instead of a
-    // group fold + group-partial publish + second fold: two memory round trips shorter).
-    // (One group — small grids — has no top counter: its last arriver is the finisher.)
-    if (G > 1) {
-      if (threadIdx.x == 0) {
-        __hip_atomic_store(&a.tickets[g * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned prev = __hip_atomic_fetch_add(&a.tickets[G * kTicketStride], 1u,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        is_last = (prev == G - 1);
-      }
-      __syncthreads();
-      if (!is_last) return;
-    }
-    AccT t = OpT::template identity<AccT>();
-    for (unsigned i = threadIdx.x; i < gridDim.x; i += BLOCK) t = OpT::apply(t, load_sc1(&partials[i]));
-    t = block_reduce<OpT, AccT, BLOCK>(t, lds);
-    if (threadIdx.x < 64) {
-      bool xf = false;
-      if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), t, false, xf);
-      if (threadIdx.x == 0) {
-        *static_cast<AccT*>(a.out) = xf ? poisoned<OpT, AccT>() : t;
-        // reset: the top counter, or (one group) the group counter itself
-        __hip_atomic_store(&a.tickets[(G > 1 ? G : 0) * kTicketStride], 0u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    return;
-  }
-
-  // Last arriver of group g: fold partials g, g+G, g+2G, ... (sc1 loads: L1 never holds them).
-  AccT s = OpT::template identity<AccT>();
-  for (unsigned i = g + threadIdx.x * G; i < gridDim.x; i += BLOCK * G)
-    s = OpT::apply(s, load_sc1(&partials[i]));
-  s = block_reduce<OpT, AccT, BLOCK>(s, lds);
-  AccT* gpart = static_cast<AccT*>(a.group_partials);
-  if (threadIdx.x == 0) {
-    store_sc1(&gpart[g], s);
-    __hip_atomic_store(&a.tickets[g * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(&a.tickets[G * kTicketStride], 1u,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = (prev == G - 1);
-  }
-  __syncthreads();
-  if (!is_last) return;
-
   if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    AccT t = lane < static_cast<int>(G) ? load_sc1(&gpart[lane]) : OpT::template identity<AccT>();
-    t = wave_reduce<OpT>(t);
     bool xf = false;
-    if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xrank_prefetch(a.xrank, xr_epoch, xr_err), t, false, xf);
-    if (lane == 0) {
-      *static_cast<AccT*>(a.out) = xf ? poisoned<OpT, AccT>() : t;
-      __hip_atomic_store(&a.tickets[G * kTicketStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.xrank) t = xrank_finish<OpT, AccT>(a.xrank, xl, bad ? poisoned<OpT, AccT>() : t, bad, xf);
+    if (threadIdx.x == 0) {
+      *static_cast<AccT*>(a.out) = (bad || xf) ? poisoned<OpT, AccT>() : t;
+      if (bad) __hip_atomic_fetch_or(a.fan + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // every slot of this launch has been read (or abandoned): the next launch's epoch
+      __hip_atomic_store(a.fan, fan_e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -1001,17 +783,16 @@ __global__ __launch_bounds__(256) void combine(T* __restrict__ inout, const T* _
 }  // namespace kern
 
 // ----------------------------------------------------------------------------------------------
-// Dispatch table keyed by (op, dtype, acc, block, unroll, policy, pipelined); replaces the
-// reference's runtime switch over 20 template instantiations per (op, T).
+// Dispatch table keyed by (op, dtype, acc, block, unroll, policy, body); replaces the reference's
+// runtime switch over 20 template instantiations per (op, T).
 // ----------------------------------------------------------------------------------------------
 namespace detail {
 
 using LaunchFn = void (*)(const kern::Args&, int grid, hipStream_t);
 
-template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT, bool PIPE, int WIN = 0>
+template <class OpT, class T, class AccT, int BLOCK, int UNROLL, bool NT, int WIN = 0>
 void launch_stream(const kern::Args& a, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((kern::reduce_stream<OpT, T, AccT, BLOCK, UNROLL, NT, PIPE, WIN>), dim3(grid), dim3(BLOCK),
-                     0, s, a);
+  hipLaunchKernelGGL((kern::reduce_stream<OpT, T, AccT, BLOCK, UNROLL, NT, WIN>), dim3(grid), dim3(BLOCK), 0, s, a);
 }
 
 constexpr int kBlocks[] = {256, 512, 1024};
@@ -1021,16 +802,13 @@ constexpr int kNumUnrolls = 4;
 
 constexpr int kCombos = 29;
 
-// Body schedules: 0 = hipcc's own schedule of the plain loop, 1 = software-pipelined (PIPE),
-// 2 / 3 = explicit load window of 2 / 4 registers per thread (stream_window; nt only).
-constexpr int kNumBodies = 4;
+// Body schedules: 0 = hipcc's own schedule of the plain loop, 1 / 2 = explicit load window of 2 / 4
+// registers per thread (stream_window_seq; nt only).
+constexpr int kNumBodies = 3;
 struct Table {
   LaunchFn fn[kCombos][kNumBlocks][kNumUnrolls][2][kNumBodies];  // [..][policy nt][body]
 };
 
-// Pipelined variants need two register sets of UNROLL 16-byte vectors: only where the
-// per-SIMD register budget allows it (BLOCK * UNROLL <= 8192); elsewhere the plain body.
-constexpr bool pipe_ok(int b, int u) { return b * u <= 8192; }
 // Explicit windows are instantiated for the non-temporal policy, 256- and 512-thread blocks and
 // unroll 2..8 (profiles/r3_window/: the measured winners and their neighbours); elsewhere null.
 constexpr bool window_ok(int b, int u, int w) { return (b == 256 || b == 512) && u <= 8 && u % w == 0; }
@@ -1039,13 +817,10 @@ template <class OpT, class T, class AccT, int BI, int UI>
 void fill_one(Table& tb, int c) {
   constexpr int B = kBlocks[BI];
   constexpr int U = kUnrolls[UI];
-  constexpr bool P = pipe_ok(B, U);
-  tb.fn[c][BI][UI][0][0] = launch_stream<OpT, T, AccT, B, U, false, false>;
-  tb.fn[c][BI][UI][1][0] = launch_stream<OpT, T, AccT, B, U, true, false>;
-  tb.fn[c][BI][UI][0][1] = launch_stream<OpT, T, AccT, B, U, false, P>;
-  tb.fn[c][BI][UI][1][1] = launch_stream<OpT, T, AccT, B, U, true, P>;
-  if constexpr (window_ok(B, U, 2)) tb.fn[c][BI][UI][1][2] = launch_stream<OpT, T, AccT, B, U, true, false, 2>;
-  if constexpr (window_ok(B, U, 4)) tb.fn[c][BI][UI][1][3] = launch_stream<OpT, T, AccT, B, U, true, false, 4>;
+  tb.fn[c][BI][UI][0][0] = launch_stream<OpT, T, AccT, B, U, false>;
+  tb.fn[c][BI][UI][1][0] = launch_stream<OpT, T, AccT, B, U, true>;
+  if constexpr (window_ok(B, U, 2)) tb.fn[c][BI][UI][1][1] = launch_stream<OpT, T, AccT, B, U, true, 2>;
+  if constexpr (window_ok(B, U, 4)) tb.fn[c][BI][UI][1][2] = launch_stream<OpT, T, AccT, B, U, true, 4>;
 }
 
 template <class OpT, class T, class AccT, int BI>

@@ -43,15 +43,9 @@ py::dict plan_dict(const LaunchPlan& p) {
   d["block"] = p.block;
   d["unroll"] = p.unroll;
   d["grid"] = p.grid;
-  d["groups"] = p.groups;
   d["nontemporal"] = p.nontemporal;
-  d["pipelined"] = p.pipelined;
   d["window"] = p.window;
   d["single_pass"] = p.single_pass;
-  d["flat"] = p.flat;
-  d["poll"] = p.poll;
-  d["balanced"] = p.balanced;
-  d["contiguous"] = p.contiguous;
   d["xskew"] = p.xskew;
   d["head"] = p.head;
   d["nvec"] = p.nvec;
@@ -63,9 +57,8 @@ py::dict plan_dict(const LaunchPlan& p) {
 
 constexpr int kSkewAuto = -2147483647 - 1;  // ReduceConfig::xcd_skew's "tuned default"
 
-ReduceConfig make_cfg(int block, int unroll, int wg_per_cu, int max_blocks, int groups,
-                      int policy, bool single_pass, int pipeline = -1, int window = -1, int xcd_skew = kSkewAuto,
-                      int64_t segment_bytes = 0) {
+ReduceConfig make_cfg(int block, int unroll, int wg_per_cu, int max_blocks, int policy, bool single_pass,
+                      int window = -1, int xcd_skew = kSkewAuto, int64_t segment_bytes = 0) {
   ReduceConfig c;
   c.segment_bytes = segment_bytes;
   c.window = window;
@@ -74,9 +67,7 @@ ReduceConfig make_cfg(int block, int unroll, int wg_per_cu, int max_blocks, int 
   c.unroll = unroll;
   c.wg_per_cu = wg_per_cu;
   c.max_blocks = max_blocks;
-  c.groups = groups;
   c.policy = policy;
-  c.pipeline = pipeline;
   c.single_pass = single_pass;
   return c;
 }
@@ -108,7 +99,6 @@ PYBIND11_MODULE(_C, m) {
   m.attr("OP_MAX") = static_cast<int>(Op::Max);
   m.attr("OP_SUMSQ") = static_cast<int>(Op::SumSq);
   m.attr("OP_AMAX") = static_cast<int>(Op::AbsMax);
-  m.attr("TICKET_STRIDE") = kTicketStride;
   // Build provenance: hash of the csrc tree this module was built from (tools/source_hash.py).
   m.def("source_hash", [] { return std::string(source_hash()); });
 
@@ -183,10 +173,10 @@ PYBIND11_MODULE(_C, m) {
   // Prepared launch for per-step loops: launch(stream) is one positional-argument call.
   py::class_<BoundReduce>(m, "BoundReduce")
       .def(py::init([](Workspace& ws, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out,
-                       int block, int unroll, int wg_per_cu, int max_blocks, int groups, int policy,
-                       bool single_pass, int pipeline, uintptr_t xrank, int window, int xcd_skew,
+                       int block, int unroll, int wg_per_cu, int max_blocks, int policy,
+                       bool single_pass, uintptr_t xrank, int window, int xcd_skew,
                        int64_t segment_bytes) {
-             ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline,
+             ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, policy, single_pass,
                                          window, xcd_skew, segment_bytes);
              cfg.xrank = as_ptr<const void>(xrank);
              return new BoundReduce(as_ptr<const void>(in), n, static_cast<DType>(dtype), static_cast<Op>(op),
@@ -194,8 +184,8 @@ PYBIND11_MODULE(_C, m) {
            }),
            py::arg("ws"), py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"), py::arg("acc"),
            py::arg("out_ptr"), py::arg("block") = 0, py::arg("unroll") = 0, py::arg("wg_per_cu") = 0,
-           py::arg("max_blocks") = 0, py::arg("groups") = 0, py::arg("policy") = -1,
-           py::arg("single_pass") = true, py::arg("pipeline") = -1, py::arg("xrank") = 0, py::arg("window") = -1,
+           py::arg("max_blocks") = 0, py::arg("policy") = -1,
+           py::arg("single_pass") = true, py::arg("xrank") = 0, py::arg("window") = -1,
            py::arg("xcd_skew") = kSkewAuto, py::arg("segment_bytes") = 0,
            py::keep_alive<1, 2>())
       .def("launch", [](const BoundReduce& b, uintptr_t stream, uintptr_t out) { b.launch(as_stream(stream), as_ptr<void>(out)); },
@@ -284,11 +274,11 @@ PYBIND11_MODULE(_C, m) {
   m.def(
       "reduce",
       [](Workspace& ws, uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t out,
-         uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks, int groups,
-         int policy, bool single_pass, int pipeline, uint64_t fanin_bound_ticks, int debug_delay_wg,
+         uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks,
+         int policy, bool single_pass, uint64_t fanin_bound_ticks, int debug_delay_wg,
          uint64_t debug_delay_ticks, int window, uintptr_t xrank, uintptr_t wg_stamps, int xcd_skew,
          uint64_t debug_delay_anchor_ticks, int64_t segment_bytes) {
-        ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline, window,
+        ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, policy, single_pass, window,
                                     xcd_skew, segment_bytes);
         cfg.xrank = as_ptr<const void>(xrank);
         cfg.debug_wg_stamps = as_ptr<uint64_t>(wg_stamps);
@@ -304,18 +294,18 @@ PYBIND11_MODULE(_C, m) {
       py::arg("ws"), py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("op"),
       py::arg("acc"), py::arg("out_ptr"), py::arg("stream") = 0, py::arg("block") = 0,
       py::arg("unroll") = 0, py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0,
-      py::arg("groups") = 0, py::arg("policy") = -1, py::arg("single_pass") = true,
-      py::arg("pipeline") = -1, py::arg("fanin_bound_ticks") = 0, py::arg("debug_delay_wg") = -1,
+      py::arg("policy") = -1, py::arg("single_pass") = true,
+      py::arg("fanin_bound_ticks") = 0, py::arg("debug_delay_wg") = -1,
       py::arg("debug_delay_ticks") = 0, py::arg("window") = -1, py::arg("xrank") = 0, py::arg("wg_stamps") = 0,
       py::arg("xcd_skew") = kSkewAuto, py::arg("debug_delay_anchor_ticks") = 0, py::arg("segment_bytes") = 0);
 
   m.def(
       "plan",
       [](uintptr_t in, uint64_t n, int dtype, int num_cus, int max_grid, int block, int unroll,
-         int wg_per_cu, int max_blocks, int groups, int policy, bool single_pass, int pipeline, int window,
+         int wg_per_cu, int max_blocks, int policy, bool single_pass, int window,
          int op, int xcd_skew, int64_t segment_bytes) {
         MIREDUCE_REQUIRE(op >= 0 && op < kNumOps, "op out of range");
-        const ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, groups, policy, single_pass, pipeline,
+        const ReduceConfig cfg = make_cfg(block, unroll, wg_per_cu, max_blocks, policy, single_pass,
                                           window, xcd_skew, segment_bytes);
         LaunchPlan p = plan_reduce(as_ptr<const void>(in), n, static_cast<DType>(dtype), cfg, num_cus, max_grid,
                                    static_cast<Op>(op));
@@ -324,15 +314,15 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("in_ptr"), py::arg("n"), py::arg("dtype"), py::arg("num_cus") = 256,
       py::arg("max_grid") = 16384, py::arg("block") = 0, py::arg("unroll") = 0,
-      py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0, py::arg("groups") = 0,
-      py::arg("policy") = -1, py::arg("single_pass") = true, py::arg("pipeline") = -1, py::arg("window") = -1,
+      py::arg("wg_per_cu") = 0, py::arg("max_blocks") = 0,
+      py::arg("policy") = -1, py::arg("single_pass") = true, py::arg("window") = -1,
       py::arg("op") = 0, py::arg("xcd_skew") = kSkewAuto, py::arg("segment_bytes") = 0);
 
   m.def(
       "reduce_partials",
       [](uintptr_t in, uint64_t n, int dtype, int op, int acc, uintptr_t partials, int max_grid,
          int num_cus, uintptr_t stream, int block, int unroll, int wg_per_cu, int max_blocks, int policy) {
-        ReduceConfig c = make_cfg(block, unroll, wg_per_cu, max_blocks, 0, policy, false);
+        ReduceConfig c = make_cfg(block, unroll, wg_per_cu, max_blocks, policy, false);
         return plan_dict(reduce_partials(as_ptr<const void>(in), n, static_cast<DType>(dtype),
                                          static_cast<Op>(op), static_cast<DType>(acc),
                                          as_ptr<void>(partials), max_grid, num_cus,

@@ -93,10 +93,8 @@ class KernelConfig:
     unroll: int = 0
     wg_per_cu: int = 0
     max_blocks: int = 0
-    groups: int = 0
     nontemporal: Optional[bool] = None  # None: size-dependent tuned choice
     single_pass: bool = True
-    pipelined: Optional[bool] = None    # None: tuned choice
     window: Optional[int] = None        # loads in flight per thread: None tuned, 0 hipcc's schedule, 2 | 4
     xcd_skew: Optional[int] = None      # XCD-weighted split, permille of rounds (+: odd XCCs more); None tuned
     segment_bytes: int = 0              # segmented launches: 0 auto (8 GiB above 16 GiB), < 0 one launch, > 0 size
@@ -111,10 +109,8 @@ class KernelConfig:
             unroll=self.unroll,
             wg_per_cu=self.wg_per_cu,
             max_blocks=self.max_blocks,
-            groups=self.groups,
             policy=self.policy,
             single_pass=self.single_pass,
-            pipeline=-1 if self.pipelined is None else int(bool(self.pipelined)),
             window=-1 if self.window is None else int(self.window),
             xcd_skew=XCD_SKEW_AUTO if self.xcd_skew is None else int(self.xcd_skew),
             segment_bytes=int(self.segment_bytes),

@@ -44,7 +44,7 @@ def test_fanin_bound_reports_error_poisons_and_recovers(dt, op):
     out = torch.zeros(1, dtype=default_acc_dtype(dt, op), device=dev)
     plan = _launch(C, red, x, out, op)
     torch.cuda.synchronize()
-    assert plan["poll"] and plan["grid"] > 1, plan
+    assert plan["single_pass"] and plan["grid"] > 1, plan
     assert out.item() == exp and red.check() is None and red.ws.error() == 0
     # workgroup 0 publishes 50 ms late against a 1 ms bound: reported, result poisoned — NaN for
     # floats, the operator's identity for integers (neutral in a cross-rank fold; ADVICE r3: not 0,

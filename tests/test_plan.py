@@ -30,11 +30,10 @@ def test_misaligned_element_rejected():
 
 
 @pytest.mark.parametrize("n", [0, 1, 100, 10**6, 10**9, 3 * 10**9])
-def test_grid_bounds_and_groups(n):
+def test_grid_bounds(n):
     C = native()
     p = C.plan(0, n, F64, num_cus=256)
     assert 1 <= p["grid"] <= 256 * 8
-    assert 1 <= p["groups"] <= min(64, p["grid"])
     tile = p["block"] * p["unroll"]
     assert p["grid"] <= max(1, -(-p["nvec"] // tile))
 
@@ -93,11 +92,10 @@ def test_window_only_where_instantiated():
     # explicit plans keep hipcc's schedule unless a window is asked for
     assert C.plan(0, 10**9, F64, block=256, unroll=8)["window"] == 0
     assert C.plan(0, 10**9, F64, block=256, unroll=8, window=4)["window"] == 4
-    # not instantiated: 1024 threads, unroll 16, the default (non-nt) policy, pipelined bodies
+    # not instantiated: 1024 threads, unroll 16, the default (non-nt) policy
     assert C.plan(0, 10**9, F64, block=1024, unroll=4, window=2)["window"] == 0
     assert C.plan(0, 10**9, F64, block=256, unroll=16, window=4)["window"] == 0
     assert C.plan(0, 10**9, F64, block=256, unroll=4, window=2, policy=0)["window"] == 0
-    assert C.plan(0, 10**9, F64, block=256, unroll=4, window=2, pipeline=1)["window"] == 0
     assert C.plan(0, 10**9, F64, block=256, unroll=2, window=4)["window"] == 0  # 4 does not divide 2
     assert C.plan(0, 10**9, F64, window=0)["window"] == 0  # the tuned plan with hipcc's schedule
     with pytest.raises(C.NativeError):
@@ -106,10 +104,10 @@ def test_window_only_where_instantiated():
 
 def test_overrides_and_caps():
     C = native()
-    p = C.plan(0, 10**9, F64, block=1024, unroll=8, wg_per_cu=2, max_blocks=100, groups=64, policy=0)
-    assert (p["block"], p["unroll"], p["grid"], p["groups"], p["nontemporal"]) == (1024, 8, 100, 64, False)
+    p = C.plan(0, 10**9, F64, block=1024, unroll=8, wg_per_cu=2, max_blocks=100, policy=0)
+    assert (p["block"], p["unroll"], p["grid"], p["nontemporal"]) == (1024, 8, 100, False)
     p = C.plan(0, 10**9, F64, single_pass=False)
-    assert p["groups"] == 0 and p["single_pass"] is False
+    assert p["single_pass"] is False
     with pytest.raises(C.NativeError):
         C.plan(0, 10, F64, block=384)
     with pytest.raises(C.NativeError):
@@ -140,16 +138,14 @@ def test_ladder_geometry_matches_reference_planner(kernel, n):
 
 def test_compiled_variants_cover_grid():
     v = native().compiled_variants()
-    plain = [s for s in v if not s.endswith("pipelined") and "window" not in s]
-    piped = [s for s in v if s.endswith("pipelined")]
+    plain = [s for s in v if "window" not in s]
     win = [s for s in v if "window" in s]
     assert len(plain) == 3 * 4 * 2  # block x unroll x policy
     # explicit windows: nt, 256/512 threads, unroll 2..8 divisible by the window
     assert len(win) == 2 * (3 + 2) and "block=256 unroll=4 policy=nt window=2" in v
-    # software-pipelined bodies exist where BLOCK * UNROLL <= 8192 (two register sets)
-    assert len(piped) == 2 * sum(1 for b in (256, 512, 1024) for u in (2, 4, 8, 16) if b * u <= 8192)
     assert "block=512 unroll=16 policy=nt" in v
-    assert "block=1024 unroll=16 policy=nt pipelined" not in v
+    # round 6: one body per plan ships (no software-pipelined variants)
+    assert len(v) == len(plain) + len(win) and not any("pipelined" in s for s in v)
 
 
 def test_single_hip_runtime_in_process():

@@ -216,3 +216,88 @@ def test_driver_record_line_in_the_stdout_tail(tmp_path):
     rs = scaling.dedupe(scaling.parse_text(src.read_text()))
     assert len(rs) == 1 and rs[0]["summary"]["run"] == "abc"
     assert scaling.summarise_vector(rs)[("direct", "INT", "MAX")][8]["gibps"] == 2500.0
+
+
+# ---------------------------------------------------------------- --from: the driver's SCALE record
+def _scale_record(tmp_path, ns=(1, 2, 4, 8), unverified=(), reason_at=None):
+    """A synthetic driver scaling record: per-N runs whose printed line sits in a stdout tail (as in
+    BENCH_r*.json), every field bench.py's line carries."""
+    runs = []
+    for n in ns:
+        line = _line(n, 7300.0 * n * (0.97 if n > 1 else 1.0), 8.0 / (7.3 * n * (0.97 if n > 1 else 1.0)))
+        line["verified"] = n not in unverified
+        line["config"]["collective"] = "fused"
+        if n == reason_at:
+            line["config"].update(collective="rccl", collective_reason="self-check: rank 2: InjectedFault: ...")
+        line["summary"] = {"plans": f"tuned default x{n}", "reduce_c_rows": {
+            "direct": "INT MAX 100.0; INT MIN 90.0; INT SUM 95.0; DOUBLE MAX 80.0; DOUBLE MIN 81.0; DOUBLE SUM 82.0"}}
+        line["decomposition"] = {"local_ms_per_step": 1.0 / n, "exchange_us_per_step": 3.0, "skew_us_per_step": 1.0,
+                                 "scaling_efficiency_vs_local": 0.99, "exchange_wait_us": {"min_rank_median": 0.5,
+                                                                                          "max_rank_median": 2.0}}
+        runs.append({"n": n, "rc": 0, "tail": "RCCL version : x\n" + json.dumps(line) + "\n---- stderr ----\n"})
+    p = tmp_path / "SCALE_r06.json"
+    p.write_text(json.dumps({"runs": runs}))
+    return p
+
+
+def test_from_driver_record_builds_everything(tmp_path):
+    # VERDICT r5 item 4: one command turns the driver's scaling record into the results files, the
+    # tables, the WRITEUP section (measured next to the projection it replaces) and both figures
+    src = _scale_record(tmp_path, reason_at=4)
+    writeup = tmp_path / "WRITEUP.md"
+    writeup.write_text("# x\n\nbefore\n" + scaling.WRITEUP_BEGIN + "\nprojection table\n" + scaling.WRITEUP_END + "\nafter\n")
+    out = tmp_path / "res"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling.py"), "--from", str(src), "--out", str(out),
+                        "--update-writeup", str(writeup)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    rows = [ln.split() for ln in (out / "DOUBLE_SUM.txt").read_text().splitlines() if ln]
+    assert [int(x[2]) for x in rows] == [1, 2, 4, 8]
+    table = (out / "writeup_scaling.md").read_text()
+    assert "| 8 | 1 GB |" in table and "projection t_x = 0" in table
+    eight = [ln for ln in table.splitlines() if ln.startswith("| 8 |")][0].split("|")
+    assert abs(float(eight[6]) - scaling.projection(8)) < 1.0  # the projection kept alongside
+    assert "rccl (self-check: rank 2" in table  # the fallback is named where it happened
+    text = writeup.read_text()
+    assert "projection table" not in text and "Measured by the driver's scaling run" in text and "after" in text
+    assert (out / "figures" / "int.png").stat().st_size > 10000 and (out / "figures" / "double.png").exists()
+    assert (out / "vector_direct" / "DOUBLE_SUM.txt").exists()  # reduce.c's own table, N > 1
+    assert "decomposition" not in table and "| 3.00 |" in table  # exchange us/step column
+
+
+def test_from_driver_record_refuses_partial_or_unverified_curves(tmp_path):
+    tool = os.path.join(ROOT, "tools", "scaling.py")
+    for kw, want in (({"ns": (1, 2, 8)}, "no headline result for N=4"),
+                     ({"unverified": (8,)}, "not verified: N=8 (verification FAILED)")):
+        src = _scale_record(tmp_path, **kw)
+        out = tmp_path / "res_bad"
+        r = subprocess.run([sys.executable, tool, "--from", str(src), "--out", str(out)], capture_output=True,
+                           text=True, timeout=120)
+        assert r.returncode == 2 and want in r.stderr, (r.stdout, r.stderr)
+        assert not out.exists()  # nothing written, nothing interpolated
+    skipped = tmp_path / "SCALE_skip.json"
+    skipped.write_text(json.dumps({"skipped": True, "reason": "no 8-GPU node"}))
+    r = subprocess.run([sys.executable, tool, "--from", str(skipped), "--out", str(tmp_path / "s")],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "skipped the scaling run (no 8-GPU node)" in r.stderr
+
+
+def test_projection_matches_the_writeup_model():
+    # docs/WRITEUP.md §2: shard G GB in G x 135.56 us + 1.9 us per launch (+ t_x)
+    assert abs(scaling.projection(8) - 8e9 / (137.46e-6) / 1e9) < 1.0 and round(scaling.projection(8)) == 58199
+    assert scaling.projection(8, 5.0) < scaling.projection(8) < 8 * scaling.projection(1)
+
+
+def test_report_figures_regenerate_from_committed_data(tmp_path):
+    # VERDICT r5 item 3: the reference's two figures (mpi/makePlots.gp), regenerated from data in the
+    # repo: BG/L VN curves, the CUDA constants, the 8-CPU MPICH curve, the MI355X lines
+    import report
+    paths = report.make_figures(str(tmp_path), bench_path=os.path.join(ROOT, "BENCH_r05.json"))
+    assert sorted(os.path.basename(p) for p in paths) == ["double.png", "int.png"]
+    assert all(os.path.getsize(p) > 10000 for p in paths)
+    s = report.series({"INT SUM": {"gbps": 7200.0}}, report.bench_vector_n1(os.path.join(ROOT, "BENCH_r05.json")),
+                      "", report.DEFAULT_MPICH)
+    labels = {lab: data for lab, _, data in s["INT"]}
+    assert abs(labels["BG/L VN SUM"][1024] - 146.818 / report.GIB_PER_GB) < 1e-6  # mpi/results/INT_SUM.txt
+    assert labels["ref CUDA SUM"] == 90.8413 and labels["MI355X 1 GPU SUM"] == 7200.0
+    assert 1 in labels["reduce.c, 8-CPU MPICH SUM"] and 8 in labels["reduce.c, 8-CPU MPICH SUM"]
+    assert labels["MI355X reduce.c (direct) SUM"][1] > 1000  # BENCH_r05's N=1 direct row (GiB/s -> GB/s)

@@ -195,10 +195,7 @@ int main(int argc, char** argv) {
     a.body = x;
     a.nvec = nvec;
     a.partials = ws.partials();
-    a.group_partials = ws.group_partials();
-    a.tickets = ws.tickets();
     a.out = out;
-    a.groups = 8;
     a.slots = ws.slots();
     a.fan = ws.fan();
     a.fan_slots = static_cast<unsigned>(ws.max_grid());
@@ -225,7 +222,7 @@ int main(int argc, char** argv) {
       const Var& v = vars[i];
       auto launch = [&]() {
         if (v.skew >= 0) {
-          detail::launch_stream<SumOp, double, double, B, U, true, false, W>(prod_args(v.skew), grid, 0);
+          detail::launch_stream<SumOp, double, double, B, U, true, W>(prod_args(v.skew), grid, 0);
         } else {
           // -1: equal static rounds; -2: the weighted split's common rounds (19 extra for the odd
           // workgroups, as production at 1e9) minus the K dynamic ones

@@ -161,10 +161,7 @@ int main(int argc, char** argv) {
     a.body = x;
     a.nvec = nvec;
     a.partials = ws.partials();
-    a.group_partials = ws.group_partials();
-    a.tickets = ws.tickets();
     a.out = out;
-    a.groups = 8;
     a.slots = ws.slots();
     a.fan = ws.fan();
     a.fan_slots = static_cast<unsigned>(ws.max_grid());
@@ -193,11 +190,11 @@ int main(int argc, char** argv) {
       const Var& v = vars[i];
       auto launch = [&]() {
         if (v.kind == 0)
-          detail::launch_stream<SumOp, int32_t, int64_t, B, U, true, false, 2>(prod_args(2 * cus), 2 * cus, 0);
+          detail::launch_stream<SumOp, int32_t, int64_t, B, U, true, 2>(prod_args(2 * cus), 2 * cus, 0);
         else if (v.kind == 1)
-          detail::launch_stream<SumOp, int32_t, int64_t, B, U, true, false, 4>(prod_args(cus), cus, 0);
+          detail::launch_stream<SumOp, int32_t, int64_t, B, U, true, 4>(prod_args(cus), cus, 0);
         else if (v.kind == 3)
-          detail::launch_stream<SumOp, int32_t, int64_t, B, U, true, false, 4>(prod_args(cus, kSkew), cus, 0);
+          detail::launch_stream<SumOp, int32_t, int64_t, B, U, true, 4>(prod_args(cus, kSkew), cus, 0);
         else {
           const uint32_t dd = v.kind == 4 ? kSkew : 0u;
           const uint32_t ra = static_cast<uint32_t>((ntiles - static_cast<uint64_t>(dd) * (cus / 2)) / cus);

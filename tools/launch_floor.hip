@@ -10,7 +10,7 @@
 //                          ordinary device memory instead of uncached;
 //   reduce_<n>             the production kern::reduce_stream (tuned plan, polled fan-in) over n
 //                          doubles, its result checked against a host sum (_coarse: on a Workspace
-//                          made with MIREDUCE_SLOTS=coarse).
+//                          made with SlotMemory::Coarse).
 //   build: make launch_floor     run: build/bin/launch_floor [--rounds=7] [--launches=200]
 #include <hip/hip_runtime.h>
 
@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void empty_kernel(int) {}
 
 __global__ __launch_bounds__(256) void args_kernel(kern::Args a) {
   if (blockIdx.x == 0 && threadIdx.x == 0)
-    *static_cast<uint64_t*>(a.out) = a.nvec + a.head + a.tail + static_cast<uint64_t>(a.groups) + a.fan_bound;
+    *static_cast<uint64_t*>(a.out) = a.nvec + a.head + a.tail + static_cast<uint64_t>(a.two_pass) + a.fan_bound;
 }
 
 // The polled fan-in without data: every workgroup publishes (epoch << 32 | 1) to its slot, the last
@@ -106,9 +106,7 @@ int main(int argc, char** argv) {
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   Workspace ws(0, 16384);
-  setenv("MIREDUCE_SLOTS", "coarse", 1);  // the A/B workspace: fan-in words in ordinary device memory
-  Workspace ws_coarse(0, 16384);
-  unsetenv("MIREDUCE_SLOTS");
+  Workspace ws_coarse(0, 16384, SlotMemory::Coarse);  // the A/B workspace: fan-in words in ordinary memory
   const std::vector<uint64_t> sizes = {1024, 1ull << 24, 125000000};
   const uint64_t nmax = sizes.back();
   double* x = nullptr;

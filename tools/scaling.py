@@ -31,6 +31,12 @@ poll, the most waiting ~ skew + xGMI latency). So a loss of efficiency at N=8
 splits into the per-GPU rate at the smaller shard (local ms vs N=1), the exchange and the skew.
 
     python tools/scaling.py SCALE_r01.json bench_*.json --out results/scaling
+    python tools/scaling.py --from SCALE_r06.json --out results/scaling --update-writeup docs/WRITEUP.md
+
+``--from`` is the one command for the driver's scaling record: results files, scaling.md, the
+reduce.c vector tables, the WRITEUP table (measured next to the one-GPU projection) and both report
+figures (tools/report.py); a skipped record, a missing rank count or an unverified N fails it
+(rc 2, nothing written) — a curve is never interpolated.
 
 Round 5+ lines are compact: each names its extras sidecar (``summary.extras_file``, bench.py's
 ``--extras-file``), which is merged in when found (as named or next to the input file); a
@@ -302,11 +308,134 @@ def write(summary, out_dir):
     return text
 
 
+# ---------------------------------------------------------------- --from: a driver's SCALE record
+HEADLINE_MODEL = "xgmi_1b_double_sum"
+HEADLINE_BYTES = 8e9
+# docs/WRITEUP.md §2's projection, from one-GPU measurements only: a shard of G GB streams in
+# G x 135.56 us plus ~1.9 us per launch (profiles/r5_floor/), plus the exchange t_x per step
+PROJ_US_PER_GB, PROJ_LAUNCH_US = 135.56, 1.9
+
+
+def projection(n: int, t_x_us: float = 0.0) -> float:
+    """Projected whole-node GB/s of the headline at N GPUs (8 GB over N shards) with exchange t_x."""
+    return HEADLINE_BYTES / ((HEADLINE_BYTES / 1e9 / n * PROJ_US_PER_GB + PROJ_LAUNCH_US + t_x_us) * 1e-6) / 1e9
+
+
+class ScalingError(RuntimeError):
+    pass
+
+
+def check_curve(per_n: dict, require) -> None:
+    """Refuse a partial or unverified curve (never interpolate): every required N measured, every
+    measured N verified."""
+    missing = [n for n in require if n not in per_n]
+    bad = [f"N={n} ({'unverified' if v.get('verified') is None else 'verification FAILED'})"
+           for n, v in sorted(per_n.items()) if v.get("verified") is not True]
+    msgs = []
+    if missing:
+        msgs.append("no headline result for " + ", ".join(f"N={n}" for n in missing))
+    if bad:
+        msgs.append("not verified: " + ", ".join(bad))
+    if msgs:
+        raise ScalingError("; ".join(msgs))
+
+
+def writeup_table(per_n: dict) -> str:
+    """The WRITEUP §2 table with the measured values next to the projection they replace."""
+    rows = ["| N | shard | measured GB/s | ms/step | efficiency | projection t_x = 0 | projection t_x = measured wait "
+            "| measured / projection | local us/step | exchange us/step | skew us/step | combine |",
+            "|---|---|---|---|---|---|---|---|---|---|---|---|"]
+    eff = efficiency(per_n)
+    for n, v in sorted(per_n.items()):
+        p0 = projection(n)
+        tx = v.get("wait_max_us")
+        px = projection(n, tx) if tx is not None else None
+        e = eff[n][1]
+        f = lambda x, fmt: "" if x is None else fmt % x  # noqa: E731
+        rows.append(f"| {n} | {8 / n:g} GB | {v['gbps']:.1f} | {f(v['ms'], '%.5f')} | {f(None if e is None else 100 * e, '%.1f %%')} "
+                    f"| {p0:.0f} | {f(px, '%.0f')} | {v['gbps'] / p0:.3f} | {f(None if v.get('local_ms') is None else 1e3 * v['local_ms'], '%.1f')} "
+                    f"| {f(v.get('exchange_us'), '%.2f')} | {f(v.get('skew_us'), '%.2f')} | {v.get('combine', '')} |")
+    return "\n".join(rows) + "\n"
+
+
+WRITEUP_BEGIN, WRITEUP_END = "<!-- scaling:begin -->", "<!-- scaling:end -->"
+
+
+def update_writeup(path: str, table: str, source: str) -> bool:
+    """Replace the text between the scaling markers of docs/WRITEUP.md with the measured table."""
+    text = open(path).read()
+    if WRITEUP_BEGIN not in text or WRITEUP_END not in text:
+        return False
+    head, rest = text.split(WRITEUP_BEGIN, 1)
+    _, tail = rest.split(WRITEUP_END, 1)
+    body = (f"\nMeasured by the driver's scaling run (`{source}`, via `tools/scaling.py --from`), next to the "
+            "one-GPU projection it replaces:\n\n" + table)
+    with open(path, "w") as f:
+        f.write(head + WRITEUP_BEGIN + body + WRITEUP_END + tail)
+    return True
+
+
+def from_driver(paths, out_dir: str, require=(1, 2, 4, 8), writeup: "str | None" = None) -> dict:
+    """A driver's scaling record(s) (SCALE_r*.json: per-N bench.py runs, their printed lines kept in
+    stdout tails) -> the results files, scaling.md, the reduce.c vector tables, the WRITEUP table
+    (writeup_scaling.md; docs/WRITEUP.md's marked section too with ``writeup``) and both report
+    figures (tools/report.py). Raises ScalingError — writing nothing — when a record was skipped, a
+    required rank count is missing or any N is unverified."""
+    results = []
+    for p in paths:
+        text = open(p).read()
+        try:
+            doc = json.loads(text)
+        except ValueError:
+            doc = None
+        if isinstance(doc, dict) and doc.get("skipped"):
+            raise ScalingError(f"{p}: the driver skipped the scaling run ({doc.get('reason', 'no reason given')})")
+        results.extend(with_sidecar(r, os.path.dirname(os.path.abspath(p))) for r in parse_text(text))
+    results = dedupe(results)
+    head = [r for r in results if key_of(r)[0] == HEADLINE_MODEL]
+    summ = summarise(head)
+    per_n = next((v for k, v in summ.items() if k[0] == HEADLINE_MODEL), {})
+    check_curve(per_n, require)
+    os.makedirs(out_dir, exist_ok=True)
+    md = write(summ, out_dir)
+    vs = summarise_vector(results)
+    write_vector(vs, out_dir)
+    write_collected(results, out_dir)
+    table = writeup_table(per_n)
+    with open(os.path.join(out_dir, "writeup_scaling.md"), "w") as f:
+        f.write(table)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import report
+    figs = report.make_figures(os.path.join(out_dir, "figures"), bench_path=paths[0],
+                               vector_dir=os.path.join(out_dir, "vector_direct"))
+    updated = update_writeup(writeup, table, ", ".join(os.path.basename(p) for p in paths)) if writeup else False
+    return {"scaling_md": md, "writeup_table": table, "figures": figs, "writeup_updated": updated,
+            "vector": sorted(vs)}
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("inputs", nargs="*", help="files with bench.py JSON (default: stdin)")
     ap.add_argument("--out", default="results/scaling")
+    ap.add_argument("--from", dest="from_", nargs="+", default=None, metavar="SCALE_rNN.json",
+                    help="the driver's scaling record(s): results files, tables, the WRITEUP table and both "
+                         "figures; fails (rc 2, nothing written) on a skipped run, a missing rank count "
+                         "(--require) or an unverified N")
+    ap.add_argument("--require", default="1,2,4,8", help="rank counts the curve must have (--from)")
+    ap.add_argument("--update-writeup", default=None, metavar="docs/WRITEUP.md",
+                    help="--from: also replace the marked scaling section of this file")
     a = ap.parse_args(argv)
+    if a.from_:
+        try:
+            r = from_driver(a.from_, a.out, tuple(int(v) for v in a.require.split(",") if v), a.update_writeup)
+        except ScalingError as e:
+            print(f"[scaling] refusing to build the scaling curve: {e}", file=sys.stderr)
+            return 2
+        print(r["scaling_md"], end="")
+        print(r["writeup_table"], end="")
+        for p in r["figures"]:
+            print(p)
+        return 0
     results = []
     if a.inputs:
         for p in a.inputs:

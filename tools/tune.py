@@ -38,9 +38,7 @@ def main():
     p.add_argument("--blocks", default="256,512")
     p.add_argument("--unrolls", default="2,4,8")
     p.add_argument("--wgs", default="0,2,4,8")
-    p.add_argument("--groups", default="8")
     p.add_argument("--policies", default="nt,default")
-    p.add_argument("--pipes", default="0", help="comma list of 0/1: software-pipelined body off/on")
     p.add_argument("--windows", default="0", help="comma list of explicit load windows (0 = hipcc's schedule, 2, 4; "
                                                   "non-nt / unsupported plans fall back to 0 and are skipped)")
     p.add_argument("--json", default="")
@@ -62,17 +60,13 @@ def main():
 def sweep(a, x, n, dt, dev):
     es = x.element_size()
     variants = []
-    for b, u, w, g, pol, pp, win in itertools.product(
+    for b, u, w, pol, win in itertools.product(
         [int(v) for v in a.blocks.split(",")], [int(v) for v in a.unrolls.split(",")],
-        [int(v) for v in a.wgs.split(",")], [int(v) for v in a.groups.split(",")], a.policies.split(","),
-        [int(v) for v in a.pipes.split(",")], [int(v) for v in a.windows.split(",")]):
-        if pp and b * u > 8192:
-            continue
-        if win and (pp or pol == "default" or b not in (256, 512) or u > 8 or u % win):
+        [int(v) for v in a.wgs.split(",")], a.policies.split(","), [int(v) for v in a.windows.split(",")]):
+        if win and (pol == "default" or b not in (256, 512) or u > 8 or u % win):
             continue  # no such window variant (reduce_kernels.hpp window_ok)
-        variants.append(KernelConfig(block=b, unroll=u, wg_per_cu=w, groups=g,
-                                     nontemporal=None if pol == "auto" else pol == "nt", pipelined=bool(pp),
-                                     window=win))
+        variants.append(KernelConfig(block=b, unroll=u, wg_per_cu=w,
+                                     nontemporal=None if pol == "auto" else pol == "nt", window=win))
     r = Reducer(dev)
     from cuda_mpi_reductions_amd.ops import default_acc_dtype
     out = torch.empty(1, dtype=default_acc_dtype(dt, a.op), device=dev)
@@ -104,8 +98,8 @@ def sweep(a, x, n, dt, dev):
         med = statistics.median(times[i])
         mn = min(times[i])
         rows.append({
-            "block": cfg.block, "unroll": cfg.unroll, "wg_per_cu": cfg.wg_per_cu, "groups": cfg.groups,
-            "policy": {None: "auto", True: "nt", False: "default"}[cfg.nontemporal], "pipe": int(bool(cfg.pipelined)),
+            "block": cfg.block, "unroll": cfg.unroll, "wg_per_cu": cfg.wg_per_cu,
+            "policy": {None: "auto", True: "nt", False: "default"}[cfg.nontemporal],
             "window": cfg.window,
             "median_ms": med, "min_ms": mn,
             "median_TBps": n * es / (med * 1e-3) / 1e12, "best_TBps": n * es / (mn * 1e-3) / 1e12,
@@ -113,9 +107,9 @@ def sweep(a, x, n, dt, dev):
     rows.sort(key=lambda r_: r_["median_ms"])
     print(f"dtype={a.dtype} op={a.op} n={n} bytes={n * es} rounds={a.rounds} iters={a.iters}")
     top = a.top if a.top > 0 else len(rows)
-    print(f"{'block':>5} {'unroll':>6} {'wg/cu':>5} {'grp':>3} {'policy':>7} {'pipe':>4} {'win':>3} {'median ms':>10} {'TB/s med':>9} {'TB/s best':>9}")
+    print(f"{'block':>5} {'unroll':>6} {'wg/cu':>5} {'policy':>7} {'win':>3} {'median ms':>10} {'TB/s med':>9} {'TB/s best':>9}")
     for row in rows[:top]:
-        print(f"{row['block']:>5} {row['unroll']:>6} {row['wg_per_cu']:>5} {row['groups']:>3} {row['policy']:>7} {row['pipe']:>4} {row['window']:>3} "
+        print(f"{row['block']:>5} {row['unroll']:>6} {row['wg_per_cu']:>5} {row['policy']:>7} {row['window']:>3} "
               f"{row['median_ms']:>10.4f} {row['median_TBps']:>9.3f} {row['best_TBps']:>9.3f}")
     return {"n": n, "bytes": n * es, "rows": rows}
 

@@ -1,6 +1,6 @@
 // Production-kernel A/B of the streaming body's load schedule (profiles/r3_window/): hipcc's own
 // schedule (WIN 0) against an explicit in-flight window of WIN loads per thread
-// (reduce_kernels.hpp stream_window), for the plans that matter at the headline sizes. The real
+// (reduce_kernels.hpp stream_window_seq), for the plans that matter at the headline sizes. The real
 // kern::reduce_stream with the polled fan-in and a Workspace, hipEvent per launch, rounds
 // interleaved in a shuffled order, median per variant; every launch's result is checked.
 //   build: make window_ab        run: build/bin/window_ab [--n=1e9] [--rounds=7] [--iters=20] [--type=float]
@@ -35,7 +35,7 @@ struct Var {
 
 template <int B, int U, int W, class T = double>
 Var mk(const char* name, int wpc) {
-  return {name, B, U, wpc, detail::launch_stream<SumOp, T, double, B, U, true, false, W>};
+  return {name, B, U, wpc, detail::launch_stream<SumOp, T, double, B, U, true, W>};
 }
 
 // Control: the first window implementation (plain-pointer nontemporal loads, no sched_barrier
@@ -97,6 +97,69 @@ Var mkg(const char* name, int wpc) {
   return {name, B, U, wpc, launch_global_window<B, U, W>};
 }
 
+// Control: the STRICT window (consume first, then issue the next load: at most WIN in flight) with
+// the production buffer loads — the form the production body had as its WIN < 0 instantiation until
+// round 6 (1-70 % slower than the loose window, profiles/r3_window/), kept here only. Interleaved
+// tiles, partials + finalize like global_window.
+template <int BLOCK, int UNROLL, int WIN>
+__global__ __launch_bounds__(BLOCK) void strict_window(kern::Args a) {
+  using V = kern::Vec16<double>::type;
+  __shared__ double lds[BLOCK / 64];
+  double acc[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) acc[u] = 0.0;
+  const V* vin = static_cast<const V*>(a.body);
+  constexpr uint64_t kTile = static_cast<uint64_t>(BLOCK) * UNROLL;
+  constexpr uint32_t kStride = BLOCK * 16;
+  const uint64_t ntiles = a.nvec / kTile, g = gridDim.x;
+  const uint32_t voff = threadIdx.x * 16;
+  uint64_t t = blockIdx.x;
+  if (t < ntiles) {
+    __amdgpu_buffer_rsrc_t rp = kern::tile_rsrc(vin + t * kTile);
+    V buf[WIN];
+#pragma unroll
+    for (int j = 0; j < WIN; ++j) buf[j] = kern::ld_buf_nt<V>(rp, voff, j * kStride);
+    for (; t + g < ntiles; t += g) {
+      const __amdgpu_buffer_rsrc_t rq = kern::tile_rsrc(vin + (t + g) * kTile);
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        acc[u] += buf[u % WIN][0] + buf[u % WIN][1];
+        __builtin_amdgcn_sched_barrier(0);  // strict: the consume completes before the next load issues
+        const int j = u + WIN;
+        buf[u % WIN] = j < UNROLL ? kern::ld_buf_nt<V>(rp, voff, j * kStride)
+                                  : kern::ld_buf_nt<V>(rq, voff, (j - UNROLL) * kStride);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      rp = rq;
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      acc[u] += buf[u % WIN][0] + buf[u % WIN][1];
+      const int j = u + WIN;
+      if (j < UNROLL) buf[u % WIN] = kern::ld_buf_nt<V>(rp, voff, j * kStride);
+    }
+  }
+  for (uint64_t i = ntiles * kTile + blockIdx.x * BLOCK + threadIdx.x; i < a.nvec; i += g * BLOCK)
+    acc[0] += vin[i][0] + vin[i][1];
+#pragma unroll
+  for (int u = 1; u < UNROLL; ++u) acc[0] += acc[u];
+  const double v = kern::block_reduce<SumOp, double, BLOCK>(acc[0], lds);
+  if (threadIdx.x == 0) static_cast<double*>(a.partials)[blockIdx.x] = v;
+}
+
+template <int B, int U, int W>
+void launch_strict_window(const kern::Args& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((strict_window<B, U, W>), dim3(grid), dim3(B), 0, s, a);
+  hipLaunchKernelGGL((kern::finalize<SumOp, double>), dim3(1), dim3(256), 0, s,
+                     static_cast<const double*>(a.partials), static_cast<uint64_t>(grid), static_cast<double*>(a.out),
+                     nullptr, nullptr, 0u);
+}
+
+template <int B, int U, int W>
+Var mks(const char* name, int wpc) {
+  return {name, B, U, wpc, launch_strict_window<B, U, W>};
+}
+
 template <class T>
 __global__ void fill(T* x, uint64_t n) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull)
@@ -115,7 +178,7 @@ int main(int argc, char** argv) {
   }
   const size_t es = f32 ? 4 : 8;
   // l<D>: buffer loads, D registers, the next load issued before the consume (D + 1 in flight at
-  // issue; the production window, template WIN = D); w<D>: strict, consume first (WIN = -D);
+  // issue; the production window, template WIN = D); w<D>: strict, consume first (strict_window);
   // g<D>: the first (plain-pointer) window, control.
   std::vector<Var> vars64 = {
       mk<256, 8, 0>("256x8x1 hipcc", 1),  mk<256, 2, 0>("256x2x3 hipcc", 3),  mk<512, 16, 0>("512x16x1 hipcc", 1),
@@ -123,7 +186,7 @@ int main(int argc, char** argv) {
       mk<256, 4, 2>("256x4x2 l2", 2),     mk<256, 4, 4>("256x4x2 l4", 2),     mk<256, 4, 2>("256x4x3 l2", 3),
       mk<512, 8, 2>("512x8x1 l2", 1),     mk<512, 8, 4>("512x8x1 l4", 1),     mk<512, 4, 2>("512x4x1 l2", 1),
       mk<256, 8, 2>("256x8x2 l2", 2),     mk<256, 8, 4>("256x8x2 l4", 2),     mkg<256, 4, 2>("256x4x2 g2", 2),
-      mk<256, 8, -4>("256x8x1 w4", 1),    mk<256, 8, -8>("256x8x1 w8", 1),
+      mks<256, 8, 4>("256x8x1 w4", 1),    mks<256, 8, 8>("256x8x1 w8", 1),
   };  std::vector<Var> vars32 = {
       mk<512, 4, 0, float>("f32 512x4x1 hipcc", 1), mk<256, 2, 0, float>("f32 256x2x3 hipcc", 3),
       mk<256, 8, 0, float>("f32 256x8x1 hipcc", 1),
@@ -160,10 +223,7 @@ int main(int argc, char** argv) {
     a.nvec = p.nvec;
     a.tail = p.tail;
     a.partials = ws.partials();
-    a.group_partials = ws.group_partials();
-    a.tickets = ws.tickets();
     a.out = out;
-    a.groups = p.groups;
     a.slots = ws.slots();
     a.fan = ws.fan();
     a.fan_bound = kern::kFanBoundTicks;

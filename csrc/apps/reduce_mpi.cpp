@@ -277,7 +277,7 @@ int main(int argc, char** argv) {
 
     struct Buf {
       DType t;
-      uint64_t count;  // this rank's count (remainder spread over the first ranks)
+      uint64_t count;  // this rank's count: N/P on every rank (reduce.c:43-44; the remainder is not reduced)
       uint64_t total;  // elements actually reduced = sum of counts
       std::vector<unsigned char> send, recv;
     };

@@ -392,6 +392,24 @@ __device__ __forceinline__ bool resolve_anchor(TileSeq& q, const XcdAnchor& x, u
   return late;
 }
 
+// 8-byte integer MIN / MAX: gfx950 has no 64-bit integer min / max, so each element costs a compare
+// (into VCC) and two selects, and folding a vector's two elements into one accumulator chains two
+// such steps with a VCC wait state between them. Folded into two accumulators instead, the two
+// chains interleave (round 6, VERDICT r5 item 5: int64 MIN ran 0.6-0.9 % below int64 SUM).
+template <class OpT, class AccT>
+inline constexpr bool kSplitFold = std::is_integral_v<AccT> && sizeof(AccT) == 8 && !std::is_same_v<OpT, SumOp>;
+
+template <class OpT, class T, class AccT, class V, int N>
+__device__ __forceinline__ void consume_vec(AccT& a, AccT& b, const V& v) {
+  if constexpr (kSplitFold<OpT, AccT> && N == 2) {
+    a = OpT::apply(a, OpT::pre(elem<T, AccT>(v, 0)));
+    b = OpT::apply(b, OpT::pre(elem<T, AccT>(v, 1)));
+  } else {
+#pragma unroll
+    for (int k = 0; k < N; ++k) a = OpT::apply(a, OpT::pre(elem<T, AccT>(v, k)));
+  }
+}
+
 // The window body over a TileSeq. The next tile is found incrementally with 32-bit uniform counters
 // (scalar compares and branches: gfx950's SALU has no 64-bit less-than, and a first version that
 // indexed the runs with 64-bit compares put them on the VALU in front of every tile's loads, 0.15-0.4 %
@@ -427,6 +445,9 @@ __device__ __forceinline__ uint32_t stream_window_seq(AccT (&acc)[UNROLL], const
   uint32_t left = q.n0;  // tiles of the current run from t on
   const uint32_t voff = threadIdx.x * 16;
   __amdgpu_buffer_rsrc_t rp = tile_rsrc(vin + t * kTile);
+  AccT acc2[kSplitFold<OpT, AccT> ? UNROLL : 1];  // the second accumulators of a split fold
+#pragma unroll
+  for (int u = 0; u < (kSplitFold<OpT, AccT> ? UNROLL : 1); ++u) acc2[u] = OpT::template identity<AccT>();
   V buf[WIN];
 #pragma unroll
   for (int j = 0; j < WIN; ++j) buf[j] = ld_buf_nt<V>(rp, voff, j * kStride);
@@ -457,8 +478,7 @@ __device__ __forceinline__ uint32_t stream_window_seq(AccT (&acc)[UNROLL], const
     const __amdgpu_buffer_rsrc_t rq = tile_rsrc(vin + t * kTile);
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-#pragma unroll
-      for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(buf[u % WIN], k)));
+      consume_vec<OpT, T, AccT, V, N>(acc[u], acc2[u], buf[u % WIN]);
       const int j = u + WIN;
       buf[u % WIN] = j < UNROLL ? ld_buf_nt<V>(rp, voff, j * kStride) : ld_buf_nt<V>(rq, voff, (j - UNROLL) * kStride);
       __builtin_amdgcn_sched_barrier(0);
@@ -490,10 +510,13 @@ __device__ __forceinline__ uint32_t stream_window_seq(AccT (&acc)[UNROLL], const
   for (; n > 1; --n) step();
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {  // the last tile: no loads of a next one
-#pragma unroll
-    for (int k = 0; k < N; ++k) acc[u] = OpT::apply(acc[u], OpT::pre(elem<T, AccT>(buf[u % WIN], k)));
+    consume_vec<OpT, T, AccT, V, N>(acc[u], acc2[u], buf[u % WIN]);
     const int j = u + WIN;
     if (j < UNROLL) buf[u % WIN] = ld_buf_nt<V>(rp, voff, j * kStride);
+  }
+  if constexpr (kSplitFold<OpT, AccT>) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) acc[u] = OpT::apply(acc[u], acc2[u]);
   }
   return total;
 }

@@ -423,8 +423,9 @@ def test_bench_plan_tuning_at_the_eight_gpu_shard(tmp_path):
     assert pt["chosen"] == max(table, key=table.get) == pt["plan_by_rank"][0]
     assert d["summary"]["plans"] == pt["chosen"]
     plan = d["config"]["kernel_plan"]
-    # (block, unroll, window, xskew): 119 rounds per workgroup at the 1 GB shard
-    want = {"tuned default": (256, 8, 4, 2), "tuned default, XCD skew 0": (256, 8, 4, 0),
+    # (block, unroll, window, xskew): 119 rounds per workgroup at the 1 GB shard; the tuned default
+    # gives the favoured XCD parity 2 + 1.8 % of the rounds = 4 (round 5, profiles/r5_skew/)
+    want = {"tuned default": (256, 8, 4, 4), "tuned default, XCD skew 0": (256, 8, 4, 0),
             "tuned default, XCD skew 40": (256, 8, 4, 5), "tuned default, XCD skew -20": (256, 8, 4, -2),
             "256x4x2 window 2": (256, 4, 2, 0)}
     assert (plan["block"], plan["unroll"], plan["window"], plan["xskew"]) == want[pt["chosen"]]

@@ -20,8 +20,7 @@ for r in 1 2; do
       --pattern=iotamod --iterations=10 --log=none --master-log=none --json=$O/size_stride.jsonl
   done
 done
-# (round 3's first pass: MIREDUCE_SPLIT=contig is 2-10 % slower than the interleaved split at every size)
-unset MIREDUCE_SPLIT
+# (round 3: the contiguous split was 2-10 % slower than the interleaved one at every size; removed in round 6)
 P1=TCP_UTCL1_TRANSLATION_MISS_sum,TCP_UTCL1_TRANSLATION_HIT_sum,TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum,TCP_UTCL1_STALL_MULTI_MISS_sum,GRBM_UTCL2_BUSY,GRBM_GUI_ACTIVE
 P2=TCC_EA0_RDREQ_sum,TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum,TCC_TAG_STALL_sum,TCC_HIT_sum
 for n in 73000000000; do

@@ -268,8 +268,10 @@ def test_bench_graph_capture_failure_falls_back_on_all_ranks(tmp_path, monkeypat
     # gloo collectives on GPU tensors cannot be captured: every rank must agree on the failure
     # and fall back to eager issue (never some ranks replaying graphs and others not).
     monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    # (the extras are not this test's subject: without them it takes ~5 s instead of ~30 s)
     r = torchrun(2, [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "6",
-                     "--warmup", "2", "--elements", "20000003", "--launch", "graph", "--collective", "rccl"],
+                     "--warmup", "2", "--elements", "20000003", "--launch", "graph", "--collective", "rccl",
+                     "--no-vector-extras", "--no-candidates"],
                  cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = bench_record(r.stdout)

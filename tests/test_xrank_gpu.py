@@ -512,3 +512,31 @@ def test_bench_ranks_hold_different_plans_and_verify(tmp_path, monkeypatch, plan
     assert len(pt["plan_by_rank"]) == 2 and pt["plan_by_rank"][1] == plan, pt
     assert all(len(t) == 5 for t in pt["gbps_by_rank"])
     assert d["summary"]["plans"].count(" x") == (1 if pt["plan_by_rank"][0] == pt["plan_by_rank"][1] else 2)
+
+
+# ---------------------------------------------------------------- fail-soft optional stages (round 6)
+@pytest.mark.parametrize("fault", ["raise@1/tune", "raise@1/selfcheck", "hang@1/tune"])
+def test_bench_optional_stage_failure_two_ranks_one_gpu(tmp_path, monkeypatch, fault):
+    # VERDICT r5 item 1 on the GPU path: plan tuning (local launches on fresh workspaces, one bounded
+    # agreement) and the fused self-check (real fused launches, local error words) fail on rank 1 of
+    # two ranks sharing the GPU. raise -> every rank falls back (tuned default plan / RCCL), the
+    # headline is measured and verified, the reason named; hang -> the agreement names the stage and
+    # the lost rank within --agree-timeout, one line, no number.
+    monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
+    r = torchrun(2, [BENCH, "--no-vector-extras", "--no-candidates", "--gpus", "2", "--backend", "gloo", "--steps", "6",
+                     "--warmup", "2", "--elements", "250000000", "--tune-steps", "6", "--agree-timeout", "8",
+                     "--xrank-timeout", "3", "--inject-fault", fault], cwd=tmp_path, timeout=600)
+    lines = [ln for ln in r.stdout.splitlines() if "{" in ln]
+    assert len(lines) == 1, (r.stdout, r.stderr[-3000:])
+    d = json.loads(lines[0][lines[0].index("{"):])
+    if fault.startswith("raise"):
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert d["verified"] is True and d["value"] > 0
+        if fault.endswith("tune"):
+            assert d["config"]["collective"] == "fused" and "rank 1: InjectedFault" in d["config"]["plan_reason"]
+        else:
+            assert d["config"]["collective"] == "rccl"
+            assert d["config"]["collective_reason"].startswith("self-check: rank 1: InjectedFault")
+    else:
+        assert r.returncode != 0 and d["value"] is None
+        assert "plan tuning: rank(s) 1 did not report within 8 s" in d["error"], d

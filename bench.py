@@ -853,12 +853,15 @@ def _replay_probe(wl, ctx, args, fault, serial: bool, step, capture: bool) -> "s
     return "; ".join(f"rank {r}: {m}" for r, m in enumerate(errs) if m)[:300] or "failed on another rank"
 
 
-def _agree_timeout(args) -> float:
-    """The bound of an optional stage's agreement: --agree-timeout, cut so that a lost rank is
-    reported by the agreement (its stage named) before the headline deadline would fire."""
+def _agree_timeout(args, at_least: float = 0.0) -> float:
+    """The bound of an optional stage's agreement: --agree-timeout (or ``at_least``, the longest a
+    live rank can legitimately take to arrive: a fused step waits up to --xrank-timeout for a peer
+    that failed before launching), cut so that a lost rank is reported by the agreement (its stage
+    named) before the headline deadline would fire."""
+    want = max(args.agree_timeout, at_least)
     left = getattr(args, "_headline_ends", None)
-    cap = (left - time.time() - 5.0) if left else args.agree_timeout
-    return max(1.0, min(args.agree_timeout, cap))
+    cap = (left - time.time() - 5.0) if left else want
+    return max(1.0, min(want, cap))
 
 
 def _try_fused(wl, ctx, args, fault, at_stage=lambda name: None) -> "str | None":
@@ -903,7 +906,8 @@ def _try_fused(wl, ctx, args, fault, at_stage=lambda name: None) -> "str | None"
     except Exception as e:  # noqa: BLE001 - this rank's report carries it; every rank falls back together
         mine["error"] = f"{type(e).__name__}: {e}"[:200]
         print(f"[bench] rank {ctx.rank}: fused self-check failed here: {mine['error']}", file=sys.stderr, flush=True)
-    rows = pdist.agree(ctx, "fused self-check", mine, _agree_timeout(args))
+    # (a rank that failed before its steps makes the others' first fused step wait --xrank-timeout)
+    rows = pdist.agree(ctx, "fused self-check", mine, _agree_timeout(args, args.xrank_timeout + 10.0))
     if (mine.get("counts") or [0])[0]:
         wl.reset_fanin()  # this rank's sticky fan-in error was reported: clear it
     ok, ref = _selfcheck_verdict(rows, wl.cfg.op, wl.new_slots(1).dtype)

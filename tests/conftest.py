@@ -43,6 +43,10 @@ GPU_FULL_SUBSAMPLE = {
     # subprocess-heavy app sweeps (each case starts ranks)
     "test_reduce_xgmi_direct_peer_reads": 2, "test_reduce_xgmi_direct_tiny_counts": 2,
     "test_bench_ranks_hold_different_plans_and_verify": 3, "test_python_cli_gpu": 2,
+    # multi-rank rehearsals by rank count: the default tier keeps the 2-rank case (the 8-rank fused and
+    # direct tests cover the wide worlds), and one of maxloc's launch modes
+    "test_bench_fused_ranks_share_one_gpu": 2, "test_bench_vector_direct_ranks_share_one_gpu": 2,
+    "test_bench_maxloc_config": 2, "test_reduce_xgmi_peer_preflight_declines_on_every_rank": 2,
 }
 
 

@@ -524,7 +524,7 @@ def test_bench_optional_stage_failure_two_ranks_one_gpu(tmp_path, monkeypatch, f
     # the lost rank within --agree-timeout, one line, no number.
     monkeypatch.setenv("MIREDUCE_FORCE_DEVICE", "0")
     r = torchrun(2, [BENCH, "--no-vector-extras", "--no-candidates", "--gpus", "2", "--backend", "gloo", "--steps", "6",
-                     "--warmup", "2", "--elements", "250000000", "--tune-steps", "6", "--agree-timeout", "8",
+                     "--warmup", "2", "--elements", "250000000", "--tune-steps", "6", "--agree-timeout", "5",
                      "--xrank-timeout", "3", "--inject-fault", fault], cwd=tmp_path, timeout=600)
     lines = [ln for ln in r.stdout.splitlines() if "{" in ln]
     assert len(lines) == 1, (r.stdout, r.stderr[-3000:])
@@ -539,4 +539,4 @@ def test_bench_optional_stage_failure_two_ranks_one_gpu(tmp_path, monkeypatch, f
             assert d["config"]["collective_reason"].startswith("self-check: rank 1: InjectedFault")
     else:
         assert r.returncode != 0 and d["value"] is None
-        assert "plan tuning: rank(s) 1 did not report within 8 s" in d["error"], d
+        assert "plan tuning: rank(s) 1 did not report within 5 s" in d["error"], d

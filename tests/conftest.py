@@ -33,6 +33,13 @@ GPU_FULL_ONLY = {
     # tests/test_fault_injection.py, tests/test_bench_policy.py)
     "test_bench_extras_hang_in_rccl_candidate_keeps_the_headline",
 }
+# Single cases in the full tier only:
+GPU_FULL_CASES = {
+    # 10 s: the hang of a rank in plan tuning, GPU form (the bounded agreement that names it is the same
+    # store exchange as on CPU ranks, tested there at 4 ranks for every stage; the GPU tier keeps the
+    # raise cases, which run the GPU code of both stages)
+    "test_bench_optional_stage_failure_two_ranks_one_gpu[hang@1/tune]",
+}
 # Parametrized sweeps: the default tier keeps the cases whose parameter indices sum to 0 mod k — a
 # Latin-style subset in which every value of every parameter still appears (every combo, every size,
 # every window plan, ...), k-fold fewer cases.
@@ -84,7 +91,7 @@ _INDICES: dict = {}
 def _tier(item) -> "str | None":
     """'full' if the item belongs to the full GPU tier only."""
     name = _name(item)
-    if name in GPU_FULL_ONLY:
+    if name in GPU_FULL_ONLY or item.name in GPU_FULL_CASES:
         return "full"
     k = GPU_FULL_SUBSAMPLE.get(name)
     idx = _INDICES.get(item.nodeid)

@@ -53,6 +53,7 @@ def test_default_tier_keeps_every_parameter_value(tmp_path):
             assert {r["params"][p] for r in kept} == {r["params"][p] for r in cases}, (fn, p)
     full = [r for r in rows if r["tier"] == "full"]
     assert {r["name"] for r in full} >= set(cf.GPU_FULL_ONLY)
+    assert {c.split("[")[0] for c in cf.GPU_FULL_CASES} <= names
     # the protocol tests stay in the default tier
     for fn in ("test_bench_eight_ranks_fused_on_one_gpu", "test_reduce_xgmi_direct_eight_ranks_on_one_gpu",
                "test_segmented_launches_match_the_reference", "test_fused_poison_reaches_every_rank",

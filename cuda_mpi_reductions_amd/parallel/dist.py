@@ -239,7 +239,13 @@ def agree(ctx: DistContext, stage: str, payload: dict, timeout_s: float = 60.0) 
     try:
         store.wait(keys, datetime.timedelta(seconds=max(0.1, timeout_s)))
     except Exception:  # noqa: BLE001 - a store timeout (DistStoreError / RuntimeError): find who is missing
-        missing = [r for r, k in enumerate(keys) if not store.check([k])]
+        missing = []
+        for r, k in enumerate(keys):
+            try:
+                if not store.check([k]):
+                    missing.append(r)
+            except Exception:  # noqa: BLE001 - the store itself is gone (its host rank died)
+                missing.append(r)
         if missing:
             raise PeerLost(stage, missing, timeout_s) from None
     return [json.loads(store.get(k)) for k in keys]

@@ -882,12 +882,13 @@ def _try_fused(wl, ctx, args, fault, at_stage=lambda name: None) -> "str | None"
       instead of waiting in a collective until the process-group timeout.
 
     Fault sites ``canary`` / ``selfcheck`` (utils/fault.py) fire inside these stages."""
-    agree_s = _agree_timeout(args)
     if args.canary and ctx.world_size > 1:
         at_stage("canary")
         from cuda_mpi_reductions_amd.parallel.canary import fused_canary
+        # (a rank whose helper failed at once arrives up to --canary-timeout before one whose helper
+        # waited the full timeout for it: the bound outlasts that)
         err = fused_canary(ctx, timeout_s=args.canary_timeout, dry=ctx.device.type != "cuda", fault=fault,
-                           agree_timeout_s=agree_s)
+                           agree_timeout_s=_agree_timeout(args, args.canary_timeout + 10.0))
         if err is not None:
             return f"canary: {err}"[:300]
     at_stage("fused self-check")

@@ -123,16 +123,18 @@ def _helper() -> int:
 
 
 def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int = 1 << 20,
-                 kind: str = "fused", fault=None, agree_timeout_s: float = 60.0) -> Optional[str]:
+                 kind: str = "fused", fault=None, agree_timeout_s: float = 100.0) -> Optional[str]:
     """Collective over the default process group: None if every rank's helper ran the exchange
     correctly, else the agreed reason ("rank r: ..." for each failing rank). ``kind``: ``fused``
     (the fused cross-rank finish) or ``direct`` (the direct one-kernel collective and the peer-read
     probe, parallel/direct.py). World 1 maps no peer memory: None without a helper. ``dry`` (CPU
     tests): helpers rendezvous and all-reduce over gloo only.
 
-    The verdicts are agreed through :func:`.dist.agree` (bounded by ``agree_timeout_s``): a rank
-    whose own part failed in Python still reports (its verdict is the error), and a rank that died
-    or hangs raises :class:`.dist.PeerLost` on the others instead of holding them in a collective.
+    The verdicts are agreed through :func:`.dist.agree` (bounded by ``agree_timeout_s``, which must
+    outlast ``timeout_s``: a rank whose helper failed at once arrives up to ``timeout_s`` before one
+    whose helper waited for it): a rank whose own part failed in Python still reports (its verdict is
+    the error), and a rank that died or hangs raises :class:`.dist.PeerLost` on the others instead of
+    holding them in a collective.
     ``fault`` (utils.fault, site ``canary``) fires after this rank's helper ended."""
     from .dist import agree
     import torch.distributed as dist
@@ -210,7 +212,7 @@ def fused_canary(ctx, timeout_s: float = 90.0, dry: bool = False, elements: int 
 def direct_canary(ctx, timeout_s: float = 90.0, dry: bool = False) -> Optional[str]:
     """:func:`fused_canary` for the direct one-kernel collective (bench.py runs it before its
     reduce.c table's direct rows and the xGMI peer-read probe)."""
-    return fused_canary(ctx, timeout_s=timeout_s, dry=dry, kind="direct", agree_timeout_s=timeout_s)
+    return fused_canary(ctx, timeout_s=timeout_s, dry=dry, kind="direct", agree_timeout_s=timeout_s + 10.0)
 
 
 if __name__ == "__main__":

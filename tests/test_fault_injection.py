@@ -27,7 +27,7 @@ def _json(r):
 
 
 REHEARSE = ["--gpus", "4", "--device", "cpu", "--elements", "200003", "--steps", "6", "--warmup", "2",
-            "--rehearse-stages", "--canary-timeout", "30", "--agree-timeout", "8", "--xrank-timeout", "2",
+            "--rehearse-stages", "--canary-timeout", "20", "--agree-timeout", "8", "--xrank-timeout", "2",
             "--no-decompose"]
 STAGE = {"canary": "canary", "selfcheck": "fused self-check", "tune": "plan tuning"}
 
@@ -64,8 +64,9 @@ def test_optional_headline_stage_failure_on_one_of_four_ranks(tmp_path, site, ki
     else:
         assert r.returncode != 0
         assert d["value"] is None and f"(stage: {STAGE[site]})" in d["error"], d
-        if kind == "hang":  # (the self-check's bound also outlasts the fused wait: --xrank-timeout + 10 s)
-            want = "within 12 s" if site == "selfcheck" else "within 8 s"
+        if kind == "hang":  # (the canary's and the self-check's bounds outlast the helper / fused waits:
+            # --canary-timeout + 10 s, --xrank-timeout + 10 s)
+            want = {"canary": "within 30 s", "selfcheck": "within 12 s"}.get(site, "within 8 s")
             assert f"rank(s) 2 did not report {want}" in d["error"], d
         else:
             assert "terminated" in d["error"] or "rank(s) 2 did not report" in d["error"], d

@@ -68,7 +68,7 @@ def _param_indices(items) -> dict:
     by_fn = {}
     for it in items:
         if _name(it) in GPU_FULL_SUBSAMPLE and getattr(it, "callspec", None) is not None:
-            by_fn.setdefault((it.fspath, _name(it)), []).append(it)
+            by_fn.setdefault((str(it.path), _name(it)), []).append(it)
     out = {}
     for its in by_fn.values():
         names = list(its[0].callspec.params)

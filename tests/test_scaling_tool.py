@@ -301,3 +301,15 @@ def test_report_figures_regenerate_from_committed_data(tmp_path):
     assert labels["ref CUDA SUM"] == 90.8413 and labels["MI355X 1 GPU SUM"] == 7200.0
     assert 1 in labels["reduce.c, 8-CPU MPICH SUM"] and 8 in labels["reduce.c, 8-CPU MPICH SUM"]
     assert labels["MI355X reduce.c (direct) SUM"][1] > 1000  # BENCH_r05's N=1 direct row (GiB/s -> GB/s)
+
+
+def test_bare_driver_line_decomposition_from_its_summary(tmp_path):
+    # the driver's records keep the printed line only (its sidecar stays on the GPU box): the table's
+    # decomposition columns come from the line's summary (local GB/s, exchange, skew, fused wait)
+    out = tmp_path / "r"
+    r = scaling.from_driver([os.path.join(ROOT, "BENCH_r05.json")], str(out), require=(1,))
+    row = [ln for ln in r["writeup_table"].splitlines() if ln.startswith("| 1 |")][0].split("|")
+    assert row[9].strip() == "1091.1" and row[10].strip() == "3.81"  # local us/step, exchange us/step
+    v = scaling.summarise(scaling.dedupe(scaling.parse_text(open(os.path.join(ROOT, "BENCH_r05.json")).read())))
+    per_n = v[("xgmi_1b_double_sum", "DOUBLE", "SUM")][1]
+    assert per_n["verified"] is True and per_n["wait_min_us"] == 0.24 and per_n["runs"] == 1

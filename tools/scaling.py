@@ -183,11 +183,35 @@ DECOMP = (("local_ms", "local_ms_per_step"), ("exchange_us", "exchange_us_per_st
           ("skew_us", "skew_us_per_step"), ("vs_local", "scaling_efficiency_vs_local"))
 
 
+def _decomp_of(r) -> dict:
+    """A run's decomposition: the sidecar's ``decomposition``, or — for a bare printed line (the
+    driver's records keep no sidecar) — the same fields rebuilt from the line's ``summary``
+    (``local_gbps``, ``exchange_us``, ``skew_us``, ``efficiency_vs_local``, ``wait_us`` = [min, max])."""
+    d = r.get("decomposition")
+    if isinstance(d, dict) and d:
+        return d
+    s = r.get("summary") if isinstance(r.get("summary"), dict) else {}
+    cfg = r.get("config") or {}
+    out = {}
+    nbytes = cfg.get("bytes_per_step")
+    if s.get("local_gbps") and nbytes:
+        out["local_ms_per_step"] = float(nbytes) / (float(s["local_gbps"]) * 1e9) * 1e3
+    for field, key in (("exchange_us_per_step", "exchange_us"), ("skew_us_per_step", "skew_us"),
+                       ("scaling_efficiency_vs_local", "efficiency_vs_local")):
+        if s.get(key) is not None:
+            out[field] = s[key]
+    w = s.get("wait_us")
+    if isinstance(w, (list, tuple)) and len(w) == 2:
+        out["exchange_wait_us"] = {"min_rank_median": w[0], "max_rank_median": w[1]}
+    return out
+
+
 def _decomposition(rs) -> dict:
     """Mean of each bench.py ``decomposition`` field over the runs that carry it (None if none do),
     plus the device-timed fused exchange wait (``exchange_wait_us``: least / most waiting rank)."""
     out = {}
-    decs = [d for d in (r.get("decomposition") or {} for r in rs) if isinstance(d, dict)]
+    decs = [_decomp_of(r) for r in rs]
+    decs = [d for d in decs if d]
     for name, field in DECOMP:
         vals = [float(d[field]) for d in decs if d.get(field) is not None]
         out[name] = sum(vals) / len(vals) if vals else None

@@ -274,6 +274,16 @@ def test_from_driver_record_refuses_partial_or_unverified_curves(tmp_path):
                            text=True, timeout=120)
         assert r.returncode == 2 and want in r.stderr, (r.stdout, r.stderr)
         assert not out.exists()  # nothing written, nothing interpolated
+    # a rank count whose run printed only its diagnostic line: the refusal quotes it
+    src = _scale_record(tmp_path, ns=(1, 2, 4))
+    doc = json.loads(src.read_text())
+    diag = {"metric": doc["runs"][0]["tail"].split('"metric": "')[1].split('"')[0], "value": None, "n_gpus": 8,
+            "error": "headline phase did not finish within 155 s (stage: canary); no measurement"}
+    doc["runs"].append({"n": 8, "rc": 2, "tail": json.dumps(diag)})
+    src.write_text(json.dumps(doc))
+    r = subprocess.run([sys.executable, tool, "--from", str(src), "--out", str(tmp_path / "x")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 2 and "N=8 (its run: headline phase did not finish" in r.stderr, r.stderr
     skipped = tmp_path / "SCALE_skip.json"
     skipped.write_text(json.dumps({"skipped": True, "reason": "no 8-GPU node"}))
     r = subprocess.run([sys.executable, tool, "--from", str(skipped), "--out", str(tmp_path / "s")],

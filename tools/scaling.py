@@ -349,15 +349,17 @@ class ScalingError(RuntimeError):
     pass
 
 
-def check_curve(per_n: dict, require) -> None:
+def check_curve(per_n: dict, require, failed: "dict | None" = None) -> None:
     """Refuse a partial or unverified curve (never interpolate): every required N measured, every
-    measured N verified."""
+    measured N verified. ``failed``: {N: error} of the runs that printed no number (their
+    diagnostic lines), quoted for the missing rank counts."""
     missing = [n for n in require if n not in per_n]
     bad = [f"N={n} ({'unverified' if v.get('verified') is None else 'verification FAILED'})"
            for n, v in sorted(per_n.items()) if v.get("verified") is not True]
     msgs = []
     if missing:
-        msgs.append("no headline result for " + ", ".join(f"N={n}" for n in missing))
+        msgs.append("no headline result for " + ", ".join(
+            f"N={n}" + (f" (its run: {str((failed or {})[n])[:160]})" if n in (failed or {}) else "") for n in missing))
     if bad:
         msgs.append("not verified: " + ", ".join(bad))
     if msgs:
@@ -419,7 +421,10 @@ def from_driver(paths, out_dir: str, require=(1, 2, 4, 8), writeup: "str | None"
     head = [r for r in results if key_of(r)[0] == HEADLINE_MODEL]
     summ = summarise(head)
     per_n = next((v for k, v in summ.items() if k[0] == HEADLINE_MODEL), {})
-    check_curve(per_n, require)
+    # (a run that printed only its diagnostic line carries the metric but no config)
+    failed = {int(r["n_gpus"]): r.get("error") or "no value" for r in results
+              if r.get("value") is None and (key_of(r)[0] == HEADLINE_MODEL or "1B-double" in str(r.get("metric")))}
+    check_curve(per_n, require, failed)
     os.makedirs(out_dir, exist_ok=True)
     md = write(summ, out_dir)
     vs = summarise_vector(results)

@@ -370,3 +370,22 @@ def test_final_line_leaves_an_ignored_signal_ignored():
         "print('emitted' if C.emit_final_line('{\"value\": 6}') else 'lost', flush=True)\n")
     assert r.returncode == 0, r.stderr
     assert r.stdout.splitlines() == ['{"value": 6}', "emitted"], r.stdout
+
+
+def test_relayed_line_behind_a_fragment_counts_as_the_result(capsys):
+    # a rank's line written on the signal path (write(2)) can follow an unterminated piece
+    # of Python's buffered stdout on the same line; the self-spawning parent must still see a result
+    # (and print no diagnostic line of its own after it)
+    import importlib.util
+    import subprocess
+    import sys
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    code = ("import os, sys, json\nsys.stdout.write('[progress] half a li'); sys.stdout.flush()\n"
+            "os.write(1, (json.dumps({'metric': 'm', 'value': 3.0, 'n_gpus': 2}) + '\\n').encode())\n")
+    child = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, start_new_session=True)
+    rc = b._relay_child(child, time.time() + 60, 2)
+    out = capsys.readouterr().out
+    assert rc == 0 and out.count('"metric"') == 1 and '"value": 3.0' in out, out
+    assert b._is_result_line('noise {"metric": "m", "value": null}') and not b._is_result_line("{not json")

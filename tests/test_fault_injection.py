@@ -389,3 +389,21 @@ def test_relayed_line_behind_a_fragment_counts_as_the_result(capsys):
     out = capsys.readouterr().out
     assert rc == 0 and out.count('"metric"') == 1 and '"value": 3.0' in out, out
     assert b._is_result_line('noise {"metric": "m", "value": null}') and not b._is_result_line("{not json")
+
+
+@pytest.mark.parametrize("test_mode", [False, True])
+def test_plan_for_rank_hook_only_in_test_runs(tmp_path, test_mode):
+    # MIREDUCE_PLAN_FOR_RANK (forces a rank onto a plan candidate) is honoured only with
+    # MIREDUCE_TEST=1, and the record then says so (plan_tuning.forced_by_env)
+    from helpers import bench_record
+    env = {"MIREDUCE_EXTRAS_DIR": str(tmp_path), "MIREDUCE_PLAN_FOR_RANK": "1=256x4x2 window 2"}
+    if test_mode:
+        env["MIREDUCE_TEST"] = "1"
+    r = torchrun(2, [BENCH, "--gpus", "2", "--device", "cpu", "--elements", "200003", "--steps", "4", "--warmup", "1",
+                     "--rehearse-stages", "--canary-timeout", "20", "--no-decompose"], cwd=tmp_path, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    pt = bench_record(r.stdout)["plan_tuning"]
+    if test_mode:
+        assert pt["plan_by_rank"][1] == "256x4x2 window 2" and pt["forced_by_env"] == {"1": "256x4x2 window 2"}
+    else:
+        assert "forced_by_env" not in pt

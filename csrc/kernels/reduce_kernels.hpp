@@ -394,16 +394,21 @@ __device__ __forceinline__ bool resolve_anchor(TileSeq& q, const XcdAnchor& x, u
 
 // 8-byte integer MIN / MAX: gfx950 has no 64-bit integer min / max, so each element costs a compare
 // (into VCC) and two selects, and folding a vector's two elements into one accumulator chains two
-// such steps with a VCC wait state between them. Folded into two accumulators instead, the two
-// chains interleave (round 6, VERDICT r5 item 5: int64 MIN ran 0.6-0.9 % below int64 SUM).
-template <class OpT, class AccT>
+// such steps with a VCC wait state between them. Folded alternately into two accumulators, the two
+// chains interleave (round 6, VERDICT r5 item 5: +0.24 % for int64 MIN, profiles/r6_ops/). The same
+// split of the widening sums (int32 into int64, fp32 into fp64) measured 0-0.9 % SLOWER
+// (profiles/r6_fold/), so they keep the single chain.
+template <class OpT, class T, class AccT>
 inline constexpr bool kSplitFold = std::is_integral_v<AccT> && sizeof(AccT) == 8 && !std::is_same_v<OpT, SumOp>;
 
 template <class OpT, class T, class AccT, class V, int N>
 __device__ __forceinline__ void consume_vec(AccT& a, AccT& b, const V& v) {
-  if constexpr (kSplitFold<OpT, AccT> && N == 2) {
-    a = OpT::apply(a, OpT::pre(elem<T, AccT>(v, 0)));
-    b = OpT::apply(b, OpT::pre(elem<T, AccT>(v, 1)));
+  if constexpr (kSplitFold<OpT, T, AccT>) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      if (k & 1) b = OpT::apply(b, OpT::pre(elem<T, AccT>(v, k)));
+      else a = OpT::apply(a, OpT::pre(elem<T, AccT>(v, k)));
+    }
   } else {
 #pragma unroll
     for (int k = 0; k < N; ++k) a = OpT::apply(a, OpT::pre(elem<T, AccT>(v, k)));
@@ -445,9 +450,9 @@ __device__ __forceinline__ uint32_t stream_window_seq(AccT (&acc)[UNROLL], const
   uint32_t left = q.n0;  // tiles of the current run from t on
   const uint32_t voff = threadIdx.x * 16;
   __amdgpu_buffer_rsrc_t rp = tile_rsrc(vin + t * kTile);
-  AccT acc2[kSplitFold<OpT, AccT> ? UNROLL : 1];  // the second accumulators of a split fold
+  AccT acc2[kSplitFold<OpT, T, AccT> ? UNROLL : 1];  // the second accumulators of a split fold
 #pragma unroll
-  for (int u = 0; u < (kSplitFold<OpT, AccT> ? UNROLL : 1); ++u) acc2[u] = OpT::template identity<AccT>();
+  for (int u = 0; u < (kSplitFold<OpT, T, AccT> ? UNROLL : 1); ++u) acc2[u] = OpT::template identity<AccT>();
   V buf[WIN];
 #pragma unroll
   for (int j = 0; j < WIN; ++j) buf[j] = ld_buf_nt<V>(rp, voff, j * kStride);
@@ -514,7 +519,7 @@ __device__ __forceinline__ uint32_t stream_window_seq(AccT (&acc)[UNROLL], const
     const int j = u + WIN;
     if (j < UNROLL) buf[u % WIN] = ld_buf_nt<V>(rp, voff, j * kStride);
   }
-  if constexpr (kSplitFold<OpT, AccT>) {
+  if constexpr (kSplitFold<OpT, T, AccT>) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) acc[u] = OpT::apply(acc[u], acc2[u]);
   }

@@ -114,6 +114,8 @@ Defaults tuned_defaults(size_t bytes, DType t, Op op) {
   // accumulation doubles the VALU work per load, collapses with it (6.06-6.22 TB/s) and streams
   // best as 256x8x2 with a window of 2 (7.15-7.27, first at every size); 16-bit MIN/MAX run the
   // window-4 plan at 7.13 and 256x8x2 window 2 at 7.25 (8 GB f16 MAX; the old 256x4x2: 7.16).
+  // (Rechecked in round 6 on two boxes, profiles/r6_plan/: no consistent int32 SUM winner, and the
+  // 256x8x2 window-2 plan first for all four 16-bit MIN / MAX pairs at 1-4 GB.)
   const bool widening_int = t == DType::Int32 && (op == Op::Sum || op == Op::SumSq);
   const bool half_cmp = dtype_is_half(t) && op != Op::Sum && op != Op::SumSq;
   if (dtype_size(t) == 8 && bytes > 192 * MB) return {256, 8, 1, 1, 4};

@@ -49,6 +49,7 @@ GPU_FULL_SUBSAMPLE = {
     "test_gpu_full_reduction": 2, "test_fused_world1_matches_torch": 2,
     # subprocess-heavy app sweeps (each case starts ranks)
     "test_reduce_xgmi_direct_peer_reads": 2, "test_reduce_xgmi_direct_tiny_counts": 2,
+    "test_reduce_xgmi_scalar_fused": 2,
     "test_bench_ranks_hold_different_plans_and_verify": 3, "test_python_cli_gpu": 2,
     # multi-rank rehearsals by rank count: the default tier keeps the 2-rank case (the 8-rank fused and
     # direct tests cover the wide worlds), and one of maxloc's launch modes

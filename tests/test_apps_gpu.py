@@ -146,7 +146,7 @@ def test_reduction_shmoo(tmp_path):
 
 def test_reduce_xgmi_single_rank_scalar_and_graph(tmp_path):
     for extra in ([], ["--graph"]):
-        r = run([os.path.join(BIN, "reduce_xgmi"), "--mode=scalar", "--n=20000003", "--dtypes=INT,LONG,FLOAT,DOUBLE",
+        r = run([os.path.join(BIN, "reduce_xgmi"), "--mode=scalar", "--n=6000007", "--dtypes=INT,LONG,FLOAT,DOUBLE",
                  "--retries=1", "--iters=3", *extra], timeout=600)
         assert r.returncode == 0, r.stderr[-3000:]
         assert "verification PASSED" in r.stderr

@@ -370,8 +370,12 @@ def test_bench_eight_ranks_auto_on_one_gpu(tmp_path, monkeypatch):
 
 
 def test_reduce_xgmi_direct_eight_ranks_on_one_gpu():
+    # Two hardware queues per rank (HIP's default here is 4): 8 ranks x 4 plus the test process's own
+    # can exceed the queues the scheduler keeps mapped at once, and a rank whose queue is swapped out
+    # leaves its peers spinning at the device-side barrier until the next time slice (one box: 50 s
+    # instead of 3 s). Each rank runs one stream, so nothing of its own waits behind the barrier.
     from helpers import BIN
-    r = torchrun(8, ["--no-python", os.path.join(BIN, "reduce_xgmi"), "--mode=vector", "--collective=direct",
+    r = torchrun(8, env={"GPU_MAX_HW_QUEUES": "2"}, script_args=["--no-python", os.path.join(BIN, "reduce_xgmi"), "--mode=vector", "--collective=direct",
                      "--ints=4000037", "--doubles=2000003", "--dtypes=INT,DOUBLE", "--retries=1", "--iters=3",
                      "--direct-grid=16", "--timeout=30", "--graph"], timeout=900)
     assert r.returncode == 0, r.stderr[-4000:]
@@ -459,11 +463,11 @@ def test_bench_replay_probe_and_decomposition_one_gpu(tmp_path):
 
 
 def test_bench_replay_probe_failure_goes_eager_one_gpu(tmp_path):
-    # a probe that misses its deadline (injected 3 s delay vs a 1 s deadline) sends the headline to
+    # a probe that misses its deadline (injected 1.5 s delay vs a 0.5 s deadline) sends the headline to
     # eager issue; it is still measured and verified (rc 0)
     r = run([sys.executable, BENCH, "--no-vector-extras", "--no-candidates", "--steps", "10", "--warmup", "2",
-             "--elements", "50000017", "--collective", "rccl", "--replay-probe", "on", "--probe-deadline", "1",
-             "--inject-fault", "delay=3000@0/capture"], cwd=tmp_path, timeout=600)
+             "--elements", "50000017", "--collective", "rccl", "--replay-probe", "on", "--probe-deadline", "0.5",
+             "--inject-fault", "delay=1500@0/capture"], cwd=tmp_path, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json(r)
     assert d["verified"] is True

@@ -360,3 +360,32 @@ def test_bench_budget_too_small_for_extras_skips_them(tmp_path):
     d = json.loads(lines[0])
     assert d["verified"] is True and "run budget" in d["summary"]["extras_skipped"], d["summary"]
     assert "decomposition" not in json.loads(side.read_text())
+
+
+@pytest.mark.parametrize("fault", [None, "raise@7/selfcheck"])
+def test_bench_rehearsed_stages_at_the_driver_world_of_eight(tmp_path, fault):
+    # The driver's scaling run ends at N=8: the optional headline stages (canary, fused self-check,
+    # per-rank plan tuning) in their CPU form at exactly that world, clean and with the last rank's
+    # self-check raising (every rank falls back to the RCCL-style combine together, the number is
+    # still measured and verified).
+    side = tmp_path / "side8.json"
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "8", "--device", "cpu", "--steps", "3", "--warmup", "1",
+            "--elements", "800009", "--rehearse-stages", "--agree-timeout", "20", "--extras-file", str(side)]
+    if fault:
+        args += ["--inject-fault", fault]
+    r = torchrun(8, args, cwd=tmp_path, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["verified"] is True and d["n_gpus"] == 8 and d["ranks_seen"] == 8
+    full = json.loads(side.read_text())
+    if fault is None:
+        assert d["config"]["collective"] == "fused"
+        assert full["config_detail"]["collective_choice"] == "auto: fused finish passed its self-check on every rank"
+        tuning = full["plan_tuning"]
+        assert len(tuning["gbps_by_rank"]) == 8 and len(tuning["plan_by_rank"]) == 8
+    else:
+        assert d["config"]["collective"] == "rccl"
+        assert "rank 7" in d["config"]["collective_reason"], d["config"]
+        assert "plan_tuning" not in full  # (tuning is for the fused step only)

@@ -262,6 +262,19 @@ def test_from_driver_record_builds_everything(tmp_path):
     assert (out / "figures" / "int.png").stat().st_size > 10000 and (out / "figures" / "double.png").exists()
     assert (out / "vector_direct" / "DOUBLE_SUM.txt").exists()  # reduce.c's own table, N > 1
     assert "decomposition" not in table and "| 3.00 |" in table  # exchange us/step column
+    # the reference's cross-processor conclusion (writeup.tex:19), restated for the measured node
+    assert "writeup.tex:19" in table and "N=8: " in table and "writeup.tex:19" in text
+
+
+def test_bgl_ranks_to_match():
+    # mpi/results/DOUBLE_SUM.txt: 60.9754 GiB/s at 1024 ranks -> 0.059546 GiB/s per rank; one GiB/s of
+    # MI355X needs 1/0.059546 = 16.79 such ranks; the reference's own INT SUM at 1024 ranks matches itself
+    assert abs(scaling.bgl_ranks_to_match(1 / scaling_gib()) - 1024 / 60.9754) < 1e-6
+    assert abs(scaling.bgl_ranks_to_match(146.818 / scaling_gib(), "INT") - 1024) < 1e-6
+
+
+def scaling_gib():
+    return 1e9 / 2 ** 30
 
 
 def test_from_driver_record_refuses_partial_or_unverified_curves(tmp_path):

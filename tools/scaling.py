@@ -384,10 +384,31 @@ def writeup_table(per_n: dict) -> str:
     return "\n".join(rows) + "\n"
 
 
+def bgl_ranks_to_match(gbps: float, dt: str = "DOUBLE", op: str = "SUM", at: int = 1024) -> float:
+    """The reference's cross-processor comparison (writeup.tex:19: BG/L's INT reduction overtakes one
+    2012 GPU at ~500-600 ranks), restated for a measured MI355X number: how many BG/L VN ranks, each
+    at the per-rank rate of the reference's own ``at``-rank run (mpi/results/<DT>_<OP>.txt), would
+    match ``gbps`` (GB/s). Like the reference, this sets an element-wise reduction against a whole-
+    array one: each moves every input byte once."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from reference_data import BGL_VN, GIB_PER_GB
+    per_rank_gibps = BGL_VN[(dt, op)][at] / at
+    return gbps * GIB_PER_GB / per_rank_gibps
+
+
+def crossover_text(per_n: dict) -> str:
+    """One sentence per measured N: the BG/L ranks that would match it (DOUBLE SUM and INT SUM rates)."""
+    parts = [f"N={n}: {bgl_ranks_to_match(v['gbps']):,.0f} (DOUBLE SUM rate) / "
+             f"{bgl_ranks_to_match(v['gbps'], 'INT'):,.0f} (INT SUM rate)" for n, v in sorted(per_n.items())]
+    return ("The reference's cross-processor conclusion (`writeup.tex:19`: BG/L's INT reduction overtakes one "
+            "2012 GPU at ~500-600 ranks), restated: BG/L VN ranks, each at the per-rank rate of the reference's "
+            "1024-rank run, needed to match the measured node — " + "; ".join(parts) + ".\n")
+
+
 WRITEUP_BEGIN, WRITEUP_END = "<!-- scaling:begin -->", "<!-- scaling:end -->"
 
 
-def update_writeup(path: str, table: str, source: str) -> bool:
+def update_writeup(path: str, table: str, source: str, crossover: str = "") -> bool:
     """Replace the text between the scaling markers of docs/WRITEUP.md with the measured table."""
     text = open(path).read()
     if WRITEUP_BEGIN not in text or WRITEUP_END not in text:
@@ -395,7 +416,7 @@ def update_writeup(path: str, table: str, source: str) -> bool:
     head, rest = text.split(WRITEUP_BEGIN, 1)
     _, tail = rest.split(WRITEUP_END, 1)
     body = (f"\nMeasured by the driver's scaling run (`{source}`, via `tools/scaling.py --from`), next to the "
-            "one-GPU projection it replaces:\n\n" + table)
+            "one-GPU projection it replaces:\n\n" + table + ("\n" + crossover if crossover else ""))
     with open(path, "w") as f:
         f.write(head + WRITEUP_BEGIN + body + WRITEUP_END + tail)
     return True
@@ -437,8 +458,11 @@ def from_driver(paths, out_dir: str, require=(1, 2, 4, 8), writeup: "str | None"
     import report
     figs = report.make_figures(os.path.join(out_dir, "figures"), bench_path=paths[0],
                                vector_dir=os.path.join(out_dir, "vector_direct"))
-    updated = update_writeup(writeup, table, ", ".join(os.path.basename(p) for p in paths)) if writeup else False
-    return {"scaling_md": md, "writeup_table": table, "figures": figs, "writeup_updated": updated,
+    cross = crossover_text(per_n)
+    with open(os.path.join(out_dir, "writeup_scaling.md"), "a") as f:
+        f.write("\n" + cross)
+    updated = update_writeup(writeup, table, ", ".join(os.path.basename(p) for p in paths), cross) if writeup else False
+    return {"scaling_md": md, "writeup_table": table, "crossover": cross, "figures": figs, "writeup_updated": updated,
             "vector": sorted(vs)}
 
 
@@ -462,6 +486,7 @@ def main(argv=None):
             return 2
         print(r["scaling_md"], end="")
         print(r["writeup_table"], end="")
+        print(r["crossover"], end="")
         for p in r["figures"]:
             print(p)
         return 0

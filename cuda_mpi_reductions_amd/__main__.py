@@ -12,8 +12,6 @@ cuda_mpi_reductions_amd.ops; verification uses torch's own fp64/int64 reduction.
 from __future__ import annotations
 
 import json
-import math
-import os
 import sys
 
 from .utils import cli

@@ -10,7 +10,6 @@ pairwise (Chan et al.) update after an all-gather of 4 values per rank.
 from __future__ import annotations
 
 import math
-from typing import Optional
 
 import torch
 

@@ -10,7 +10,7 @@ and the CPU references ``sumreduceCPU``/``minreduceCPU``/``maxreduceCPU``
 from __future__ import annotations
 
 import threading
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Optional
 
 import torch

@@ -32,6 +32,9 @@ GPU_FULL_ONLY = {
     # 29 s: a 25 s extras deadline (the extras watchdog is CPU-tested at 2 and 4 ranks,
     # tests/test_fault_injection.py, tests/test_bench_policy.py)
     "test_bench_extras_hang_in_rccl_candidate_keeps_the_headline",
+    # 4 s: examples/06 at world 1 (the default tier runs the same example at three ranks,
+    # test_example_xgmi_collectives_three_ranks_one_gpu, and the world-1 fused finish in test_xrank_gpu.py)
+    "test_example_xgmi_collectives_single",
 }
 # Single cases in the full tier only:
 GPU_FULL_CASES = {
@@ -49,7 +52,8 @@ GPU_FULL_SUBSAMPLE = {
     "test_gpu_full_reduction": 2, "test_fused_world1_matches_torch": 2,
     # subprocess-heavy app sweeps (each case starts ranks)
     "test_reduce_xgmi_direct_peer_reads": 2, "test_reduce_xgmi_direct_tiny_counts": 2,
-    "test_reduce_xgmi_scalar_fused": 2,
+    "test_reduce_xgmi_scalar_fused": 2, "test_reduction_multipass_cputhresh": 2,
+    "test_reduction_app_methods_types": 2,
     "test_bench_ranks_hold_different_plans_and_verify": 3, "test_python_cli_gpu": 2,
     # multi-rank rehearsals by rank count: the default tier keeps the 2-rank case (the 8-rank fused and
     # direct tests cover the wide worlds), and one of maxloc's launch modes

@@ -370,7 +370,8 @@ def test_bench_rehearsed_stages_at_the_driver_world_of_eight(tmp_path, fault):
     # still measured and verified).
     side = tmp_path / "side8.json"
     args = [os.path.join(ROOT, "bench.py"), "--gpus", "8", "--device", "cpu", "--steps", "3", "--warmup", "1",
-            "--elements", "800009", "--rehearse-stages", "--agree-timeout", "20", "--extras-file", str(side)]
+            "--elements", "800009", "--rehearse-stages", "--agree-timeout", "20", "--xrank-timeout", "3",
+            "--extras-file", str(side)]
     if fault:
         args += ["--inject-fault", fault]
     r = torchrun(8, args, cwd=tmp_path, timeout=600)

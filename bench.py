@@ -1349,9 +1349,10 @@ def _tune_plan(wl, ctx, args, fault, kernel, cands) -> "tuple[KernelConfig, dict
     of every rank's table. A candidate whose fan-in flagged an error on any rank is out for every
     rank; if any rank's tuning raised, EVERY rank keeps the tuned default (already bound) and the
     record says why; a rank that died or hangs makes the others raise PeerLost (main() prints the
-    line naming the stage). Only then, with every rank's choice known, are the chosen plans bound
-    (one collective re-bind, skipped when every rank keeps the default); if that re-bind fails
-    anywhere, every rank returns to the default plan. Fault site ``tune`` fires before the
+    line naming the stage). Only then, with every rank's choice known, are the chosen plans bound:
+    each rank re-binds its own lanes, keeping its fused channel (``wl.use_kernel`` is local — no
+    collective; skipped when every rank keeps the default), and one more bounded agreement checks
+    the re-binds: if one failed anywhere, every rank returns to the default plan. Fault site ``tune`` fires before the
     candidates are measured. Returns this rank's kernel config and the record (``chosen`` = rank
     0's plan, ``plan_by_rank`` = every rank's, ``gbps_by_rank`` = every rank's table)."""
     T = max(4, args.tune_steps) if args.tune_steps else _auto_tune_steps(wl.bytes_total / ctx.world_size)
@@ -1414,7 +1415,7 @@ def _tune_plan(wl, ctx, args, fault, kernel, cands) -> "tuple[KernelConfig, dict
         return kernel, rec
     bind_err = None
     try:
-        wl.use_kernel(chosen, streams=1)  # collective: every rank re-binds, each with its own plan
+        wl.use_kernel(chosen, streams=1)  # local: this rank's lanes, its own plan, the same channel
     except Exception as e:  # noqa: BLE001
         bind_err = f"{type(e).__name__}: {e}"[:200]
     bad = [f"rank {r}: {row['error']}" for r, row in

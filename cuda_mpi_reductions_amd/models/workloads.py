@@ -306,9 +306,27 @@ class ScalarReduction:
 
     def use_kernel(self, kernel: KernelConfig, streams: Optional[int] = None) -> None:
         """Re-bind every lane with another streaming-kernel plan (fresh reducers; same data and
-        combine). Collective when the combine is ``fused``."""
+        combine). LOCAL, also with the fused finish: each lane keeps its channel, whose mailboxes,
+        epoch counter and error word belong to the exchange, not to the plan (every rank still makes
+        one fused launch per step, so the epochs stay in step), so ranks may re-plan each on their
+        own and no rank can be left waiting in a collective (bench.py's per-rank plan tuning).
+        Changing the number of lanes goes through :meth:`use_collective` (collective when fused)."""
         self.kernel = kernel
-        self.use_collective(self.collective, streams=streams)
+        n = self.n_streams if streams is None else max(1, int(streams))
+        if self.ctx.device.type != "cuda":
+            return  # CPU ranks reduce on the host: no plan to bind
+        if n != len(self.lanes) or not self.lanes:
+            self.use_collective(self.collective, streams=streams)
+            return
+        dev = self.ctx.device
+        torch.cuda.synchronize(dev)
+        lanes = []
+        for stream, _red, _bound, ch in self.lanes:
+            reducer = Reducer(dev, config=kernel)
+            lanes.append((stream, reducer, reducer.bind(self.x, self.cfg.op, self.acc, out=self._bound_out, xrank=ch), ch))
+        self.lanes, self._local_bound, self._next = lanes, None, 0
+        self.reducer, self.bound = lanes[0][1], lanes[0][2]
+        torch.cuda.synchronize(dev)
 
     @property
     def bytes_total(self) -> int:

@@ -544,3 +544,36 @@ def test_bench_optional_stage_failure_two_ranks_one_gpu(tmp_path, monkeypatch, f
     else:
         assert r.returncode != 0 and d["value"] is None
         assert "plan tuning: rank(s) 1 did not report within 5 s" in d["error"], d
+
+
+def test_use_kernel_rebinds_locally_and_keeps_the_channel():
+    # bench.py binds each rank's tuned plan with ScalarReduction.use_kernel: local (no collective),
+    # the lane keeps its fused channel, whose epoch counter runs on across the re-bind, and the
+    # steps stay exact under the new plan
+    from dataclasses import replace
+    from cuda_mpi_reductions_amd.models import CONFIGS, scalar_workload
+    from cuda_mpi_reductions_amd.ops import KernelConfig
+    from cuda_mpi_reductions_amd.parallel import dist as pdist
+    ctx = pdist.init(backend="gloo", device_type="cuda")  # (the fused finish needs no RCCL)
+    try:
+        cfg = replace(CONFIGS["xgmi_1b_double_sum"], n_total=30_000_017)
+        wl = scalar_workload(cfg, ctx, collective="fused").setup()
+        ch = wl.channels[0]
+        slots = wl.new_slots(6)
+        for i in range(3):
+            wl.step(slots[i:i + 1])
+        torch.cuda.synchronize()
+        assert ch.epoch() == 3
+        plan0 = dict(wl.reducer.last_plan)
+        wl.use_kernel(KernelConfig(block=256, unroll=4, wg_per_cu=2, window=2), streams=1)
+        assert wl.channels[0] is ch and wl.lanes[0][3] is ch
+        assert wl.reducer.last_plan["unroll"] == 4 and wl.reducer.last_plan != plan0
+        for i in range(3, 6):
+            wl.step(slots[i:i + 1])
+        torch.cuda.synchronize()
+        assert ch.epoch() == 6 and ch.error() == 0 and wl.error_counts() == [0, 0, 0, 0]
+        ref = wl.x.sum(dtype=torch.float64).item()
+        for v in slots.cpu().tolist():
+            assert abs(v - ref) <= 1e-9 * abs(ref), (v, ref)
+    finally:
+        pdist.shutdown(ctx)

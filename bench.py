@@ -874,8 +874,10 @@ def _try_fused(wl, ctx, args, fault, at_stage=lambda name: None) -> "str | None"
       (parallel/canary.py) — a fault of the peer mapping there cannot take this process, and the
       headline, down with it; the helpers' verdicts are agreed through a bounded store exchange;
     * channel setup: collective by construction (``open_channel`` raises on every rank together);
-    * ``fused self-check``: 3 fused steps, this rank's error words and the same kernel's partial
-      without a channel — all LOCAL, inside a try — then one bounded agreement
+    * ``fused self-check``: one bounded agreement that every rank is ready (a rank that failed
+      before launching makes every rank fall back at once, not after a peer's fused step waited
+      --xrank-timeout for it); then 3 fused steps, this rank's error words and the same kernel's
+      partial without a channel — all LOCAL, inside a try — then one bounded agreement
       (:func:`parallel.dist.agree`) of every rank's report, from which every rank derives the same
       verdict. A rank whose part raised reports the error; one that died or hangs makes the others
       raise :class:`parallel.dist.PeerLost` (main() prints the diagnostic line naming the stage)
@@ -898,16 +900,29 @@ def _try_fused(wl, ctx, args, fault, at_stage=lambda name: None) -> "str | None"
         wl.use_collective("rccl", streams=1)
         return f"setup: {e}"[:300]
     mine = {"error": None}
+
+    def failed_here(e: Exception) -> None:
+        mine["error"] = f"{type(e).__name__}: {e}"[:200]
+        print(f"[bench] rank {ctx.rank}: fused self-check failed here: {mine['error']}", file=sys.stderr, flush=True)
     try:
         fault.at(ctx.rank, fault.spec.step, "selfcheck", "fused self-check")
         slots = wl.new_slots(3)
+    except Exception as e:  # noqa: BLE001 - this rank's report carries it; every rank falls back together
+        failed_here(e)
+    # Every rank ready before any fused launch: a rank that failed before its steps would otherwise
+    # leave the others' first fused step waiting --xrank-timeout in the kernel for its partial.
+    ready = pdist.agree(ctx, "fused self-check", {"error": mine["error"]}, _agree_timeout(args))
+    errs = [f"rank {r}: {row['error']}" for r, row in enumerate(ready) if row.get("error")]
+    if errs:
+        wl.use_collective("rccl", streams=1)
+        return ("self-check: " + "; ".join(errs))[:300]
+    try:
         for i in range(3):
             wl.step(slots[i:i + 1])
         mine.update(_selfcheck_report(wl, slots))
-    except Exception as e:  # noqa: BLE001 - this rank's report carries it; every rank falls back together
-        mine["error"] = f"{type(e).__name__}: {e}"[:200]
-        print(f"[bench] rank {ctx.rank}: fused self-check failed here: {mine['error']}", file=sys.stderr, flush=True)
-    # (a rank that failed before its steps makes the others' first fused step wait --xrank-timeout)
+    except Exception as e:  # noqa: BLE001 - as above
+        failed_here(e)
+    # (a rank that fails during its steps still makes the others' fused steps wait --xrank-timeout)
     rows = pdist.agree(ctx, "fused self-check", mine, _agree_timeout(args, args.xrank_timeout + 10.0))
     if (mine.get("counts") or [0])[0]:
         wl.reset_fanin()  # this rank's sticky fan-in error was reported: clear it

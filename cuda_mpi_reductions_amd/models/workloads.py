@@ -310,7 +310,9 @@ class ScalarReduction:
         epoch counter and error word belong to the exchange, not to the plan (every rank still makes
         one fused launch per step, so the epochs stay in step), so ranks may re-plan each on their
         own and no rank can be left waiting in a collective (bench.py's per-rank plan tuning).
-        Changing the number of lanes goes through :meth:`use_collective` (collective when fused)."""
+        Changing the number of lanes goes through :meth:`use_collective` (collective when fused).
+        As with :meth:`use_collective`, graphs captured from the old lanes must not be replayed after
+        it (their workspaces are released)."""
         self.kernel = kernel
         n = self.n_streams if streams is None else max(1, int(streams))
         if self.ctx.device.type != "cuda":

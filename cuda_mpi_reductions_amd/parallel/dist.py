@@ -241,10 +241,12 @@ def agree(ctx: DistContext, stage: str, payload: dict, timeout_s: float = 60.0) 
     except Exception:  # noqa: BLE001 - a store timeout (DistStoreError / RuntimeError): find who is missing
         missing = []
         for r, k in enumerate(keys):
+            if r == ctx.rank:
+                continue  # (this rank's own report was set above)
             try:
                 if not store.check([k]):
                     missing.append(r)
-            except Exception:  # noqa: BLE001 - the store itself is gone (its host rank died)
+            except Exception:  # noqa: BLE001 - the store itself is gone (its host, rank 0, died)
                 missing.append(r)
         if missing:
             raise PeerLost(stage, missing, timeout_s) from None
